@@ -1,0 +1,610 @@
+// C-ABI implementation (include/dcfm.h): handle, HBM allocation, layout
+// conversion between the reference's MATLAB column-major arrays and the
+// device layout (dcfm_internal.h), the per-iteration launch sequence of the hot
+// loop (divideconquer.m:90-197) and the RCCL exchanges over xGMI.
+#include "../../include/dcfm.h"
+#include "dcfm_internal.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace dcfm;
+
+namespace {
+
+struct ProfRec { int kid; hipEvent_t a, b; };
+
+}  // namespace
+
+struct dcfm_handle {
+    dcfm_config cfg{};
+    Dims d{};
+    Bufs b{};
+    DrawsDev dr{};
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    bool comm_ok = false;
+    int cur = 0;                  // delta/tau buffer in use
+    int B = 16;                   // saved samples per flush
+    int batch = 0;                // saved samples pending in Lb
+    int64_t saved = 0;
+    bool have_data = false, have_state = false;
+    std::string err;
+    std::vector<void *> allocs;
+    double *draws_mem = nullptr;
+    bool prof = false;
+    std::vector<ProfRec> recs;
+    std::vector<hipEvent_t> evpool;
+    double kms[DCFM_K_COUNT] = {};
+    int64_t kcnt[DCFM_K_COUNT] = {};
+};
+
+static std::string g_err;  // errors without a handle
+
+static int fail(dcfm_handle *h, int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (h) h->err = buf; else g_err = buf;
+    return code;
+}
+
+#define HIPC(h, x)                                                                        \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess)                                                             \
+            return fail(h, DCFM_ERR_HIP, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                              \
+    } while (0)
+
+#define NCCLC(h, x)                                                                       \
+    do {                                                                                  \
+        ncclResult_t r_ = (x);                                                            \
+        if (r_ != ncclSuccess)                                                            \
+            return fail(h, DCFM_ERR_RCCL, "%s failed: %s", #x, ncclGetErrorString(r_));   \
+    } while (0)
+
+static int dalloc(dcfm_handle *h, double **p, size_t n) {
+    void *q = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc(&q, n * sizeof(double));
+    if (e != hipSuccess)
+        return fail(h, DCFM_ERR_ALLOC, "hipMalloc(%zu doubles) failed: %s", n, hipGetErrorString(e));
+    e = hipMemset(q, 0, n * sizeof(double));
+    if (e != hipSuccess) return fail(h, DCFM_ERR_HIP, "hipMemset failed: %s", hipGetErrorString(e));
+    h->allocs.push_back(q);
+    *p = static_cast<double *>(q);
+    return DCFM_OK;
+}
+
+static int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+// ---------------------------------------------------------------------------
+// profiling helpers
+// ---------------------------------------------------------------------------
+static hipEvent_t get_event(dcfm_handle *h) {
+    if (!h->evpool.empty()) {
+        hipEvent_t e = h->evpool.back();
+        h->evpool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+struct KTimer {
+    dcfm_handle *h;
+    int kid;
+    hipEvent_t a = nullptr;
+    KTimer(dcfm_handle *h_, int k) : h(h_), kid(k) {
+        if (h->prof) {
+            a = get_event(h);
+            if (a) (void)hipEventRecord(a, h->stream);
+        }
+    }
+    ~KTimer() {
+        if (h->prof && a) {
+            hipEvent_t b = get_event(h);
+            if (b) {
+                (void)hipEventRecord(b, h->stream);
+                h->recs.push_back({kid, a, b});
+            }
+        }
+    }
+};
+
+static void collect_prof(dcfm_handle *h) {
+    if (h->recs.empty()) return;
+    (void)hipStreamSynchronize(h->stream);
+    for (auto &r : h->recs) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            h->kms[r.kid] += ms;
+            h->kcnt[r.kid] += 1;
+        }
+        h->evpool.push_back(r.a);
+        h->evpool.push_back(r.b);
+    }
+    h->recs.clear();
+}
+
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int dcfm_abi_version(void) { return DCFM_ABI_VERSION; }
+
+const char *dcfm_last_error(const dcfm_handle *h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+const char *dcfm_kernel_name(int id) {
+    static const char *names[DCFM_K_COUNT] = {"k_prep",  "k_wpass", "k_zdraw",  "k_xred",
+                                              "k_xdraw", "k_cpass", "k_lambda", "k_colsum",
+                                              "k_delta", "k_save",  "k_assemble", "rccl"};
+    return (id >= 0 && id < DCFM_K_COUNT) ? names[id] : "?";
+}
+
+int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
+    if (!cfg || !out) return fail(nullptr, DCFM_ERR_INVALID, "null argument");
+    *out = nullptr;
+    const dcfm_config &c = *cfg;
+    if (c.n < 1 || c.P < 1 || c.g < 1 || c.K < 1)
+        return fail(nullptr, DCFM_ERR_INVALID, "n, P, g, K must be >= 1");
+    if (c.K > KP)
+        return fail(nullptr, DCFM_ERR_UNSUPPORTED, "K = %d > %d not supported by this build", c.K, KP);
+    if (!(c.rho >= 0.0 && c.rho <= 1.0)) return fail(nullptr, DCFM_ERR_INVALID, "rho must be in [0,1]");
+    if (c.thin < 1 || c.mcmc < 0 || c.burnin < 0)
+        return fail(nullptr, DCFM_ERR_INVALID, "thin >= 1, mcmc >= 0, burnin >= 0 required");
+    const int nranks = c.nranks < 1 ? 1 : c.nranks;
+    if (c.rank < 0 || c.rank >= nranks) return fail(nullptr, DCFM_ERR_INVALID, "bad rank");
+    if (c.g % nranks)
+        return fail(nullptr, DCFM_ERR_UNSUPPORTED, "g = %d not divisible by nranks = %d", c.g, nranks);
+    if ((int64_t)c.P * c.g > 2000000000LL / 1) {}
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev < 1)
+        return fail(nullptr, DCFM_ERR_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+    if (c.device < 0 || c.device >= ndev) return fail(nullptr, DCFM_ERR_INVALID, "bad device %d", c.device);
+
+    dcfm_handle *h = new dcfm_handle();
+    h->cfg = c;
+    h->cfg.nranks = nranks;
+    HIPC(h, hipSetDevice(c.device));
+    HIPC(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+
+    Dims &d = h->d;
+    d.n = c.n; d.P = c.P; d.g = c.g; d.K = c.K;
+    d.nranks = nranks; d.rank = c.rank;
+    d.G = c.g / nranks;
+    d.shard0 = c.rank * d.G;
+    d.NP = round_up(c.n, 16);
+    d.PP = round_up(c.P, 16);
+    d.p = c.P * c.g;
+    d.rho = c.rho; d.sr = std::sqrt(c.rho); d.s1r = std::sqrt(1.0 - c.rho);
+    d.as_ = c.as_; d.bs = c.bs; d.df = c.df; d.ad1 = c.ad1; d.bd1 = c.bd1; d.ad2 = c.ad2; d.bd2 = c.bd2;
+    d.seed = c.seed;
+    d.inject = (c.flags & DCFM_FLAG_INJECT_DRAWS) ? 1 : 0;
+    h->B = c.asm_batch > 0 ? c.asm_batch : 16;
+
+    Bufs &b = h->b;
+    const size_t G = d.G, NP = d.NP, PP = d.PP, g = d.g, p = d.p;
+    b.LDB = round_up(h->B * d.K, 16);
+    int rc = DCFM_OK;
+#define ALLOC(ptr, n) if ((rc = dalloc(h, &(ptr), (n))) != DCFM_OK) { int r2 = rc; std::string m = h->err; dcfm_destroy(h); g_err = m; return r2; }
+    ALLOC(b.Y, G * NP * PP);
+    ALLOC(b.yy, G * PP);
+    ALLOC(b.Lam, G * PP * KP);
+    ALLOC(b.omega, G * PP);
+    ALLOC(b.ps, G * PP);
+    ALLOC(b.psi, G * PP * KP);
+    ALLOC(b.Plam, G * PP * KP);
+    ALLOC(b.X, NP * KP);
+    ALLOC(b.Z, G * NP * KP);
+    ALLOC(b.delta, 2 * g * KP);
+    ALLOC(b.tau, 2 * g * KP);
+    ALLOC(b.W, G * NP * KP);
+    ALLOC(b.A, G * KP * KP);
+    ALLOC(b.R, G * KP * KP);
+    ALLOC(b.Rdi, G * KP);
+    ALLOC(b.Sp, ((G + 3) / 4) * NP * KP);
+    ALLOC(b.xin, (NP + KP) * KP);
+    if (nranks > 1) { ALLOC(b.xall, (size_t)nranks * (NP + KP) * KP); } else b.xall = b.xin;
+    ALLOC(b.C, G * PP * KP);
+    ALLOC(b.E, G * KP * KP);
+    ALLOC(b.cpart, G * (PP / 8) * KP);
+    ALLOC(b.sloc, G * KP);
+    if (nranks > 1) { ALLOC(b.sall, g * KP); } else b.sall = b.sloc;
+    ALLOC(b.Lb, p * (size_t)b.LDB);
+    ALLOC(b.wsum, p);
+    ALLOC(b.Sigma, p * p);
+#undef ALLOC
+    // lower-triangle assembly tiles, dealt round-robin over ranks
+    {
+        const int nt = (d.p + ASM_TILE - 1) / ASM_TILE;
+        std::vector<int2> tl;
+        int64_t idx = 0;
+        for (int ti = 0; ti < nt; ++ti)
+            for (int tj = 0; tj <= ti; ++tj, ++idx)
+                if (idx % nranks == c.rank) tl.push_back(make_int2(ti, tj));
+        b.ntiles = (int)tl.size();
+        void *q = nullptr;
+        HIPC(h, hipMalloc(&q, std::max<size_t>(1, tl.size()) * sizeof(int2)));
+        h->allocs.push_back(q);
+        b.tiles = static_cast<int2 *>(q);
+        if (!tl.empty()) HIPC(h, hipMemcpy(b.tiles, tl.data(), tl.size() * sizeof(int2), hipMemcpyHostToDevice));
+    }
+    // pad delta/tau with ones
+    {
+        std::vector<double> ones(2 * g * KP, 1.0);
+        HIPC(h, hipMemcpy(b.delta, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice));
+        HIPC(h, hipMemcpy(b.tau, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    *out = h;
+    return DCFM_OK;
+}
+
+void dcfm_destroy(dcfm_handle *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->cfg.device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (auto &r : h->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    for (auto e : h->evpool) (void)hipEventDestroy(e);
+    if (h->comm) ncclCommDestroy(h->comm);
+    for (void *q : h->allocs) (void)hipFree(q);
+    if (h->draws_mem) (void)hipFree(h->draws_mem);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int dcfm_comm_unique_id(uint8_t out[128]) {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(nullptr, DCFM_ERR_RCCL, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+    std::memcpy(out, &id, 128);
+    return DCFM_OK;
+}
+
+int dcfm_comm_init(dcfm_handle *h, const uint8_t id[128]) {
+    if (!h || !id) return fail(h, DCFM_ERR_INVALID, "null argument");
+    if (h->d.nranks == 1) return DCFM_OK;
+    HIPC(h, hipSetDevice(h->cfg.device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    NCCLC(h, ncclCommInitRank(&h->comm, h->d.nranks, uid, h->d.rank));
+    h->comm_ok = true;
+    return DCFM_OK;
+}
+
+// Yd local: n x P x G column-major: (i, j, m) at i + n*j + n*P*m  ->  Y[m][i][j]
+int dcfm_set_data(dcfm_handle *h, const double *Yd) {
+    if (!h || !Yd) return fail(h, DCFM_ERR_INVALID, "null argument");
+    const Dims &d = h->d;
+    HIPC(h, hipSetDevice(h->cfg.device));
+    std::vector<double> buf((size_t)d.NP * d.PP, 0.0);
+    std::vector<double> yy((size_t)d.G * d.PP, 0.0);
+    for (int m = 0; m < d.G; ++m) {
+        std::fill(buf.begin(), buf.end(), 0.0);
+        const double *src = Yd + (size_t)m * d.n * d.P;
+        for (int j = 0; j < d.P; ++j) {
+            double s = 0.0;
+            for (int i = 0; i < d.n; ++i) {
+                const double v = src[(size_t)j * d.n + i];
+                buf[(size_t)i * d.PP + j] = v;
+                s += v * v;
+            }
+            yy[(size_t)m * d.PP + j] = s;
+        }
+        HIPC(h, hipMemcpy(h->b.Y + (size_t)m * d.NP * d.PP, buf.data(), buf.size() * sizeof(double),
+                          hipMemcpyHostToDevice));
+    }
+    HIPC(h, hipMemcpy(h->b.yy, yy.data(), yy.size() * sizeof(double), hipMemcpyHostToDevice));
+    h->have_data = true;
+    return DCFM_OK;
+}
+
+// P x K x G col-major (j,k,m) at j + P*k + P*K*m  <->  dev [m][j][k] (PP x KP)
+static void pk_to_dev(const Dims &d, const double *src, std::vector<double> &dst) {
+    dst.assign((size_t)d.G * d.PP * KP, 0.0);
+    for (int m = 0; m < d.G; ++m)
+        for (int k = 0; k < d.K; ++k)
+            for (int j = 0; j < d.P; ++j)
+                dst[((size_t)m * d.PP + j) * KP + k] = src[(size_t)j + (size_t)d.P * k + (size_t)d.P * d.K * m];
+}
+static void pk_from_dev(const Dims &d, const std::vector<double> &src, double *dst) {
+    for (int m = 0; m < d.G; ++m)
+        for (int k = 0; k < d.K; ++k)
+            for (int j = 0; j < d.P; ++j)
+                dst[(size_t)j + (size_t)d.P * k + (size_t)d.P * d.K * m] = src[((size_t)m * d.PP + j) * KP + k];
+}
+// n x K x G col-major (i,k,m) <-> dev [m][i][k] (NP x KP)
+static void nk_to_dev(const Dims &d, const double *src, int G, std::vector<double> &dst) {
+    dst.assign((size_t)G * d.NP * KP, 0.0);
+    for (int m = 0; m < G; ++m)
+        for (int k = 0; k < d.K; ++k)
+            for (int i = 0; i < d.n; ++i)
+                dst[((size_t)m * d.NP + i) * KP + k] = src[(size_t)i + (size_t)d.n * k + (size_t)d.n * d.K * m];
+}
+static void nk_from_dev(const Dims &d, const std::vector<double> &src, int G, double *dst) {
+    for (int m = 0; m < G; ++m)
+        for (int k = 0; k < d.K; ++k)
+            for (int i = 0; i < d.n; ++i)
+                dst[(size_t)i + (size_t)d.n * k + (size_t)d.n * d.K * m] = src[((size_t)m * d.NP + i) * KP + k];
+}
+// P x G col-major (j,m) <-> dev [m][j] (PP)
+static void p_to_dev(const Dims &d, const double *src, std::vector<double> &dst) {
+    dst.assign((size_t)d.G * d.PP, 0.0);
+    for (int m = 0; m < d.G; ++m)
+        for (int j = 0; j < d.P; ++j) dst[(size_t)m * d.PP + j] = src[(size_t)j + (size_t)d.P * m];
+}
+static void p_from_dev(const Dims &d, const std::vector<double> &src, double *dst) {
+    for (int m = 0; m < d.G; ++m)
+        for (int j = 0; j < d.P; ++j) dst[(size_t)j + (size_t)d.P * m] = src[(size_t)m * d.PP + j];
+}
+// K x 1 x g col-major (k,m) <-> dev [m][k] (KP), pads 1
+static void k_to_dev(const Dims &d, const double *src, std::vector<double> &dst) {
+    dst.assign((size_t)d.g * KP, 1.0);
+    for (int m = 0; m < d.g; ++m)
+        for (int k = 0; k < d.K; ++k) dst[(size_t)m * KP + k] = src[(size_t)k + (size_t)d.K * m];
+}
+static void k_from_dev(const Dims &d, const std::vector<double> &src, double *dst) {
+    for (int m = 0; m < d.g; ++m)
+        for (int k = 0; k < d.K; ++k) dst[(size_t)k + (size_t)d.K * m] = src[(size_t)m * KP + k];
+}
+
+static int up(dcfm_handle *h, double *dev, const std::vector<double> &v) {
+    HIPC(h, hipMemcpy(dev, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice));
+    return DCFM_OK;
+}
+static int down(dcfm_handle *h, std::vector<double> &v, const double *dev, size_t n) {
+    v.resize(n);
+    HIPC(h, hipMemcpy(v.data(), dev, n * sizeof(double), hipMemcpyDeviceToHost));
+    return DCFM_OK;
+}
+
+int dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s) {
+    if (!h || !s) return fail(h, DCFM_ERR_INVALID, "null argument");
+    if (!s->Lambda || !s->ps || !s->omega || !s->psi || !s->Plam || !s->X || !s->Z || !s->delta || !s->tauh)
+        return fail(h, DCFM_ERR_INVALID, "set_state: every member except eta is required");
+    const Dims &d = h->d;
+    HIPC(h, hipSetDevice(h->cfg.device));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    std::vector<double> v;
+    int rc;
+    pk_to_dev(d, s->Lambda, v); if ((rc = up(h, h->b.Lam, v))) return rc;
+    pk_to_dev(d, s->psi, v);    if ((rc = up(h, h->b.psi, v))) return rc;
+    pk_to_dev(d, s->Plam, v);   if ((rc = up(h, h->b.Plam, v))) return rc;
+    p_to_dev(d, s->ps, v);      if ((rc = up(h, h->b.ps, v))) return rc;
+    p_to_dev(d, s->omega, v);   if ((rc = up(h, h->b.omega, v))) return rc;
+    nk_to_dev(d, s->X, 1, v);   if ((rc = up(h, h->b.X, v))) return rc;
+    nk_to_dev(d, s->Z, d.G, v); if ((rc = up(h, h->b.Z, v))) return rc;
+    h->cur = 0;
+    k_to_dev(d, s->delta, v);   if ((rc = up(h, h->b.delta, v))) return rc;
+    k_to_dev(d, s->tauh, v);    if ((rc = up(h, h->b.tau, v))) return rc;
+    h->have_state = true;
+    return DCFM_OK;
+}
+
+int dcfm_get_state(dcfm_handle *h, dcfm_state_view *o) {
+    if (!h || !o) return fail(h, DCFM_ERR_INVALID, "null argument");
+    const Dims &d = h->d;
+    HIPC(h, hipSetDevice(h->cfg.device));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    std::vector<double> v;
+    int rc;
+    const size_t npk = (size_t)d.G * d.PP * KP, nnk = (size_t)d.G * d.NP * KP;
+    if (o->Lambda) { if ((rc = down(h, v, h->b.Lam, npk))) return rc; pk_from_dev(d, v, o->Lambda); }
+    if (o->psi) { if ((rc = down(h, v, h->b.psi, npk))) return rc; pk_from_dev(d, v, o->psi); }
+    if (o->Plam) { if ((rc = down(h, v, h->b.Plam, npk))) return rc; pk_from_dev(d, v, o->Plam); }
+    if (o->ps) { if ((rc = down(h, v, h->b.ps, (size_t)d.G * d.PP))) return rc; p_from_dev(d, v, o->ps); }
+    if (o->omega) { if ((rc = down(h, v, h->b.omega, (size_t)d.G * d.PP))) return rc; p_from_dev(d, v, o->omega); }
+    if (o->X) { if ((rc = down(h, v, h->b.X, (size_t)d.NP * KP))) return rc; nk_from_dev(d, v, 1, o->X); }
+    if (o->Z) { if ((rc = down(h, v, h->b.Z, nnk))) return rc; nk_from_dev(d, v, d.G, o->Z); }
+    if (o->eta) {
+        launch_eta(d, h->b, h->b.W, h->stream);   // W is scratch between iterations
+        HIPC(h, hipGetLastError());
+        HIPC(h, hipStreamSynchronize(h->stream));
+        if ((rc = down(h, v, h->b.W, nnk))) return rc;
+        nk_from_dev(d, v, d.G, o->eta);
+    }
+    const size_t nkg = (size_t)d.g * KP;
+    if (o->delta) { if ((rc = down(h, v, h->b.delta + h->cur * nkg, nkg))) return rc; k_from_dev(d, v, o->delta); }
+    if (o->tauh) { if ((rc = down(h, v, h->b.tau + h->cur * nkg, nkg))) return rc; k_from_dev(d, v, o->tauh); }
+    return DCFM_OK;
+}
+
+int dcfm_set_draws(dcfm_handle *h, const dcfm_draws_view *dv, int64_t first_iter, int64_t n_iter) {
+    if (!h || !dv || n_iter < 1) return fail(h, DCFM_ERR_INVALID, "bad argument");
+    if (!dv->NZ || !dv->NX || !dv->NL || !dv->Gpsi || !dv->Gdelta || !dv->Gps)
+        return fail(h, DCFM_ERR_INVALID, "set_draws: all six arrays required");
+    const Dims &d = h->d;
+    HIPC(h, hipSetDevice(h->cfg.device));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    const size_t T = n_iter;
+    const size_t nNZ = (size_t)d.K * d.n * d.g * T, nNX = (size_t)d.K * d.n * T,
+                 nNL = (size_t)d.K * d.P * d.g * T, nPsi = (size_t)d.P * d.K * d.g * T,
+                 nDel = (size_t)d.K * d.g * T, nPs = (size_t)d.P * d.g * T;
+    const size_t tot = nNZ + nNX + nNL + nPsi + nDel + nPs;
+    if (h->draws_mem) { (void)hipFree(h->draws_mem); h->draws_mem = nullptr; }
+    void *q = nullptr;
+    HIPC(h, hipMalloc(&q, tot * sizeof(double)));
+    h->draws_mem = static_cast<double *>(q);
+    double *p = h->draws_mem;
+    const double *srcs[6] = {dv->NZ, dv->NX, dv->NL, dv->Gpsi, dv->Gdelta, dv->Gps};
+    const size_t cnt[6] = {nNZ, nNX, nNL, nPsi, nDel, nPs};
+    const double **dsts[6] = {&h->dr.NZ, &h->dr.NX, &h->dr.NL, &h->dr.Gpsi, &h->dr.Gdelta, &h->dr.Gps};
+    for (int k = 0; k < 6; ++k) {
+        HIPC(h, hipMemcpy(p, srcs[k], cnt[k] * sizeof(double), hipMemcpyHostToDevice));
+        *dsts[k] = p;
+        p += cnt[k];
+    }
+    h->dr.first_iter = first_iter;
+    h->dr.n_iter = n_iter;
+    return DCFM_OK;
+}
+
+static int flush_batch(dcfm_handle *h) {
+    if (h->batch == 0) return DCFM_OK;
+    Dims &d = h->d;
+    Bufs &b = h->b;
+    if (d.nranks > 1) {
+        KTimer t(h, DCFM_K_COMM);
+        const size_t rows = (size_t)d.G * d.P;
+        NCCLC(h, ncclGroupStart());
+        NCCLC(h, ncclAllGather(b.Lb + (size_t)d.rank * rows * b.LDB, b.Lb, rows * b.LDB, ncclDouble, h->comm, h->stream));
+        NCCLC(h, ncclAllGather(b.wsum + (size_t)d.rank * rows, b.wsum, rows, ncclDouble, h->comm, h->stream));
+        NCCLC(h, ncclGroupEnd());
+    }
+    const int kext = round_up(h->batch * d.K, 8);
+    const double effsamp = (double)h->cfg.mcmc / (double)h->cfg.thin;   // dc:45 (Q8)
+    {
+        KTimer t(h, DCFM_K_ASSEMBLE);
+        launch_assemble(d, b, kext, 1.0 / effsamp, h->stream);
+    }
+    HIPC(h, hipGetLastError());
+    HIPC(h, hipMemsetAsync(b.Lb, 0, (size_t)d.p * b.LDB * sizeof(double), h->stream));
+    HIPC(h, hipMemsetAsync(b.wsum, 0, (size_t)d.p * sizeof(double), h->stream));
+    h->batch = 0;
+    return DCFM_OK;
+}
+
+int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
+    if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
+    if (!h->have_data || !h->have_state) return fail(h, DCFM_ERR_INVALID, "set_data and set_state first");
+    if (first_iter < 1 || n_iter < 0) return fail(h, DCFM_ERR_INVALID, "iterations are 1-based");
+    Dims &d = h->d;
+    Bufs &b = h->b;
+    if (d.nranks > 1 && !h->comm_ok) return fail(h, DCFM_ERR_INVALID, "dcfm_comm_init first (nranks > 1)");
+    if (d.inject) {
+        if (!h->dr.NZ) return fail(h, DCFM_ERR_INVALID, "INJECT_DRAWS set but no draws");
+        if (first_iter < h->dr.first_iter || first_iter + n_iter > h->dr.first_iter + h->dr.n_iter)
+            return fail(h, DCFM_ERR_INVALID, "iterations [%lld,%lld) not covered by injected draws",
+                        (long long)first_iter, (long long)(first_iter + n_iter));
+    }
+    HIPC(h, hipSetDevice(h->cfg.device));
+    hipStream_t s = h->stream;
+    const size_t nkg = (size_t)d.g * KP;
+    for (int64_t it = first_iter; it < first_iter + n_iter; ++it) {
+        { KTimer t(h, DCFM_K_PREP);   launch_prep(d, b, s); }
+        { KTimer t(h, DCFM_K_WPASS);  launch_wpass(d, b, s); }
+        { KTimer t(h, DCFM_K_ZDRAW);  launch_zdraw(d, b, h->dr, it, s); }
+        { KTimer t(h, DCFM_K_XRED);   launch_xred(d, b, s); }
+        if (d.nranks > 1) {
+            KTimer t(h, DCFM_K_COMM);
+            NCCLC(h, ncclAllGather(b.xin, b.xall, (size_t)(d.NP + KP) * KP, ncclDouble, h->comm, s));
+        }
+        { KTimer t(h, DCFM_K_XDRAW);  launch_xdraw(d, b, h->dr, it, s); }
+        { KTimer t(h, DCFM_K_CPASS);  launch_cpass(d, b, s); }
+        { KTimer t(h, DCFM_K_LAMBDA); launch_lambda(d, b, h->dr, it, b.tau + h->cur * nkg, s); }
+        { KTimer t(h, DCFM_K_COLSUM); launch_colsum(d, b, s); }
+        if (d.nranks > 1) {
+            KTimer t(h, DCFM_K_COMM);
+            NCCLC(h, ncclAllGather(b.sloc, b.sall, (size_t)d.G * KP, ncclDouble, h->comm, s));
+        }
+        {
+            KTimer t(h, DCFM_K_DELTA);
+            launch_delta(d, b, h->dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+                         b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);
+        }
+        h->cur ^= 1;
+        HIPC(h, hipGetLastError());
+        if (it % h->cfg.thin == 0 && it > h->cfg.burnin) {                // dc:180
+            { KTimer t(h, DCFM_K_SAVE); launch_save(d, b, h->batch, s); }
+            HIPC(h, hipGetLastError());
+            h->batch += 1;
+            h->saved += 1;
+            if (h->batch == h->B) {
+                int rc = flush_batch(h);
+                if (rc) return rc;
+            }
+        }
+    }
+    int rc = flush_batch(h);
+    if (rc) return rc;
+    if (h->prof) collect_prof(h);
+    return DCFM_OK;
+}
+
+int dcfm_synchronize(dcfm_handle *h) {
+    if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
+    HIPC(h, hipSetDevice(h->cfg.device));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    return DCFM_OK;
+}
+
+int64_t dcfm_saved_samples(const dcfm_handle *h) { return h ? h->saved : -1; }
+
+int dcfm_get_sigma(dcfm_handle *h, double *out) {
+    if (!h || !out) return fail(h, DCFM_ERR_INVALID, "null argument");
+    Dims &d = h->d;
+    HIPC(h, hipSetDevice(h->cfg.device));
+    const size_t pp = (size_t)d.p * d.p;
+    double *tmp = nullptr;
+    void *q = nullptr;
+    HIPC(h, hipMalloc(&q, pp * sizeof(double)));
+    tmp = static_cast<double *>(q);
+    int rc = DCFM_OK;
+    if (d.nranks > 1) {
+        ncclResult_t r = ncclAllReduce(h->b.Sigma, tmp, pp, ncclDouble, ncclSum, h->comm, h->stream);
+        if (r != ncclSuccess) rc = fail(h, DCFM_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+    } else {
+        hipError_t e = hipMemcpyAsync(tmp, h->b.Sigma, pp * sizeof(double), hipMemcpyDeviceToDevice, h->stream);
+        if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "hipMemcpyAsync: %s", hipGetErrorString(e));
+    }
+    if (rc == DCFM_OK) {
+        launch_mirror(tmp, d.p, h->stream);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(out, tmp, pp * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "get_sigma: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(tmp);
+    return rc;
+}
+
+int dcfm_set_profiling(dcfm_handle *h, int enable) {
+    if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
+    h->prof = enable != 0;
+    if (enable) {
+        std::fill(h->kms, h->kms + DCFM_K_COUNT, 0.0);
+        std::fill(h->kcnt, h->kcnt + DCFM_K_COUNT, 0);
+    }
+    return DCFM_OK;
+}
+
+int dcfm_get_kernel_stats(dcfm_handle *h, double ms[DCFM_K_COUNT], int64_t launches[DCFM_K_COUNT]) {
+    if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
+    collect_prof(h);
+    for (int k = 0; k < DCFM_K_COUNT; ++k) {
+        if (ms) ms[k] = h->kms[k];
+        if (launches) launches[k] = h->kcnt[k];
+    }
+    return DCFM_OK;
+}
+
+int dcfm_rng_fill(int device, uint64_t seed, int kind, double shape, int32_t site, int32_t shard,
+                  int64_t iter, int64_t count, double *out) {
+    if (!out || count < 0 || (kind != 0 && kind != 1) || (kind == 1 && !(shape >= 1.0)))
+        return fail(nullptr, DCFM_ERR_INVALID, "rng_fill: bad argument");
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return fail(nullptr, DCFM_ERR_HIP, "hipSetDevice: %s", hipGetErrorString(e));
+    void *q = nullptr;
+    e = hipMalloc(&q, std::max<int64_t>(count, 1) * sizeof(double));
+    if (e != hipSuccess) return fail(nullptr, DCFM_ERR_ALLOC, "hipMalloc: %s", hipGetErrorString(e));
+    launch_rng_fill(seed, kind, shape, site, shard, iter, count, static_cast<double *>(q), nullptr);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(out, q, count * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(q);
+    if (e != hipSuccess) return fail(nullptr, DCFM_ERR_HIP, "rng_fill: %s", hipGetErrorString(e));
+    return DCFM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,78 @@
+// Internal layout + kernel launch declarations for libdcfm (MI355X / gfx950).
+//
+// HBM layout (C order, last index fastest), G = local shards, mg = global shard:
+//   Y      [G][NP][PP]   standardised data, rows i padded to NP (x16), cols j to PP (x16), zeros
+//   yy     [G][PP]       sum_i Y_ij^2 (set_data)                -> residual SS identity
+//   Lam    [G][PP][KP]   loadings, k padded to KP = 32 with zeros
+//   omega  [G][PP]       diag(Omega);   ps [G][PP]
+//   psi    [G][PP][KP];  Plam [G][PP][KP]
+//   X      [NP][KP]      replicated;    Z [G][NP][KP]
+//   delta, tau [2][g][KP] replicated on every rank, double-buffered per iteration
+//   W      [G][NP][KP]   W_m = Y_m (omega o Lambda_m)                    (k_wpass)
+//   A      [G][KP][KP]   A_m = Lambda_m' diag(omega) Lambda_m             (k_prep)
+//   R      [G][KP][KP]   cholcov(I + (1-rho) A_m), upper, identity-padded (k_prep)
+//   Sp     [ceil(G/4)][NP][KP]  per-4-shard partial of sum_m (W_m - sqrt(1-rho) A_m Z_m')
+//   xin    [NP+KP][KP]   local sum over shards of Sp (rows < NP) and A (rows >= NP)
+//   xall   [nranks][NP+KP][KP]  all-gathered xin (== xin when nranks == 1)
+//   C      [G][PP][KP]   C_m = Y_m' eta_m  (k_cpass);  E [G][KP][KP] = eta_m' eta_m
+//   cpart  [G][PP/8][KP] per-8-row partial column sums of psi o Lambda^2 (k_lambda)
+//   sloc   [G][KP], sall [g][KP]  column sums (all-gathered)
+//   Lb     [p][LDB]      saved Lambda rows of the current assembly batch, sample s at cols s*K..
+//   wsum   [p]           sum of saved omega of the batch
+//   Sigma  [p][p]        lower triangle accumulated (each rank: its tiles), mirrored on get
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dcfm {
+
+constexpr int KP = 32;         // padded factor count (K <= 32 in this build)
+constexpr int ASM_TILE = 128;  // covariance-assembly output tile
+
+struct Dims {
+    int n, P, g, K, G;          // G = local shards
+    int NP, PP;                 // padded rows / cols
+    int shard0;                 // first global shard of this rank
+    int nranks, rank;
+    int p;                      // P * g
+    double rho, sr, s1r;        // rho, sqrt(rho), sqrt(1-rho)
+    double as_, bs, df, ad1, bd1, ad2, bd2;
+    uint64_t seed;
+    int inject;
+};
+
+// injected draws on device, [T][...] with T = n_iter of dcfm_set_draws
+struct DrawsDev {
+    const double *NZ, *NX, *NL, *Gpsi, *Gdelta, *Gps;  // full-g arrays
+    int64_t first_iter, n_iter;
+};
+
+struct Bufs {
+    double *Y, *yy, *Lam, *omega, *ps, *psi, *Plam, *X, *Z, *delta, *tau;
+    double *W, *A, *R, *Rdi, *Sp, *xin, *xall, *C, *E, *cpart, *sloc, *sall;
+    double *Lb, *wsum, *Sigma;
+    int2 *tiles;
+    int ntiles, LDB;
+};
+
+// launchers (kernels.hip)
+void launch_prep(const Dims &d, const Bufs &b, hipStream_t s);
+void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s);
+void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
+void launch_xred(const Dims &d, const Bufs &b, hipStream_t s);
+void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
+void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s);
+void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
+                   const double *tau_cur, hipStream_t s);
+void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s);
+void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
+                  const double *delta_in, const double *tau_in, double *delta_out,
+                  double *tau_out, hipStream_t s);
+void launch_save(const Dims &d, const Bufs &b, int slot, hipStream_t s);
+void launch_assemble(const Dims &d, const Bufs &b, int kext, double inv_eff, hipStream_t s);
+void launch_mirror(double *S, int p, hipStream_t s);
+void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s);
+void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,
+                     int64_t count, double *out, hipStream_t s);
+
+}  // namespace dcfm

@@ -1,0 +1,887 @@
+// Hand-written CDNA4 (gfx950) kernels for one Gibbs iteration of the
+// divide-and-conquer factor model (reference divideconquer.m:90-196) and the
+// covariance assembly.  fp64 throughout (the reference is double precision).
+//
+// Kernel map (per iteration, in order)                         reference lines
+//   k_prep     A_m = Lambda' diag(w) Lambda, R_m = cholcov(I+(1-rho)A_m)   dc:98-100,114-115
+//   k_wpass    W_m = Y_m (w o Lambda_m)           fp64 MFMA, Y pass 1      dc:102-103,122-123
+//   k_zdraw    Z rows: R\ , R'\ , noise; partial sum_m (W - s1r A Z')      dc:101-107,121-124
+//   k_xred     sum partials over local shards (+ sum_m A_m)                dc:112-116,120-124
+//   [RCCL all-gather across ranks]
+//   k_xdraw    Xprec = gI + rho sum A, cholcov, X rows                     dc:117-128
+//   k_cpass    C_m = Y_m' eta_m, E_m = eta_m' eta_m  fp64 MFMA, Y pass 2   dc:133,138,141
+//   k_lambda   per loading row: Q, chol, 3 solves, Lambda_j; psi_j;        dc:140-145,150,
+//              SS_j via identity, ps_j, omega_j; column sums of psi o L^2  dc:156,169-171
+//   k_colsum   per-shard column sums                                       dc:156
+//   [RCCL all-gather across ranks]
+//   k_delta    MGP chain (quirks Q4/Q5) for all shards, Plam refresh       dc:155-165,175-177
+//   saved iterations: k_save (+ RCCL all-gather at flush), k_assemble      dc:180-195
+//
+// The residual pass of dc:169-170 needs no third read of Y: with C_j = eta'Y_j
+// and E = eta'eta already computed for the loading draw,
+//   SS_j = sum_i (Y_ij - eta_i Lambda_j')^2 = yy_j - 2 Lambda_j.C_j + Lambda_j E Lambda_j'.
+#include "dcfm_internal.h"
+#include "philox.h"
+
+#include <algorithm>
+
+namespace dcfm {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ d4 mfma16x16x4(double a, double b, d4 c) {
+    // v_mfma_f64_16x16x4_f64: A[i=lane&15][k=lane>>4], B[k=lane>>4][j=lane&15],
+    // C/D: col = lane&15, row = (lane>>4) + 4*reg
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// eta = sqrt(rho) X + sqrt(1-rho) Z    (dc:81,133) — one definition for every use
+__device__ __forceinline__ double eta_of(double sr, double s1r, double x, double z) {
+    return sr * x + s1r * z;
+}
+
+// ----------------------------------------------------------------------------
+// small in-LDS Cholesky (lower, L L' = S), S is KP x KP with row stride KP+1,
+// executed by every thread of the block (nthreads >= 64).
+// ----------------------------------------------------------------------------
+__device__ void lds_cholesky(double (*S)[KP + 1], int t, int nthreads) {
+    for (int k = 0; k < KP; ++k) {
+        __syncthreads();
+        if (t == 0) S[k][k] = sqrt(S[k][k]);
+        __syncthreads();
+        if (t > k && t < KP) S[t][k] = S[t][k] / S[k][k];
+        __syncthreads();
+        for (int e = t; e < KP * KP; e += nthreads) {
+            const int r = e / KP, c = e % KP;
+            if (r > k && c > k && c <= r) S[r][c] -= S[r][k] * S[c][k];
+        }
+    }
+    __syncthreads();
+}
+
+// ============================================================================
+// k_prep: A_m and R_m = cholcov(eye(K) + (1-rho) A_m)          dc:98-100
+// ============================================================================
+__global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__ Lam,
+                                              const double *__restrict__ omega,
+                                              double *__restrict__ A, double *__restrict__ R,
+                                              double *__restrict__ Rdi) {
+    __shared__ double S[KP][KP + 1];
+    const int m = blockIdx.x;
+    const int t = threadIdx.x;
+    const double *L = Lam + (size_t)m * d.PP * KP;
+    const double *w = omega + (size_t)m * d.PP;
+    const int b = t & 31, ag = t >> 5;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < d.P; ++j) {
+        const double wj = w[j];
+        const double lb = L[j * KP + b];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] += (L[j * KP + ag + 8 * q] * wj) * lb;  // Zmsg'*Lambda
+    }
+    double *Am = A + (size_t)m * KP * KP;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int a = ag + 8 * q;
+        Am[a * KP + b] = acc[q];
+        // cholcov reads the upper triangle (a <= b): lower factor of S with S[b][a] = Zprec[a][b]
+        if (a <= b) S[b][a] = (a == b ? 1.0 : 0.0) + (1.0 - d.rho) * acc[q];
+    }
+    lds_cholesky(S, t, 256);
+    double *Rm = R + (size_t)m * KP * KP;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int a = ag + 8 * q;
+        Rm[a * KP + b] = (a <= b) ? S[b][a] : 0.0;   // R = L', upper, R'R = Zprec
+    }
+    if (t < KP) Rdi[(size_t)m * KP + t] = 1.0 / S[t][t];
+}
+
+// ============================================================================
+// k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA
+// one wave = (shard m, 16 rows i) x 32 k; reduction over j in chunks of 8:
+// lane (r = lane&15, q = lane>>4) holds Y[i0+r][8t+2q .. +1]; k-step 2t uses
+// element 0, 2t+1 element 1 (the B operand uses the same j <-> (q,e) map).
+// ============================================================================
+__global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict__ Y,
+                                               const double *__restrict__ Lam,
+                                               const double *__restrict__ omega,
+                                               double *__restrict__ W) {
+    const int m = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i0 = (blockIdx.x * 4 + wave) * 16;
+    if (i0 >= d.NP) return;
+    const int r = lane & 15, q = lane >> 4;
+    const double *Yrow = Y + ((size_t)m * d.NP + i0 + r) * d.PP;
+    const double *L = Lam + (size_t)m * d.PP * KP;
+    const double *w = omega + (size_t)m * d.PP;
+    d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    const int nch = d.PP >> 3;
+#pragma unroll 4
+    for (int t = 0; t < nch; ++t) {
+        const int j = 8 * t + 2 * q;
+        const d2 y = *reinterpret_cast<const d2 *>(Yrow + j);
+        const d2 wj = *reinterpret_cast<const d2 *>(w + j);
+        const double b00 = wj.x * L[j * KP + r];
+        const double b01 = wj.x * L[j * KP + 16 + r];
+        const double b10 = wj.y * L[(j + 1) * KP + r];
+        const double b11 = wj.y * L[(j + 1) * KP + 16 + r];
+        acc0 = mfma16x16x4(y.x, b00, acc0);
+        acc1 = mfma16x16x4(y.x, b01, acc1);
+        acc0 = mfma16x16x4(y.y, b10, acc0);
+        acc1 = mfma16x16x4(y.y, b11, acc1);
+    }
+    double *Wt = W + ((size_t)m * d.NP + i0) * KP;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        Wt[(q + 4 * g) * KP + r] = acc0[g];
+        Wt[(q + 4 * g) * KP + 16 + r] = acc1[g];
+    }
+}
+
+// ============================================================================
+// k_zdraw: per (row i, shard m), lane = row.                    dc:101-107,121-123
+//   bz = sqrt(1-rho) (W_i - sqrt(rho) A X_i)            (= sqrt(1-rho) Zmsg'(Y_i - sqrt(rho) L X_i))
+//   v  = R \ bz ;  Z_i = R' \ (v + eps)                 (quirk Q2 order)
+//   S_i += W_i - sqrt(1-rho) A Z_i                       (Xmsg'(Y_i - sqrt(1-rho) L Z_i))
+// 4 shards per block (one per wave), reduced in LDS -> Sp[blockIdx.y].
+// ============================================================================
+__global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W,
+                                               const double *__restrict__ A,
+                                               const double *__restrict__ R,
+                                               const double *__restrict__ Rdi,
+                                               const double *__restrict__ X,
+                                               double *__restrict__ Z, double *__restrict__ Sp,
+                                               DrawsDev dr, int64_t iter) {
+    __shared__ double red[2][64][KP + 1];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int m = blockIdx.y * 4 + wave;
+    const int i = blockIdx.x * 64 + lane;
+    double s[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) s[k] = 0.0;
+    if (m < d.G && i < d.n) {
+        const double *Am = A + (size_t)m * KP * KP;
+        const double *Rm = R + (size_t)m * KP * KP;
+        const double *Rd = Rdi + (size_t)m * KP;
+        const double *Wi = W + ((size_t)m * d.NP + i) * KP;
+        const double *Xi = X + (size_t)i * KP;
+        double x[KP], t[KP];
+#pragma unroll
+        for (int k = 0; k < KP; k += 2) {
+            const d2 v = *reinterpret_cast<const d2 *>(Xi + k);
+            x[k] = v.x;
+            x[k + 1] = v.y;
+        }
+#pragma unroll
+        for (int a = 0; a < KP; ++a) {
+            double acc = 0.0;
+#pragma unroll
+            for (int b = 0; b < KP; ++b) acc += Am[a * KP + b] * x[b];
+            t[a] = d.s1r * (Wi[a] - d.sr * acc);
+        }
+        // back substitution R v = bz (R upper)
+#pragma unroll
+        for (int a = KP - 1; a >= 0; --a) {
+            double acc = t[a];
+#pragma unroll
+            for (int b = a + 1; b < KP; ++b) acc -= Rm[a * KP + b] * t[b];
+            t[a] = acc * Rd[a];
+        }
+        // + eps  (dc:104 normrnd(0,1,[K,1]))
+        const int mg = d.shard0 + m;
+        if (d.inject) {
+            const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + i) * d.K;
+#pragma unroll
+            for (int k = 0; k < KP; ++k)
+                if (k < d.K) t[k] += nz[k];
+        } else {
+            const Rng rng(d.seed);
+#pragma unroll
+            for (int k = 0; k < KP; k += 2) {
+                if (k < d.K) {
+                    double n0, n1;
+                    rng.normal2(SITE_Z, mg, i, k >> 1, (uint32_t)iter, n0, n1);
+                    t[k] += n0;
+                    if (k + 1 < d.K) t[k + 1] += n1;
+                }
+            }
+        }
+        // forward substitution R' z = v + eps
+#pragma unroll
+        for (int a = 0; a < KP; ++a) {
+            double acc = t[a];
+#pragma unroll
+            for (int b = 0; b < a; ++b) acc -= Rm[b * KP + a] * t[b];
+            t[a] = acc * Rd[a];
+        }
+        double *Zi = Z + ((size_t)m * d.NP + i) * KP;
+#pragma unroll
+        for (int k = 0; k < KP; k += 2) {
+            d2 v;
+            v.x = (k < d.K) ? t[k] : 0.0;
+            v.y = (k + 1 < d.K) ? t[k + 1] : 0.0;
+            *reinterpret_cast<d2 *>(Zi + k) = v;
+        }
+#pragma unroll
+        for (int a = 0; a < KP; ++a) {
+            double acc = 0.0;
+#pragma unroll
+            for (int b = 0; b < KP; ++b) acc += Am[a * KP + b] * t[b];
+            s[a] = Wi[a] - d.s1r * acc;
+        }
+    }
+    // deterministic 4-wave reduction: ((s0 + s2) + (s1 + s3))
+    if (wave >= 2) {
+#pragma unroll
+        for (int k = 0; k < KP; ++k) red[wave - 2][lane][k] = s[k];
+    }
+    __syncthreads();
+    if (wave < 2) {
+#pragma unroll
+        for (int k = 0; k < KP; ++k) s[k] += red[wave][lane][k];
+    }
+    __syncthreads();
+    if (wave == 1) {
+#pragma unroll
+        for (int k = 0; k < KP; ++k) red[0][lane][k] = s[k];
+    }
+    __syncthreads();
+    if (wave == 0 && i < d.NP) {
+        double *o = Sp + ((size_t)blockIdx.y * d.NP + i) * KP;
+#pragma unroll
+        for (int k = 0; k < KP; k += 2) {
+            d2 v;
+            v.x = s[k] + red[0][lane][k];
+            v.y = s[k + 1] + red[0][lane][k + 1];
+            *reinterpret_cast<d2 *>(o + k) = v;
+        }
+    }
+}
+
+// ============================================================================
+// k_xred: xin[i][k] = sum_q Sp[q][i][k];  xin[NP+a][b] = sum_m A_m[a][b]     dc:113-116,121-124
+// ============================================================================
+__global__ __launch_bounds__(256) void k_xred(Dims d, const double *__restrict__ Sp,
+                                              const double *__restrict__ A,
+                                              double *__restrict__ xin) {
+    const int nq = (d.G + 3) >> 2;
+    const size_t total = (size_t)(d.NP + KP) * KP;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total;
+         e += (size_t)gridDim.x * blockDim.x) {
+        const size_t row = e / KP;
+        double acc = 0.0;
+        if (row < (size_t)d.NP) {
+            for (int q = 0; q < nq; ++q) acc += Sp[(size_t)q * d.NP * KP + e];
+        } else {
+            const size_t off = e - (size_t)d.NP * KP;
+            for (int m = 0; m < d.G; ++m) acc += A[(size_t)m * KP * KP + off];
+        }
+        xin[e] = acc;
+    }
+}
+
+// ============================================================================
+// k_xdraw: X rows.  Xprec = g*I + rho*sum_m A_m (all ranks), Rx = cholcov,     dc:117-128
+//   X_i = Rx' \ (Rx \ (sqrt(rho) S_i) + eps)
+// one wave per 64 rows; every block factors the KxK Xprec itself (cheap).
+// ============================================================================
+__global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__ xall,
+                                              double *__restrict__ X, DrawsDev dr, int64_t iter) {
+    __shared__ double S[KP][KP + 1];
+    __shared__ double Rd[KP];
+    const int t = threadIdx.x;
+    const size_t stride = (size_t)(d.NP + KP) * KP;
+    for (int e = t; e < KP * KP; e += 64) {
+        const int a = e / KP, b = e % KP;
+        double v = 0.0;
+        for (int rk = 0; rk < d.nranks; ++rk) v += xall[rk * stride + (size_t)(d.NP + a) * KP + b];
+        if (a <= b) S[b][a] = (a == b ? (double)d.g : 0.0) + d.rho * v;   // upper triangle (cholcov)
+    }
+    lds_cholesky(S, t, 64);
+    if (t < KP) Rd[t] = 1.0 / S[t][t];
+    __syncthreads();
+    const int i = blockIdx.x * 64 + t;
+    if (i >= d.n) return;
+    double v[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) v[k] = 0.0;
+    for (int rk = 0; rk < d.nranks; ++rk) {
+        const double *s = xall + rk * stride + (size_t)i * KP;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) v[k] += s[k];
+    }
+#pragma unroll
+    for (int k = 0; k < KP; ++k) v[k] = d.sr * v[k];     // bx = sqrt(rho)*sumx2
+    // Rx v' = bx (Rx[a][b] = S[b][a], upper)
+#pragma unroll
+    for (int a = KP - 1; a >= 0; --a) {
+        double acc = v[a];
+#pragma unroll
+        for (int b = a + 1; b < KP; ++b) acc -= S[b][a] * v[b];
+        v[a] = acc * Rd[a];
+    }
+    if (d.inject) {
+        const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + i) * d.K;
+#pragma unroll
+        for (int k = 0; k < KP; ++k)
+            if (k < d.K) v[k] += nx[k];
+    } else {
+        const Rng rng(d.seed);
+#pragma unroll
+        for (int k = 0; k < KP; k += 2) {
+            if (k < d.K) {
+                double n0, n1;
+                rng.normal2(SITE_X, 0, i, k >> 1, (uint32_t)iter, n0, n1);
+                v[k] += n0;
+                if (k + 1 < d.K) v[k + 1] += n1;
+            }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < KP; ++a) {
+        double acc = v[a];
+#pragma unroll
+        for (int b = 0; b < a; ++b) acc -= S[a][b] * v[b];
+        v[a] = acc * Rd[a];
+    }
+    double *Xi = X + (size_t)i * KP;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) Xi[k] = (k < d.K) ? v[k] : 0.0;
+}
+
+// ============================================================================
+// k_cpass: [C_m | E_m] = [Y_m | eta_m]' eta_m    fp64 MFMA, Y pass 2      dc:133,138,141
+// one wave = (shard m, 16-column tile of [Y | eta]) x 32 k, reduction over i.
+// ============================================================================
+__global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict__ Y,
+                                               const double *__restrict__ X,
+                                               const double *__restrict__ Z,
+                                               double *__restrict__ C, double *__restrict__ E) {
+    const int m = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ntY = d.PP >> 4;
+    const int nt = blockIdx.x * 4 + wave;
+    if (nt >= ntY + KP / 16) return;
+    const bool isE = nt >= ntY;
+    const int c0 = isE ? (nt - ntY) * 16 : nt * 16;
+    const int r = lane & 15, q = lane >> 4;
+    const double *Ym = Y + (size_t)m * d.NP * d.PP + c0 + r;
+    const double *Zm = Z + (size_t)m * d.NP * KP;
+    d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    const int ns = d.NP >> 2;
+#pragma unroll 4
+    for (int s = 0; s < ns; ++s) {
+        const int i = 4 * s + q;
+        const double e0 = eta_of(d.sr, d.s1r, X[i * KP + r], Zm[i * KP + r]);
+        const double e1 = eta_of(d.sr, d.s1r, X[i * KP + 16 + r], Zm[i * KP + 16 + r]);
+        const double a = isE ? (c0 == 0 ? e0 : e1) : Ym[(size_t)i * d.PP];
+        acc0 = mfma16x16x4(a, e0, acc0);
+        acc1 = mfma16x16x4(a, e1, acc1);
+    }
+    double *out = isE ? (E + (size_t)m * KP * KP) : (C + (size_t)m * d.PP * KP);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int row = c0 + q + 4 * g;
+        out[row * KP + r] = acc0[g];
+        out[row * KP + 16 + r] = acc1[g];
+    }
+}
+
+// ============================================================================
+// k_lambda: loading rows.  A half-wave (32 lanes) owns one row j; lane r holds
+// row r of Q_j = diag(Plam_j) + ps_j E_m in registers.        dc:140-145 (+150,156,169-171)
+//   L = chol(Q,'lower') right-looking, column k broadcast through LDS
+//   v = L \ (ps_j C_j);  Lambda_j = L' \ (v + z)             (= ylam + mlam)
+//   psi_j  = Gpsi * 1/(df/2 + 0.5 lambda^2 tau)               (dc:150, tau of the previous it.)
+//   SS_j   = yy_j - 2 lambda.C_j + lambda' E lambda  ->  ps_j = Gps * 1/(bs + 0.5 SS_j), w = 1/ps
+// 8 rows per 256-thread block; per-block column sums of psi o lambda^2 -> cpart.
+// ============================================================================
+constexpr int LS = KP + 2;   // LDS row stride: column KP holds 1/l_kk
+
+__device__ __forceinline__ double readsel(double x, int c, bool upper) {
+    const double lo = readlane_d(x, c);
+    const double hi = readlane_d(x, 32 + c);
+    return upper ? hi : lo;
+}
+
+__global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict__ C,
+                                                const double *__restrict__ E,
+                                                const double *__restrict__ yy,
+                                                const double *__restrict__ tau_cur,
+                                                double *__restrict__ Lam, double *__restrict__ psi,
+                                                double *__restrict__ Plam, double *__restrict__ ps,
+                                                double *__restrict__ omega,
+                                                double *__restrict__ cpart, DrawsDev dr,
+                                                int64_t iter) {
+    __shared__ double LT[8][KP][LS];   // LT[h][k][c] = L[c][k]  (column k of L, contiguous)
+    __shared__ double Es[KP][KP + 1];  // E_m, shared by the block's 8 rows (same shard)
+    __shared__ double csum[8][KP];
+    const int m = blockIdx.y;
+    const int mg = d.shard0 + m;
+    const int lane = threadIdx.x & 63;
+    const int hw = threadIdx.x >> 5;          // half-wave id 0..7
+    const bool upper = (lane >= 32);
+    const int r = lane & 31;                  // matrix row
+    const int j = blockIdx.x * 8 + hw;
+    const bool valid = j < d.P;
+    const bool real = r < d.K;
+    const size_t rowoff = ((size_t)m * d.PP + (valid ? j : 0)) * KP;
+
+    {
+        const double *Em = E + (size_t)m * KP * KP;
+        for (int e = threadIdx.x; e < KP * KP; e += 256) Es[e / KP][e % KP] = Em[e];
+    }
+    __syncthreads();
+    // --- build Q row r and rhs
+    const double psj = valid ? ps[(size_t)m * d.PP + j] : 0.0;
+    double q[KP];
+#pragma unroll
+    for (int c = 0; c < KP; ++c) q[c] = psj * Es[r][c];
+    const double plam = (valid && real) ? Plam[rowoff + r] : 1.0;
+#pragma unroll
+    for (int c = 0; c < KP; ++c)
+        if (c == r) q[c] = (real && valid) ? plam + q[c] : 1.0;
+    const double cjr = valid ? C[rowoff + r] : 0.0;
+    double bv = psj * cjr;
+
+    // --- Cholesky
+    double (*Lt)[LS] = LT[hw];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const double dkk = readsel(q[k], k, upper);
+        const double lkk = sqrt(dkk);
+        const double ikk = 1.0 / lkk;
+        const double lrk = (r > k) ? q[k] * ikk : (r == k ? lkk : 0.0);
+        q[k] = lrk;
+        Lt[k][r] = lrk;
+        if (r == k) Lt[k][KP] = ikk;
+#pragma unroll
+        for (int c = k + 1; c < KP; ++c) q[c] -= lrk * Lt[k][c];
+        // keep the trailing update eager: without this hipcc sinks each FMA to
+        // the step that consumes q[c] and keeps O(K^2) loaded L values live
+#pragma unroll
+        for (int c = k + 1; c < KP; ++c) asm volatile("" : "+v"(q[c]));
+    }
+    // --- forward solve L v = b   (L[r][c] = Lt[c][r])
+    double vr = 0.0;
+#pragma unroll 2
+    for (int c = 0; c < KP; ++c) {
+        const double vc = readsel(bv, c, upper) * Lt[c][KP];
+        if (r == c) vr = vc;
+        if (r > c) bv -= Lt[c][r] * vc;
+    }
+    // --- + z  (dc:142 normrnd(0,1,K,1))
+    double z = 0.0;
+    if (real && valid) {
+        if (d.inject) {
+            z = dr.NL[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + r];
+        } else {
+            const Rng rng(d.seed);
+            z = rng.normal(SITE_LAMBDA, mg, j, r, (uint32_t)iter);
+        }
+    }
+    double wr = vr + z;
+    // --- back solve L' x = w
+    double xr = 0.0;
+#pragma unroll 2
+    for (int c = KP - 1; c >= 0; --c) {
+        const double xc = readsel(wr, c, upper) * Lt[c][KP];
+        if (r == c) xr = xc;
+        if (r < c) wr -= Lt[r][c] * xc;       // L[c][r]
+    }
+    if (!real) xr = 0.0;
+
+    // --- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr
+    // broadcast x through LDS (reuse column KP+1 slot of each row: LT[h][r][KP+1])
+    Lt[r][KP + 1] = xr;
+    double ex = 0.0;
+#pragma unroll
+    for (int c = 0; c < KP; ++c) ex += Es[c][r] * Lt[c][KP + 1];   // (E x)_r, E symmetric
+    double contrib = xr * (ex - 2.0 * cjr);
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) contrib += __shfl_xor(contrib, o, 32);
+
+    // --- psi (dc:150), uses tau of the previous iteration (Q11)
+    double psir = 0.0;
+    if (real && valid) {
+        const double tr = tau_cur[(size_t)mg * KP + r];
+        const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xr * xr * tr));
+        double G;
+        if (d.inject) {
+            G = dr.Gpsi[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + r) * d.P + j];
+        } else {
+            const Rng rng(d.seed);
+            G = rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, mg, j, r, (uint32_t)iter);
+        }
+        psir = scale * G;
+    }
+    csum[hw][r] = psir * (xr * xr);       // mat = psijh .* Lambda.^2 (dc:156)
+
+    if (valid) {
+        Lam[rowoff + r] = xr;
+        if (real) psi[rowoff + r] = psir;
+        if (r == 0) {
+            const double SS = yy[(size_t)m * d.PP + j] + contrib;
+            double G;
+            if (d.inject) {
+                G = dr.Gps[((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j];
+            } else {
+                const Rng rng(d.seed);
+                G = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg, j, 0, (uint32_t)iter);
+            }
+            const double psn = (1.0 / (d.bs + 0.5 * SS)) * G;   // dc:170
+            ps[(size_t)m * d.PP + j] = psn;
+            omega[(size_t)m * d.PP + j] = 1.0 / psn;            // dc:171 (Q1)
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < KP) {
+        double s = 0.0;
+#pragma unroll
+        for (int h = 0; h < 8; ++h) s += csum[h][threadIdx.x];
+        cpart[((size_t)m * (d.PP >> 3) + blockIdx.x) * KP + threadIdx.x] = s;
+    }
+}
+
+// ============================================================================
+// k_colsum: sloc[m][k] = sum_b cpart[m][b][k]                               dc:156 sum(mat)
+// ============================================================================
+__global__ __launch_bounds__(64) void k_colsum(Dims d, const double *__restrict__ cpart,
+                                               double *__restrict__ sloc) {
+    const int m = blockIdx.x, k = threadIdx.x;
+    if (k >= KP) return;
+    const int nb = (d.P + 7) >> 3;
+    double s = 0.0;
+    for (int b = 0; b < nb; ++b) s += cpart[((size_t)m * (d.PP >> 3) + b) * KP + k];
+    sloc[(size_t)m * KP + k] = s;
+}
+
+// ============================================================================
+// k_delta: multiplicative-gamma-process chain                      dc:154-165, 174-177
+//   K >= 2: every shard's h>=2 step reads shard 1's ALREADY-updated delta_h (Q4);
+//           each block re-runs shard 1's chain first (deterministic, identical).
+//   K == 1: cumprod over the K x 1 x g array runs along shards (Q5):
+//           tau_used(m) = prod_{m'<m} delta_new(m') * delta_old(m).
+// grid = all g shards (delta/tau replicated on every rank); local blocks also
+// refresh Plam = psi o tau'.
+// ============================================================================
+__device__ __forceinline__ double wave_scan_prod(double v, int l) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_up(v, o, 64);
+        if (l >= o) v *= u;
+    }
+    return v;
+}
+
+__device__ double delta_G(const Dims &d, const DrawsDev &dr, int64_t iter, int mg, int h) {
+    if (d.inject) return dr.Gdelta[((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + h];
+    const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - h);
+    const Rng rng(d.seed);
+    return rng.gamma(shape, SITE_DELTA, mg, 0, h, (uint32_t)iter);
+}
+
+// runs one shard's chain; lane l holds delta_l, tau_l, s_l, G_l (l < K)
+__device__ void delta_chain(const Dims &d, int l, double &dl, double &tl, double sl, double Gl,
+                            bool own, double d0new) {
+    const bool act = l < d.K;
+    double dot = wave_sum(act ? tl * sl : 0.0);
+    const double d_1 = readlane_d(dl, 0);
+    double bd = d.bd1 + (0.5 * (1.0 / d_1)) * dot;               // dc:157
+    const double g0 = readlane_d(Gl, 0);
+    if (l == 0) dl = (1.0 / bd) * g0;                             // dc:158
+    tl = wave_scan_prod(dl, l);                                   // dc:158 cumprod
+    for (int h = 1; h < d.K; ++h) {
+        dot = wave_sum((act && l >= h) ? tl * sl : 0.0);
+        const double dref = own ? readlane_d(dl, h) : readlane_d(d0new, h);   // delta(h) (Q4)
+        bd = d.bd2 + (0.5 * (1.0 / dref)) * dot;                  // dc:161
+        const double gh = readlane_d(Gl, h);
+        if (l == h) dl = (1.0 / bd) * gh;                         // dc:163
+        tl = wave_scan_prod(dl, l);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_delta(Dims d, const double *__restrict__ sall,
+                                               const double *__restrict__ delta_in,
+                                               const double *__restrict__ tau_in,
+                                               double *__restrict__ delta_out,
+                                               double *__restrict__ tau_out,
+                                               const double *__restrict__ psi,
+                                               double *__restrict__ Plam, DrawsDev dr,
+                                               int64_t iter) {
+    __shared__ double tnew[KP];
+    const int m = blockIdx.x;   // global shard
+    const int t = threadIdx.x;
+    if (t < 64) {
+        const int l = t;
+        const int lk = l < KP ? l : 0;
+        if (d.K >= 2) {
+            double G0 = (l < d.K) ? delta_G(d, dr, iter, 0, l) : 1.0;
+            double d0 = (l < KP) ? delta_in[lk] : 1.0;
+            double t0 = (l < KP) ? tau_in[lk] : 1.0;
+            const double s0 = (l < KP) ? sall[lk] : 0.0;
+            delta_chain(d, l, d0, t0, s0, G0, true, 0.0);
+            double dm = d0, tm = t0;
+            if (m != 0) {
+                const double Gm = (l < d.K) ? delta_G(d, dr, iter, m, l) : 1.0;
+                dm = (l < KP) ? delta_in[(size_t)m * KP + lk] : 1.0;
+                tm = (l < KP) ? tau_in[(size_t)m * KP + lk] : 1.0;
+                const double sm = (l < KP) ? sall[(size_t)m * KP + lk] : 0.0;
+                delta_chain(d, l, dm, tm, sm, Gm, false, d0);
+            }
+            if (l < KP) {
+                const bool act = l < d.K;
+                delta_out[(size_t)m * KP + l] = act ? dm : delta_in[(size_t)m * KP + l];
+                tau_out[(size_t)m * KP + l] = act ? tm : tau_in[(size_t)m * KP + l];
+                tnew[l] = tm;
+            }
+        } else {
+            if (l == 0) {
+                double prefix = 1.0, dnew = 0.0;
+                for (int mm = 0; mm <= m; ++mm) {
+                    const double dold = delta_in[(size_t)mm * KP];
+                    const double tused = prefix * dold;
+                    const double bd = d.bd1 + (0.5 * (1.0 / dold)) * (tused * sall[(size_t)mm * KP]);
+                    dnew = (1.0 / bd) * delta_G(d, dr, iter, mm, 0);
+                    prefix = prefix * dnew;
+                }
+                delta_out[(size_t)m * KP] = dnew;
+                tau_out[(size_t)m * KP] = prefix;
+                tnew[0] = prefix;
+            }
+            if (l >= 1 && l < KP) {
+                delta_out[(size_t)m * KP + l] = delta_in[(size_t)m * KP + l];
+                tau_out[(size_t)m * KP + l] = tau_in[(size_t)m * KP + l];
+            }
+        }
+    }
+    __syncthreads();
+    const int ml = m - d.shard0;
+    if (ml < 0 || ml >= d.G) return;
+    const size_t base = (size_t)ml * d.PP * KP;
+    for (int e = t; e < d.P * KP; e += 256) {
+        const int k = e % KP;
+        if (k < d.K) Plam[base + e] = psi[base + e] * tnew[k];   // dc:176
+    }
+}
+
+// ============================================================================
+// saved samples: Lb[(mg*P + j)][slot*K + k] = Lambda, wsum += omega         dc:180-186
+// ============================================================================
+__global__ __launch_bounds__(256) void k_save(Dims d, const double *__restrict__ Lam,
+                                              const double *__restrict__ omega,
+                                              double *__restrict__ Lb, double *__restrict__ wsum,
+                                              int LDB, int slot) {
+    const size_t total = (size_t)d.G * d.P * d.K;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total;
+         e += (size_t)gridDim.x * blockDim.x) {
+        const int k = e % d.K;
+        const size_t jm = e / d.K;
+        const int j = jm % d.P, m = jm / d.P;
+        const size_t a = (size_t)(d.shard0 + m) * d.P + j;
+        Lb[a * LDB + (size_t)slot * d.K + k] = Lam[((size_t)m * d.PP + j) * KP + k];
+        if (k == 0) wsum[a] += omega[(size_t)m * d.PP + j];
+    }
+}
+
+// ============================================================================
+// k_assemble: Sigma[a][b] += (coef(a,b)/effsamp) sum_kk Lb[a][kk] Lb[b][kk]
+//                            + [a==b] wsum[a]/effsamp                       dc:184-195
+// coef = 1 inside a diagonal shard block (Lambda_r Lambda_r' + Omega_r), rho
+// across blocks (rho Lambda_r Lambda_c').  Lower-triangle 128x128 tiles only;
+// 4 waves in 2x2, each 64x64 = 4x4 tiles of v_mfma_f64_16x16x4; operands
+// streamed from L2 with one chunk (8 k) of register prefetch.
+// ============================================================================
+__global__ __launch_bounds__(256) void k_assemble(Dims d, const double *__restrict__ Lb, int LDB,
+                                                  int kext, const double *__restrict__ wsum,
+                                                  double inv_eff, const int2 *__restrict__ tiles,
+                                                  double *__restrict__ Sig) {
+    const int2 T = tiles[blockIdx.x];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 15, q = lane >> 4;
+    const int a0 = T.x * ASM_TILE + (wave >> 1) * 64;
+    const int b0 = T.y * ASM_TILE + (wave & 1) * 64;
+    const int p = d.p;
+    const double *pa[4], *pb[4];
+    bool va[4], vb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int ar = a0 + 16 * u + r, br = b0 + 16 * u + r;
+        va[u] = ar < p;
+        vb[u] = br < p;
+        pa[u] = Lb + (size_t)(va[u] ? ar : 0) * LDB + 2 * q;
+        pb[u] = Lb + (size_t)(vb[u] ? br : 0) * LDB + 2 * q;
+    }
+    d4 acc[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[u][v] = d4{0.0, 0.0, 0.0, 0.0};
+    const d2 zero2 = {0.0, 0.0};
+    d2 an[4], bn[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        an[u] = va[u] ? *reinterpret_cast<const d2 *>(pa[u]) : zero2;
+        bn[u] = vb[u] ? *reinterpret_cast<const d2 *>(pb[u]) : zero2;
+    }
+    for (int kc = 0; kc < kext; kc += 8) {
+        d2 ac[4], bc[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { ac[u] = an[u]; bc[u] = bn[u]; }
+        if (kc + 8 < kext) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                an[u] = va[u] ? *reinterpret_cast<const d2 *>(pa[u] + kc + 8) : zero2;
+                bn[u] = vb[u] ? *reinterpret_cast<const d2 *>(pb[u] + kc + 8) : zero2;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[u][v] = mfma16x16x4(ac[u].x, bc[v].x, acc[u][v]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[u][v] = mfma16x16x4(ac[u].y, bc[v].y, acc[u][v]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int a = a0 + 16 * u + q + 4 * g;
+            if (a >= p) continue;
+            const int sa = a / d.P;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int b = b0 + 16 * v + r;
+                if (b > a || b >= p) continue;
+                const double coef = (b / d.P == sa) ? 1.0 : d.rho;
+                double val = coef * acc[u][v][g] * inv_eff;
+                if (a == b) val += wsum[a] * inv_eff;
+                Sig[(size_t)a * p + b] += val;
+            }
+        }
+    }
+}
+
+// Sigma[a][b] = Sigma[b][a] for a < b (lower -> upper), 32x32 LDS tiles
+__global__ __launch_bounds__(256) void k_mirror(double *__restrict__ S, int p) {
+    __shared__ double tile[32][33];
+    const int tr = blockIdx.y, tc = blockIdx.x;   // destination tile (upper: tr <= tc)
+    if (tr > tc) return;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int yy = ty; yy < 32; yy += 8) {
+        const int sr = tc * 32 + yy, sc = tr * 32 + tx;   // source lower tile (tc, tr)
+        tile[yy][tx] = (sr < p && sc < p) ? S[(size_t)sr * p + sc] : 0.0;
+    }
+    __syncthreads();
+    for (int yy = ty; yy < 32; yy += 8) {
+        const int dr = tr * 32 + yy, dc = tc * 32 + tx;
+        if (dr < p && dc < p && dr < dc) S[(size_t)dr * p + dc] = tile[tx][yy];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_eta(Dims d, const double *__restrict__ X,
+                                             const double *__restrict__ Z, double *__restrict__ eta) {
+    const size_t total = (size_t)d.G * d.NP * KP;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total;
+         e += (size_t)gridDim.x * blockDim.x) {
+        const size_t ik = e % ((size_t)d.NP * KP);
+        eta[e] = eta_of(d.sr, d.s1r, X[ik], Z[e]);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_rng_fill(uint64_t seed, int kind, double shape, int site,
+                                                  int shard, int64_t iter, int64_t count,
+                                                  double *__restrict__ out) {
+    const Rng rng(seed);
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < count;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t row = (uint32_t)(e / 32), k = (uint32_t)(e % 32);
+        out[e] = kind == 0 ? rng.normal(site, shard, row, k, (uint32_t)iter)
+                           : rng.gamma(shape, site, shard, row, k, (uint32_t)iter);
+    }
+}
+
+// ============================================================================
+// launchers
+// ============================================================================
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+void launch_prep(const Dims &d, const Bufs &b, hipStream_t s) {
+    hipLaunchKernelGGL(k_prep, dim3(d.G), dim3(256), 0, s, d, b.Lam, b.omega, b.A, b.R, b.Rdi);
+}
+void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s) {
+    hipLaunchKernelGGL(k_wpass, dim3(cdiv(d.NP, 64), d.G), dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W);
+}
+void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+    hipLaunchKernelGGL(k_zdraw, dim3(cdiv(d.NP, 64), cdiv(d.G, 4)), dim3(256), 0, s, d, b.W, b.A, b.R,
+                       b.Rdi, b.X, b.Z, b.Sp, dr, iter);
+}
+void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
+    const int total = (d.NP + KP) * KP;
+    hipLaunchKernelGGL(k_xred, dim3(cdiv(total, 256)), dim3(256), 0, s, d, b.Sp, b.A, b.xin);
+}
+void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+    hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 64)), dim3(64), 0, s, d, b.xall, b.X, dr, iter);
+}
+void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
+    const int nt = d.PP / 16 + KP / 16;
+    hipLaunchKernelGGL(k_cpass, dim3(cdiv(nt, 4), d.G), dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E);
+}
+void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
+                   const double *tau_cur, hipStream_t s) {
+    hipLaunchKernelGGL(k_lambda, dim3(cdiv(d.P, 8), d.G), dim3(256), 0, s, d, b.C, b.E, b.yy, tau_cur,
+                       b.Lam, b.psi, b.Plam, b.ps, b.omega, b.cpart, dr, iter);
+}
+void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s) {
+    hipLaunchKernelGGL(k_colsum, dim3(d.G), dim3(64), 0, s, d, b.cpart, b.sloc);
+}
+void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
+                  const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
+                  hipStream_t s) {
+    hipLaunchKernelGGL(k_delta, dim3(d.g), dim3(256), 0, s, d, b.sall, delta_in, tau_in, delta_out,
+                       tau_out, b.psi, b.Plam, dr, iter);
+}
+void launch_save(const Dims &d, const Bufs &b, int slot, hipStream_t s) {
+    const size_t total = (size_t)d.G * d.P * d.K;
+    const int grid = (int)std::min<size_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_save, dim3(grid), dim3(256), 0, s, d, b.Lam, b.omega, b.Lb, b.wsum, b.LDB, slot);
+}
+void launch_assemble(const Dims &d, const Bufs &b, int kext, double inv_eff, hipStream_t s) {
+    if (b.ntiles == 0) return;
+    hipLaunchKernelGGL(k_assemble, dim3(b.ntiles), dim3(256), 0, s, d, b.Lb, b.LDB, kext, b.wsum,
+                       inv_eff, b.tiles, b.Sigma);
+}
+void launch_mirror(double *S, int p, hipStream_t s) {
+    const int nt = cdiv(p, 32);
+    hipLaunchKernelGGL(k_mirror, dim3(nt, nt), dim3(256), 0, s, S, p);
+}
+void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s) {
+    const size_t total = (size_t)d.G * d.NP * KP;
+    const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_eta, dim3(grid), dim3(256), 0, s, d, b.X, b.Z, eta_out);
+}
+void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,
+                     int64_t count, double *out, hipStream_t s) {
+    const int grid = (int)std::min<int64_t>((count + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_rng_fill, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, seed, kind, shape, site,
+                       shard, iter, count, out);
+}
+
+}  // namespace dcfm

@@ -1,0 +1,176 @@
+"""Handle wrapper around the C ABI: the hot loop of divideconquer.m (dc:90-197).
+
+Arrays cross the boundary in the reference's MATLAB shapes and column-major
+order (``Lambda`` P x K x g_local, ``Yd`` n x P x g_local, ``delta`` K x 1 x g,
+...), exactly as a MEX gateway would pass them.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+
+STATE_FIELDS = ("Lambda", "ps", "omega", "psi", "Plam", "X", "Z", "eta", "delta", "tauh")
+
+
+@dataclass(frozen=True)
+class Hyper:
+    """dc:62-65 (hard-coded in the reference)."""
+    as_: float = 1.0
+    bs: float = 0.3
+    df: float = 3.0
+    ad1: float = 2.0
+    bd1: float = 1.0
+    ad2: float = 2.0
+    bd2: float = 1.0
+
+
+def _f64F(a) -> np.ndarray:
+    return np.asfortranarray(np.asarray(a, dtype=np.float64))
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class Sampler:
+    """One rank's handle: shards [rank*g_local, (rank+1)*g_local) of a chain."""
+
+    def __init__(self, n, P, g, K, rho, burnin, mcmc, thin, *, hyper: Hyper = Hyper(), seed=0,
+                 nranks=1, rank=0, device=0, inject_draws=False, asm_batch=0):
+        self.lib = _abi.load_library()
+        cfg = _abi.DcfmConfig()
+        cfg.n, cfg.P, cfg.g, cfg.K = int(n), int(P), int(g), int(K)
+        cfg.rho = float(rho)
+        cfg.burnin, cfg.mcmc, cfg.thin = int(burnin), int(mcmc), int(thin)
+        cfg.as_, cfg.bs, cfg.df = hyper.as_, hyper.bs, hyper.df
+        cfg.ad1, cfg.bd1, cfg.ad2, cfg.bd2 = hyper.ad1, hyper.bd1, hyper.ad2, hyper.bd2
+        cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        cfg.nranks, cfg.rank, cfg.device = int(nranks), int(rank), int(device)
+        cfg.flags = _abi.DCFM_FLAG_INJECT_DRAWS if inject_draws else 0
+        cfg.asm_batch = int(asm_batch)
+        self.cfg = cfg
+        h = C.c_void_p()
+        rc = self.lib.dcfm_create(C.byref(cfg), C.byref(h))
+        _abi.check(self.lib, None, rc)
+        self.h = h
+        self.n, self.P, self.g, self.K = cfg.n, cfg.P, cfg.g, cfg.K
+        self.nranks, self.rank = cfg.nranks, cfg.rank
+        self.g_local = self.g // self.nranks
+        self.shard0 = self.rank * self.g_local
+
+    # -- lifecycle -------------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.dcfm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        _abi.check(self.lib, self.h, rc)
+
+    # -- multi-rank -------------------------------------------------------------
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = _abi.load_library()
+        buf = (C.c_uint8 * 128)()
+        _abi.check(lib, None, lib.dcfm_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._check(self.lib.dcfm_comm_init(self.h, buf))
+
+    # -- inputs ----------------------------------------------------------------
+    def set_data(self, Yd_local):
+        Y = _f64F(Yd_local)
+        if Y.shape != (self.n, self.P, self.g_local):
+            raise ValueError(f"Yd_local must be n x P x g_local = {(self.n, self.P, self.g_local)}, got {Y.shape}")
+        self._check(self.lib.dcfm_set_data(self.h, _ptr(Y)))
+
+    def _shapes(self):
+        n, P, K, gl, g = self.n, self.P, self.K, self.g_local, self.g
+        return {"Lambda": (P, K, gl), "ps": (P, 1, gl), "omega": (P, gl), "psi": (P, K, gl),
+                "Plam": (P, K, gl), "X": (n, K), "Z": (n, K, gl), "eta": (n, K, gl),
+                "delta": (K, 1, g), "tauh": (K, 1, g)}
+
+    def set_state(self, state: dict):
+        """state: MATLAB-shaped arrays; local shards for per-shard fields, all g for delta/tauh."""
+        shapes = self._shapes()
+        keep = []
+        view = _abi.DcfmStateView()
+        for f in STATE_FIELDS:
+            if f == "eta":
+                continue
+            a = _f64F(state[f])
+            if a.size != int(np.prod(shapes[f])):
+                raise ValueError(f"{f}: expected shape {shapes[f]}, got {a.shape}")
+            keep.append(a)
+            setattr(view, f, _ptr(a))
+        self._check(self.lib.dcfm_set_state(self.h, C.byref(view)))
+
+    def set_draws(self, draws: dict, first_iter: int, n_iter: int):
+        """draws: full-g arrays NZ (K,n,g,T), NX (K,n,T), NL (K,P,g,T), Gpsi (P,K,g,T),
+        Gdelta (K,g,T), Gps (P,g,T) — the layout of oracle.IterDraws.stacked()."""
+        view = _abi.DcfmDrawsView()
+        keep = []
+        for f in ("NZ", "NX", "NL", "Gpsi", "Gdelta", "Gps"):
+            a = _f64F(draws[f])
+            keep.append(a)
+            setattr(view, f, _ptr(a))
+        self._check(self.lib.dcfm_set_draws(self.h, C.byref(view), int(first_iter), int(n_iter)))
+
+    # -- hot loop ----------------------------------------------------------------
+    def run(self, first_iter: int, n_iter: int):
+        self._check(self.lib.dcfm_run(self.h, int(first_iter), int(n_iter)))
+
+    def synchronize(self):
+        self._check(self.lib.dcfm_synchronize(self.h))
+
+    # -- outputs -------------------------------------------------------------------
+    def get_state(self, fields=STATE_FIELDS) -> dict:
+        shapes = self._shapes()
+        out = {f: np.zeros(shapes[f], dtype=np.float64, order="F") for f in fields}
+        view = _abi.DcfmStateView()
+        for f, a in out.items():
+            setattr(view, f, _ptr(a))
+        self._check(self.lib.dcfm_get_state(self.h, C.byref(view)))
+        return out
+
+    def get_sigma(self) -> np.ndarray:
+        p = self.P * self.g
+        S = np.zeros((p, p), dtype=np.float64, order="F")
+        self._check(self.lib.dcfm_get_sigma(self.h, _ptr(S)))
+        return S
+
+    def saved_samples(self) -> int:
+        return int(self.lib.dcfm_saved_samples(self.h))
+
+    # -- measurement -----------------------------------------------------------------
+    def set_profiling(self, on: bool):
+        self._check(self.lib.dcfm_set_profiling(self.h, 1 if on else 0))
+
+    def kernel_stats(self) -> dict:
+        ms = (C.c_double * _abi.K_COUNT)()
+        cnt = (C.c_int64 * _abi.K_COUNT)()
+        self._check(self.lib.dcfm_get_kernel_stats(self.h, ms, cnt))
+        return {name: (ms[i], cnt[i]) for name, i in _abi.KERNEL_IDS.items()}
+
+
+def rng_fill(kind: str, count: int, *, seed=0, shape=1.0, site=15, shard=0, iteration=0, device=0):
+    """On-device Philox variates exactly as the sweep draws them (diagnostic)."""
+    lib = _abi.load_library()
+    out = np.zeros(int(count), dtype=np.float64)
+    k = {"normal": 0, "gamma": 1}[kind]
+    rc = lib.dcfm_rng_fill(int(device), int(seed), k, float(shape), int(site), int(shard),
+                           int(iteration), int(count), _ptr(out))
+    _abi.check(lib, None, rc)
+    return out

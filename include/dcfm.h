@@ -1,0 +1,165 @@
+/*
+ * dcfm.h — C ABI of the MI355X-native Gibbs sweep + covariance assembly for the
+ * divide-and-conquer sparse latent-factor model (Sabnis & Pati, arXiv 1612.02875).
+ *
+ * Drop-in boundary.  The reference has no plugin or operator
+ * API: its only interface is the MATLAB function
+ *     Sigmaout = divideconquer(Y,g,k,BURNIN,MCMC,thin,rho)      (divideconquer.m:1)
+ * and the boundary sits INSIDE it, between the driver (dc:29-87: zero-column
+ * removal, partition, standardisation, hyper-parameters, initial draws) and the
+ * iteration loop (dc:90-197).  These entry points take over exactly the loop's
+ * read/write set; a MEX gateway or the Python host twin
+ * (package ``dcfm_amd``, ctypes) calls them.
+ *
+ * Conventions
+ *  - Plain C, no exceptions cross the ABI.  Every int-returning call returns
+ *    DCFM_OK (0) or a DCFM_ERR_* code; dcfm_last_error() gives the message.
+ *  - Host arrays are MATLAB column-major with the reference's shapes (so a MEX
+ *    gateway passes mxGetPr/mxGetDoubles pointers straight through).  The
+ *    caller owns every host buffer; the library copies and never keeps a
+ *    caller pointer.
+ *  - "local" arrays cover the shards this rank owns: global shards
+ *    [shard0, shard0 + g_local) with g_local = g / nranks, shard0 = rank*g_local.
+ *  - A handle is not thread-safe.  One process (one host thread) per GPU.
+ *  - dcfm_run is asynchronous w.r.t. the host (work is queued on the handle's
+ *    HIP stream); dcfm_get_*, dcfm_synchronize block.
+ */
+#ifndef DCFM_H
+#define DCFM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCFM_ABI_VERSION 1
+
+/* status codes */
+#define DCFM_OK              0
+#define DCFM_ERR_INVALID     1   /* bad argument / shape / call order            */
+#define DCFM_ERR_UNSUPPORTED 2   /* valid for the reference, not yet built here  */
+#define DCFM_ERR_HIP         3   /* HIP runtime error (incl. no device)          */
+#define DCFM_ERR_RCCL        4   /* RCCL error                                   */
+#define DCFM_ERR_NUMERIC     5   /* non-finite state detected                    */
+#define DCFM_ERR_ALLOC       6   /* device or host allocation failed             */
+
+/* dcfm_config.flags */
+#define DCFM_FLAG_INJECT_DRAWS 0x1u  /* read standard variates from dcfm_set_draws
+                                        buffers instead of on-device Philox        */
+
+typedef struct dcfm_handle dcfm_handle;
+
+/* Replaces the scalars the loop reads: dc:41 (P, K), dc:45 (N, effsamp),
+ * dc:62-65 (hyper-parameters), plus build-side placement and RNG settings. */
+typedef struct {
+    int32_t n;          /* observations (rows of Y), dc:30                       */
+    int32_t P;          /* variables per shard, P = p/g, dc:41                   */
+    int32_t g;          /* total number of shards (groups), dc:1                 */
+    int32_t K;          /* factors per shard, K = k/g, dc:41                     */
+    double  rho;        /* correlation of the shared factor, dc:1                */
+    int64_t burnin;     /* BURNIN, dc:1                                          */
+    int64_t mcmc;       /* MCMC, dc:1;  effsamp = mcmc/thin (dc:45, quirk Q8)    */
+    int64_t thin;       /* thin, dc:1                                            */
+    double  as_, bs, df, ad1, bd1, ad2, bd2;  /* dc:62-65 (1,0.3,3,2,1,2,1)      */
+    uint64_t seed;      /* Philox key (counter-based RNG; ignored with INJECT)   */
+    int32_t nranks;     /* ranks sharing the chain (1 = single GPU)              */
+    int32_t rank;       /* this rank                                             */
+    int32_t device;     /* HIP device ordinal this handle runs on                */
+    uint32_t flags;     /* DCFM_FLAG_*                                           */
+    int32_t asm_batch;  /* saved samples per covariance-assembly flush (0 = 16)  */
+    int32_t reserved[7];
+} dcfm_config;
+
+/* Sampler state (dc:69-87, updated by dc:90-177).  All column-major.
+ * NULL members are skipped by get, and are an error for set unless noted. */
+typedef struct {
+    double *Lambda;  /* P x K x g_local   loadings                  (dc:70,144) */
+    double *ps;      /* P x 1 x g_local   residual precisions       (dc:69,170) */
+    double *omega;   /* P x g_local       diag(Omega) (Q1: = ps at init,
+                                          = 1./ps after dc:171)                 */
+    double *psi;     /* P x K x g_local   psijh                     (dc:73,150) */
+    double *Plam;    /* P x K x g_local   loading precisions        (dc:77,176) */
+    double *X;       /* n x K             shared factor, replicated (dc:71,128) */
+    double *Z;       /* n x K x g_local   shard factors             (dc:71,106) */
+    double *eta;     /* n x K x g_local   get only; set ignores it (Q12)        */
+    double *delta;   /* K x 1 x g         ALL shards (replicated)   (dc:74,163) */
+    double *tauh;    /* K x 1 x g         ALL shards (replicated)   (dc:76,163) */
+} dcfm_state_view;
+
+/* Injected standard variates, ALL shards, column-major,
+ * one trailing iteration dimension of length n_iter:
+ *   NZ K x n x g x T (dc:104)   NX K x n x T (dc:126)   NL K x P x g x T (dc:142)
+ *   Gpsi P x K x g x T  standard gamma, shape df/2+0.5       (dc:150)
+ *   Gdelta K x g x T    shape ad1+P*K/2 (h=1), ad2+P*(K-h+1)/2 (dc:158,163)
+ *   Gps P x g x T       shape as+n/2                           (dc:170)     */
+typedef struct {
+    const double *NZ, *NX, *NL, *Gpsi, *Gdelta, *Gps;
+} dcfm_draws_view;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+int  dcfm_create(const dcfm_config *cfg, dcfm_handle **out);
+void dcfm_destroy(dcfm_handle *h);
+const char *dcfm_last_error(const dcfm_handle *h);   /* h may be NULL */
+int  dcfm_abi_version(void);
+
+/* ---- multi-rank: RCCL communicator over xGMI ----------------------------
+ * Rank 0 calls dcfm_comm_unique_id, the host broadcasts the 128 bytes
+ * (torch.distributed / MPI / files — any side channel), every rank calls
+ * dcfm_comm_init.  Not needed when nranks == 1. */
+int  dcfm_comm_unique_id(uint8_t out[128]);
+int  dcfm_comm_init(dcfm_handle *h, const uint8_t id[128]);
+
+/* ---- inputs -------------------------------------------------------------- */
+/* Yd(:,:,shard0+1 : shard0+g_local) after dc:48-59, n x P x g_local.        */
+int  dcfm_set_data(dcfm_handle *h, const double *Yd_local);
+int  dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s);
+/* Draws for iterations first_iter .. first_iter+n_iter-1 (1-based, as iter). */
+int  dcfm_set_draws(dcfm_handle *h, const dcfm_draws_view *d, int64_t first_iter, int64_t n_iter);
+
+/* ---- the hot loop (dc:90-197) ------------------------------------------- */
+/* Runs iterations first_iter .. first_iter+n_iter-1 (1-based).  Saved
+ * iterations (mod(iter,thin)==0 && iter>burnin, dc:180) feed the covariance
+ * assembly (dc:182-195); pending saved samples are flushed before return.   */
+int  dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter);
+int  dcfm_synchronize(dcfm_handle *h);
+
+/* ---- outputs ------------------------------------------------------------ */
+int  dcfm_get_state(dcfm_handle *h, dcfm_state_view *out);
+/* Sigmaout, p x p (p = P*g), symmetric, in the reference's permuted and
+ * standardised coordinates (dc:186-195, quirk Q7).  Collective when
+ * nranks > 1: every rank must call it; every rank receives the full matrix. */
+int  dcfm_get_sigma(dcfm_handle *h, double *out);
+int64_t dcfm_saved_samples(const dcfm_handle *h);
+
+/* ---- measurement --------------------------------------------------------- */
+/* Per-kernel HIP-event timing on the handle's stream (off by default).
+ * Kernel ids: DCFM_K_* below.  Times are accumulated device milliseconds. */
+#define DCFM_K_PREP     0
+#define DCFM_K_WPASS    1
+#define DCFM_K_ZDRAW    2
+#define DCFM_K_XRED     3
+#define DCFM_K_XDRAW    4
+#define DCFM_K_CPASS    5
+#define DCFM_K_LAMBDA   6
+#define DCFM_K_COLSUM   7
+#define DCFM_K_DELTA    8
+#define DCFM_K_SAVE     9
+#define DCFM_K_ASSEMBLE 10
+#define DCFM_K_COMM     11
+#define DCFM_K_COUNT    12
+int  dcfm_set_profiling(dcfm_handle *h, int enable);
+int  dcfm_get_kernel_stats(dcfm_handle *h, double ms[DCFM_K_COUNT], int64_t launches[DCFM_K_COUNT]);
+const char *dcfm_kernel_name(int id);
+
+/* ---- diagnostics (RNG statistical tests) --------------------------------
+ * Fills out[0..count) with on-device Philox variates exactly as the sweep
+ * draws them: kind 0 = standard normal, kind 1 = standard gamma(shape).
+ * Variate i uses counter (site, shard, row = i / 32, k = i % 32, iter). */
+int  dcfm_rng_fill(int device, uint64_t seed, int kind, double shape, int32_t site,
+                   int32_t shard, int64_t iter, int64_t count, double *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCFM_H */
