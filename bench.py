@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Benchmark: Gibbs iterations/sec of the divide-and-conquer factor sampler at c3.
+
+Workload (BASELINE.json configs[2], the metric's configuration):
+  p = 19,968 (P = 312 x g = 64 shards), n = 1,000, K = 30 factors per shard
+  (k = 1,920), rho = 0.5, thin = 5.  burnin = 0 so covariance assembly (one
+  saved sample every 5 iterations, flushed in batches of 16) is inside the timed
+  region.  Synthetic sparse-factor data (seeded; no dataset ships with the
+  reference).  One "step" = one Gibbs iteration (divideconquer.m:90-197) of the
+  whole chain; with N GPUs the 64 shards are split N ways (strong scaling, RCCL
+  all-gathers over xGMI for the cross-shard exchanges).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "Gibbs iters/sec (node) at p=20k,n=1k,g=64; cov-assembly MFMA util %"
+FP64_MFMA_PEAK_TFLOPS = 78.6      # MI355X dense fp64 matrix (spec; = fp64 vector)
+HBM_PEAK_GBS = 8000.0             # MI355X HBM3E spec
+
+
+def synth_data(n, p, k0=10, sparsity=0.7, seed=20161209):
+    """Sparse-factor synthetic data: Y = F L0' + E."""
+    r = np.random.Generator(np.random.PCG64(seed))
+    L0 = r.standard_normal((p, k0))
+    L0[r.random((p, k0)) < sparsity] = 0.0
+    sig2 = r.uniform(0.2, 1.0, size=p)
+    F = r.standard_normal((n, k0))
+    return F @ L0.T + r.standard_normal((n, p)) * np.sqrt(sig2)[None, :]
+
+
+def algorithmic_work(kname, d, n_launch_samples):
+    """(flops, bytes, bound) per launch — the minimum the reference maths needs."""
+    n, P, K, G, p, nr = d["n"], d["P"], d["K"], d["G"], d["p"], d["nranks"]
+    if kname == "k_wpass":     # W_m = Y_m (w o L_m): one fp64 read of Y, L, w; write W
+        return 2.0 * G * n * P * K, 8.0 * (G * n * P + G * P * (K + 1) + G * n * K), "hbm"
+    if kname == "k_cpass":     # [C|E] = [Y|eta]' eta: read Y, X, Z; write C, E
+        return 2.0 * G * n * (P + K) * K, 8.0 * (G * n * P + n * K + G * n * K + G * P * K), "hbm"
+    if kname == "k_assemble":  # lower triangle of sum_s coef.(L_s L_s') over the batch
+        return float(p) * (p + 1) * n_launch_samples * K / nr, 16.0 * p * (p + 1) / 2 / nr, "mfma"
+    if kname == "k_lambda":
+        return G * P * (K ** 3 / 3.0 + 6.0 * K * K), 8.0 * G * P * (4 * K + 4), "mfma"
+    if kname == "k_zdraw":
+        return G * n * (4.0 * K * K + 2.0 * K * K), 8.0 * G * n * 4 * K, "hbm"
+    return 0.0, 0.0, "hbm"
+
+
+def cpu_baseline_run(n, p, g, K, rho, steps=5, thin=5):
+    """Vectorised NumPy restatement (oracle, 'port') on a bounded c3 sample."""
+    import oracle
+    from oracle import dc_oracle as F
+    from oracle import vectorised as V
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max((i.get("num_threads", 1) for i in threadpool_info()), default=1)
+    except Exception:
+        cores = os.cpu_count() or 1
+    Y = synth_data(n, p)
+    hyper = F.Hyper()
+    Yk, n, pk, P, K_, keep = F.preprocess(Y, g, K * g)
+    src = oracle.DrawSource(1, n, pk, g, K, hyper)
+    init = src.init()
+    Yd = F.standardize(F.partition(Yk, g, init.varind))
+    st = F.initialise(n, P, K, g, rho, hyper, init)
+    draws = [src.iteration(t) for t in range(1, steps + 1)]
+    D = V.Data(Yd)
+    t0 = time.perf_counter()
+    V.run_chain(D, st, rho, hyper, lambda it: draws[it - 1], 1, steps, 0, steps, thin)
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "iter/s", "cores": int(cores), "kind": "port",
+            "sample": f"{steps} Gibbs iterations of c3 (incl. {steps // thin} covariance assembly at thin={thin}), "
+                      f"vectorised NumPy/OpenBLAS restatement of divideconquer.m:90-196 (not MATLAB), {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--thin", type=int, default=5)
+    ap.add_argument("--asm-batch", type=int, default=16)
+    ap.add_argument("--g", type=int, default=64)
+    ap.add_argument("--P", type=int, default=312)
+    ap.add_argument("--n", type=int, default=1000)
+    ap.add_argument("--K", type=int, default=30)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=10)
+    ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")    # rendezvous + timing only; data path is RCCL in libdcfm
+
+    import __graft_entry__ as ge
+    dcfm = ge.load_package()
+
+    g, P, n, K, rho, thin = args.g, args.P, args.n, args.K, 0.5, args.thin
+    p = g * P
+    N = args.warmup + args.steps
+    burnin, mcmc = 0, N
+    Y = synth_data(n, p)
+    hyper = dcfm.Hyper()
+    Yk, n, pk, P, K_, keep = dcfm.preprocess(Y, g, K * g)
+    init = dcfm.driver._HostInitDraws(1, n, pk, g, K, hyper)
+    Yd = dcfm.partition_standardize(Yk, g, init.varind)
+    state = dcfm.initial_state(n, P, K, g, rho, hyper, init)
+    gl = g // world
+    s0 = rank * gl
+
+    smp = dcfm.Sampler(n, P, g, K, rho, burnin, mcmc, thin, seed=1, nranks=world, rank=rank,
+                       device=local_rank, asm_batch=args.asm_batch)
+    if world > 1:
+        obj = [dcfm.Sampler.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        smp.comm_init(obj[0])
+    smp.set_data(Yd[:, :, s0:s0 + gl])
+    smp.set_state(dcfm.local_state(state, s0, gl))
+    del Y, Yk, Yd
+
+    have_torch_gpu = torch.cuda.is_available()
+    def sync():
+        smp.synchronize()
+        if have_torch_gpu:
+            torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    smp.run(1, args.warmup)
+    sync()
+    if not args.no_profile:
+        smp.set_profiling(True)
+    barrier(); sync()
+    t0 = time.perf_counter()
+    smp.run(args.warmup + 1, args.steps)
+    sync(); barrier()
+    dt = time.perf_counter() - t0
+    stats = smp.kernel_stats() if not args.no_profile else {}
+    saved_in_region = sum(1 for t in range(args.warmup + 1, N + 1) if t % thin == 0)
+    smp.close()
+
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    value = args.steps / dt
+    d = {"n": n, "P": P, "K": K, "G": gl, "p": p, "nranks": world}
+    kern = {}
+    roof = None
+    if stats:
+        for name, (ms, cnt) in stats.items():
+            if cnt == 0:
+                continue
+            avg_s = ms / cnt / 1e3
+            if name == "k_assemble":
+                nflush = cnt
+                samples_per = saved_in_region / max(nflush, 1)
+                fl, by, bound = algorithmic_work(name, d, samples_per)
+            else:
+                fl, by, bound = algorithmic_work(name, d, 0)
+            kern[name] = {"ms_total": round(ms, 4), "launches": int(cnt), "avg_us": round(avg_s * 1e6, 2),
+                          "gflops_per_launch": round(fl / 1e9, 4), "mb_per_launch": round(by / 1e6, 3),
+                          "tflops": round(fl / avg_s / 1e12, 3) if avg_s > 0 else None,
+                          "gbs": round(by / avg_s / 1e9, 1) if avg_s > 0 else None, "bound": bound}
+        dom = max((k for k in kern if k != "rccl"), key=lambda k: kern[k]["ms_total"])
+        kd = kern[dom]
+        if kd["bound"] == "mfma":
+            ach, peak, unit = kd["tflops"], FP64_MFMA_PEAK_TFLOPS, "TFLOP/s"
+        else:
+            ach, peak, unit = kd["gbs"], HBM_PEAK_GBS, "GB/s"
+        roof = {"kernel": dom, "bound": kd["bound"], "achieved": ach, "peak": peak, "unit": unit,
+                "frac": round(ach / peak, 4) if ach else None, "traffic": None,
+                "note": "achieved = algorithmic work per launch / mean HIP-event duration in the timed region"}
+
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "iter/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (sparse factor model, seed 20161209; random init via driver dc:68-87)",
+        "config": {"workload": f"c3: p={p} (P={P} x g={g}), n={n}, K={K} (k={K * g}), rho={rho}, "
+                               f"thin={thin}, burnin=0 (assembly in timed region), asm_batch={args.asm_batch}",
+                   "global_batch": n, "parallelism": f"shards{g}/gpus{world}"},
+        "roofline": roof,
+    }
+    if "k_assemble" in kern:
+        out["assembly_mfma_util"] = round(kern["k_assemble"]["tflops"] / FP64_MFMA_PEAK_TFLOPS, 4)
+    out["kernels"] = kern
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_run(n, p, g, K, rho, steps=args.cpu_steps, thin=thin)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -4,104 +4,115 @@ Same mathematics and quirks as :mod:`oracle.dc_oracle` (see its header and
 oracle/__init__.py: parity unpinned), batched over shards/rows so the host
 BLAS does the work.  Uses:
 
-* as a cross-check of the faithful loop (agreement to ~1e-12 relative);
-* as the ``cpu_baseline`` in bench.py ("port", not MATLAB): it is the
-  strongest CPU form of the reference algorithm we can time on the GPU box.
+* as a cross-check of the faithful loop (agreement to ~1e-12 relative), which
+  also checks the algebraic identities below (the HIP kernels use them too);
+* as the ``cpu_baseline`` in bench.py ("port", not MATLAB): the strongest CPU
+  form of the reference algorithm we can time on the GPU box.
 
-It operates on the same :class:`oracle.dc_oracle.SamplerState` (MATLAB shapes).
+Identities used (exact in real arithmetic; rounding-level differences only):
+  Zmsg' (Y_i - sqrt(rho) L X_i)  = W_i - sqrt(rho) A X_i           W = Y (w o L), A = (w o L)' L
+  sum_m Xmsg'(Y_i - sqrt(1-rho) L Z_i) = sum_m W_i - sqrt(1-rho) A' Z_i ... (A' = L'(w o L))
+  sum_i (Y_ij - eta_i L_j')^2 = yy_j - 2 L_j.C_j + L_j E L_j'      C = eta'Y, E = eta'eta
+  Sigma = rho L L' + (1-rho) blkdiag(L_r L_r') + diag(w)           (dc:184-192 block loop)
+
+It operates on the same :class:`oracle.dc_oracle.SamplerState` (MATLAB shapes);
+``Ys`` is the shard-major contiguous copy of Yd (g x n x P).
 """
 from __future__ import annotations
 
 import numpy as np
-from scipy.linalg import solve_triangular
+from scipy.linalg.blas import dsyrk
 
 from .dc_oracle import Hyper, SamplerState, matlab_cumprod_delta
 from .draws import IterDraws
 
 
-def _sym_upper(A):
-    return np.triu(A) + np.swapaxes(np.triu(A, 1), -1, -2)
+class Data:
+    """Yd in shard-major contiguous layout + per-column sums of squares."""
+
+    def __init__(self, Yd):
+        self.Yd = Yd
+        self.Ys = np.ascontiguousarray(np.moveaxis(Yd, 2, 0))        # g x n x P
+        self.yy = np.einsum("mij,mij->mj", self.Ys, self.Ys)          # g x P
 
 
-def _batched_tri_solve(L, B, lower: bool, trans: bool = False):
-    """Solve op(L) x = b for a stack of triangular L (..., K, K), b (..., K)."""
-    M = np.swapaxes(L, -1, -2) if trans else L
-    return np.linalg.solve(M, B[..., None])[..., 0]
+def _as_data(Yd):
+    return Yd if isinstance(Yd, Data) else Data(Yd)
 
 
-def update_Z(st: SamplerState, Yd, rho, d: IterDraws):
-    """dc:97-108, batched over rows."""
-    n, P, g = Yd.shape
+def _chol_upper_from_upper(A):
+    """cholcov on a stack (..., K, K): upper factor from the upper triangle."""
+    S = np.triu(A) + np.swapaxes(np.triu(A, 1), -1, -2)
+    return np.swapaxes(np.linalg.cholesky(S), -1, -2)
+
+
+def _solve(M, B):
+    return np.linalg.solve(M, B)
+
+
+def update_ZX(st: SamplerState, D: Data, rho, d: IterDraws):
+    """dc:97-129 (Z then X), Y read once for W."""
+    g, n, P = D.Ys.shape
     K = st.Lambda.shape[1]
-    for m in range(g):
-        Lam = st.Lambda[:, :, m]
-        Zmsg = Lam * st.omega[:, m][:, None]
-        Zprec = np.eye(K) + (1 - rho) * (Zmsg.T @ Lam)
-        R = np.linalg.cholesky(_sym_upper(Zprec)).T                       # cholcov: upper
-        Rz = Yd[:, :, m] - X_times(st.X, np.sqrt(rho) * Lam)             # n x P
-        bz = np.sqrt(1 - rho) * (Rz @ Zmsg)                              # n x K
-        vz = solve_triangular(R, bz.T, lower=False)                      # R \ b   (K x n)
-        mz = solve_triangular(R.T, vz, lower=True)                       # R' \ v  (Q2)
-        yz = solve_triangular(R.T, d.NZ[:, :, m], lower=True)
-        st.Z[:, :, m] = (mz + yz).T
-
-
-def X_times(X, LamScaled):
-    return X @ LamScaled.T
-
-
-def update_X(st: SamplerState, Yd, rho, d: IterDraws):
-    """dc:111-129, batched over rows (cross-shard sums kept)."""
-    n, P, g = Yd.shape
-    K = st.Lambda.shape[1]
-    LamW = st.Lambda * st.omega[:, None, :]                              # P x K x g
-    sumx1 = np.einsum("pkm,plm->kl", LamW, st.Lambda)
+    Lg = np.ascontiguousarray(np.moveaxis(st.Lambda, 2, 0))         # g x P x K
+    w = st.omega.T                                                   # g x P
+    Lw = Lg * w[:, :, None]                                          # Zmsg, dc:98
+    A = np.swapaxes(Lw, 1, 2) @ Lg                                   # g x K x K, dc:99
+    W = D.Ys @ Lw                                                    # g x n x K  (Y pass)
+    # Z (dc:99-107): R = cholcov(I + (1-rho) A), Z = R'\(R\bz + eps)
+    R = _chol_upper_from_upper(np.eye(K)[None] + (1 - rho) * A)
+    bz = np.sqrt(1 - rho) * (W - np.sqrt(rho) * (st.X[None] @ np.swapaxes(A, 1, 2)))   # g x n x K
+    v = _solve(R, np.swapaxes(bz, 1, 2))                             # g x K x n
+    eps = np.moveaxis(d.NZ, 2, 0)                                    # g x K x n
+    Z = _solve(np.swapaxes(R, 1, 2), v + eps)                        # g x K x n
+    st.Z[...] = np.moveaxis(np.swapaxes(Z, 1, 2), 0, 2)
+    # X (dc:112-128)
+    Zg = np.swapaxes(Z, 1, 2)                                        # g x n x K
+    sumx1 = A.sum(axis=0)
     Xprec = g * np.eye(K) + rho * sumx1
-    R = np.linalg.cholesky(_sym_upper(Xprec)).T
-    sumx2 = np.zeros((n, K))
-    for m in range(g):
-        Rx = Yd[:, :, m] - st.Z[:, :, m] @ (np.sqrt(1 - rho) * st.Lambda[:, :, m]).T
-        sumx2 += Rx @ LamW[:, :, m]
+    Rx = _chol_upper_from_upper(Xprec)
+    sumx2 = (W - np.sqrt(1 - rho) * (Zg @ np.swapaxes(A, 1, 2))).sum(axis=0)   # n x K
     bx = np.sqrt(rho) * sumx2
-    vx = solve_triangular(R, bx.T, lower=False)
-    mx = solve_triangular(R.T, vx, lower=True)
-    yx = solve_triangular(R.T, d.NX, lower=True)
-    st.X[:, :] = (mx + yx).T
+    vx = np.linalg.solve(Rx, bx.T)
+    st.X[...] = np.linalg.solve(Rx.T, vx + d.NX).T
 
 
 def update_eta(st: SamplerState, rho):
     st.eta[...] = np.sqrt(rho) * st.X[:, :, None] + np.sqrt(1 - rho) * st.Z
 
 
-def update_Lambda(st: SamplerState, Yd, d: IterDraws):
-    """dc:136-146, all rows of all shards in one batched Cholesky."""
-    n, P, g = Yd.shape
+def update_Lambda_psi_delta_ps(st: SamplerState, D: Data, hyper: Hyper, d: IterDraws):
+    """dc:136-172 batched; SS_j by the identity (no residual pass over Y)."""
+    g, n, P = D.Ys.shape
     K = st.Lambda.shape[1]
-    E = np.einsum("nkm,nlm->mkl", st.eta, st.eta)                       # g x K x K
-    C = np.einsum("nkm,npm->mpk", st.eta, Yd)                           # g x P x K
-    ps = st.ps[:, 0, :].T                                               # g x P
+    eta = np.ascontiguousarray(np.moveaxis(st.eta, 2, 0))          # g x n x K
+    E = np.swapaxes(eta, 1, 2) @ eta                                 # g x K x K, dc:138
+    C = np.swapaxes(D.Ys, 1, 2) @ eta                                # g x P x K  (Y pass)
+    ps = st.ps[:, 0, :].T                                            # g x P (previous it., Q11)
     Q = ps[:, :, None, None] * E[:, None, :, :]
     idx = np.arange(K)
-    Q[:, :, idx, idx] += np.moveaxis(st.Plam, 2, 0)                     # g x P x K
+    Q[:, :, idx, idx] += np.moveaxis(st.Plam, 2, 0)
     b = ps[:, :, None] * C
-    L = np.linalg.cholesky(Q)
-    v = _batched_tri_solve(L, b, lower=True)
-    mlam = _batched_tri_solve(L, v, lower=False, trans=True)
-    z = np.moveaxis(d.NL, (0, 1, 2), (2, 1, 0))                         # g x P x K
-    ylam = _batched_tri_solve(L, z, lower=False, trans=True)
-    st.Lambda[...] = np.moveaxis(ylam + mlam, 0, 2)
-
-
-def update_psi(st: SamplerState, hyper: Hyper, d: IterDraws):
-    tau = st.tauh[:, 0, :][None, :, :]                                  # 1 x K x g
-    scale = 1.0 / (hyper.df / 2 + 0.5 * (st.Lambda ** 2 * tau))
-    st.psi[...] = scale * d.Gpsi
+    L = np.linalg.cholesky(Q)                                        # dc:142
+    z = np.moveaxis(d.NL, (0, 1, 2), (2, 1, 0))                      # g x P x K
+    v = np.linalg.solve(L, b[..., None])[..., 0]
+    lam = np.linalg.solve(np.swapaxes(L, -1, -2), (v + z)[..., None])[..., 0]   # g x P x K
+    st.Lambda[...] = np.moveaxis(lam, 0, 2)
+    # psi (dc:150)
+    tau = st.tauh[:, 0, :][None, :, :]
+    st.psi[...] = (1.0 / (hyper.df / 2 + 0.5 * (st.Lambda ** 2 * tau))) * d.Gpsi
+    # delta / tau (dc:155-165)
+    update_delta_tau(st, hyper, d)
+    # ps (dc:169-171): SS = yy - 2 lam.C + lam E lam'
+    SS = D.yy - 2.0 * np.einsum("mjk,mjk->mj", lam, C) + np.einsum("mjk,mkl,mjl->mj", lam, E, lam)
+    st.ps[:, 0, :] = ((1.0 / (hyper.bs + 0.5 * SS)) * d.Gps.T).T
+    st.omega[...] = 1.0 / st.ps[:, 0, :]
 
 
 def update_delta_tau(st: SamplerState, hyper: Hyper, d: IterDraws):
-    """dc:154-165: the sequential chain is scalar work; kept as in the faithful loop."""
+    """dc:154-165: sequential scalar chain, kept as in the faithful loop (Q4, Q5)."""
     P, K, g = st.Lambda.shape
-    colsum = (st.psi * st.Lambda ** 2).sum(axis=0)                      # K x g
+    colsum = (st.psi * st.Lambda ** 2).sum(axis=0)                   # K x g
     delta, tauh = st.delta, st.tauh
     for m in range(g):
         cs = colsum[:, m]
@@ -114,53 +125,50 @@ def update_delta_tau(st: SamplerState, hyper: Hyper, d: IterDraws):
             tauh[:, :, m] = np.cumprod(delta[:, :, m], axis=0)
 
 
-def update_ps(st: SamplerState, Yd, hyper: Hyper, d: IterDraws):
-    n, P, g = Yd.shape
-    for m in range(g):
-        Ytil = Yd[:, :, m] - st.eta[:, :, m] @ st.Lambda[:, :, m].T
-        st.ps[:, 0, m] = (1.0 / (hyper.bs + 0.5 * np.einsum("ij,ij->j", Ytil, Ytil))) * d.Gps[:, m]
-    st.omega[...] = 1.0 / st.ps[:, 0, :]
-
-
 def update_Plam(st: SamplerState):
     st.Plam[...] = st.psi * st.tauh[:, 0, :][None, :, :]
 
 
 def gibbs_iteration(st: SamplerState, Yd, rho, hyper: Hyper, d: IterDraws):
-    update_Z(st, Yd, rho, d)
-    update_X(st, Yd, rho, d)
+    D = _as_data(Yd)
+    update_ZX(st, D, rho, d)
     update_eta(st, rho)
-    update_Lambda(st, Yd, d)
-    update_psi(st, hyper, d)
-    update_delta_tau(st, hyper, d)
-    update_ps(st, Yd, hyper, d)
+    update_Lambda_psi_delta_ps(st, D, hyper, d)
     update_Plam(st)
     return st
 
 
-def assemble_into(Sigmaout, st: SamplerState, rho, effsamp):
-    """dc:182-195 as one GEMM: rho*L*L' + (1-rho)*blkdiag(L_r L_r') + diag(omega)."""
+def assemble_lower(SigLower, st: SamplerState, rho, effsamp):
+    """dc:184-194 into the LOWER triangle of SigLower (Fortran order), via SYRK.
+
+    Sigmaout is symmetric by construction, so the dc:195 symmetrisation is the
+    identity here; the full matrix is lower + lower' - diag (see ``full``).
+    """
     P, K, g = st.Lambda.shape
-    L = np.moveaxis(st.Lambda, 2, 0).reshape(P * g, K)
-    Sigma = (rho * L) @ L.T
+    L = np.asfortranarray(np.moveaxis(st.Lambda, 2, 0).reshape(P * g, K))
+    SigLower[...] = dsyrk(rho / effsamp, L, beta=1.0, c=SigLower, lower=1, overwrite_c=1)
     for r in range(g):
         s = slice(r * P, (r + 1) * P)
         Lr = st.Lambda[:, :, r]
-        Sigma[s, s] = Lr @ Lr.T + np.diag(st.omega[:, r])
-    Sigmaout += Sigma / effsamp
-    Sigmaout += Sigmaout.T
-    Sigmaout *= 0.5
-    return Sigmaout
+        blk = ((1 - rho) / effsamp) * (Lr @ Lr.T) + np.diag(st.omega[:, r] / effsamp)
+        SigLower[s, s] += np.tril(blk)
+    return SigLower
+
+
+def full(SigLower):
+    return np.tril(SigLower) + np.tril(SigLower, -1).T
 
 
 def run_chain(Yd, st: SamplerState, rho, hyper: Hyper, draws, first_iter, n_iter,
-              burnin, mcmc, thin, Sigmaout=None):
-    n, P, g = Yd.shape
+              burnin, mcmc, thin, SigLower=None):
+    """Returns the lower-triangle accumulator (Fortran order); ``full()`` mirrors it."""
+    D = _as_data(Yd)
+    g, n, P = D.Ys.shape
     effsamp = mcmc / thin
-    if Sigmaout is None:
-        Sigmaout = np.zeros((P * g, P * g))
+    if SigLower is None:
+        SigLower = np.zeros((P * g, P * g), order="F")
     for it in range(first_iter, first_iter + n_iter):
-        gibbs_iteration(st, Yd, rho, hyper, draws(it))
+        gibbs_iteration(st, D, rho, hyper, draws(it))
         if it % thin == 0 and it > burnin:
-            Sigmaout = assemble_into(Sigmaout, st, rho, effsamp)
-    return Sigmaout
+            assemble_lower(SigLower, st, rho, effsamp)
+    return SigLower
