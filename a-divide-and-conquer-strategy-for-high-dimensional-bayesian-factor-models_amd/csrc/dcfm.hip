@@ -186,7 +186,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     d.G = c.g / nranks;
     d.shard0 = c.rank * d.G;
     d.NP = round_up(c.n, 16);
-    d.PP = round_up(c.P, 16);
+    d.PP = round_up(c.P, 32);
     d.p = c.P * c.g;
     d.rho = c.rho; d.sr = std::sqrt(c.rho); d.s1r = std::sqrt(1.0 - c.rho);
     d.as_ = c.as_; d.bs = c.bs; d.df = c.df; d.ad1 = c.ad1; d.bd1 = c.bd1; d.ad2 = c.ad2; d.bd2 = c.bd2;
@@ -214,7 +214,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     ALLOC(b.A, G * KP * KP);
     ALLOC(b.R, G * KP * KP);
     ALLOC(b.Rdi, G * KP);
-    ALLOC(b.Sp, ((G + 3) / 4) * NP * KP);
+    ALLOC(b.Sp, G * NP * KP);
     ALLOC(b.xin, (NP + KP) * KP);
     if (nranks > 1) { ALLOC(b.xall, (size_t)nranks * (NP + KP) * KP); } else b.xall = b.xin;
     ALLOC(b.C, G * PP * KP);

@@ -3,10 +3,10 @@
 // covariance assembly.  fp64 throughout (the reference is double precision).
 //
 // Kernel map (per iteration, in order)                         reference lines
-//   k_prep     A_m = Lambda' diag(w) Lambda, R_m = cholcov(I+(1-rho)A_m)   dc:98-100,114-115
+//   k_prep     A_m = Lambda' diag(w) Lambda (MFMA), R_m = cholcov(I+(1-rho)A_m)  dc:98-100,114-115
 //   k_wpass    W_m = Y_m (w o Lambda_m)           fp64 MFMA, Y pass 1      dc:102-103,122-123
-//   k_zdraw    Z rows: R\ , R'\ , noise; partial sum_m (W - s1r A Z')      dc:101-107,121-124
-//   k_xred     sum partials over local shards (+ sum_m A_m)                dc:112-116,120-124
+//   k_zdraw    Z rows: R\ , R'\ , noise; per-shard (W - s1r A Z')          dc:101-107,121-124
+//   k_xred     sum over local shards (+ sum_m A_m)                         dc:112-116,120-124
 //   [RCCL all-gather across ranks]
 //   k_xdraw    Xprec = gI + rho sum A, cholcov, X rows                     dc:117-128
 //   k_cpass    C_m = Y_m' eta_m, E_m = eta_m' eta_m  fp64 MFMA, Y pass 2   dc:133,138,141
@@ -42,10 +42,22 @@ __device__ __forceinline__ double readlane_d(double x, int l) {
     return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
+// value of x held by lane c of this lane's half-wave
+__device__ __forceinline__ double readsel(double x, int c, bool upper) {
+    const double lo = readlane_d(x, c);
+    const double hi = readlane_d(x, 32 + c);
+    return upper ? hi : lo;
+}
+
+// 1/sqrt(x) to full fp64 precision: hardware estimate + 2 Newton steps
+__device__ __forceinline__ double rsqrt_f64(double x) {
+    double y = __builtin_amdgcn_rsq(x);
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    for (int it = 0; it < 2; ++it) {
+        const double e = fma(-x * y, y, 1.0);
+        y = fma(0.5 * y, e, y);
+    }
+    return y;
 }
 
 // eta = sqrt(rho) X + sqrt(1-rho) Z    (dc:81,133) — one definition for every use
@@ -54,60 +66,94 @@ __device__ __forceinline__ double eta_of(double sr, double s1r, double x, double
 }
 
 // ----------------------------------------------------------------------------
-// small in-LDS Cholesky (lower, L L' = S), S is KP x KP with row stride KP+1,
-// executed by every thread of the block (nthreads >= 64).
+// Register Cholesky of a KP x KP SPD matrix per half-wave (32 lanes).
+// Lane r = lane & 31 holds row r in q[] (entries c <= r are read).  On return
+// q[c] = L[r][c] (0 for c > r) and the LDS image Lt[k][c] = L[c][k] (column k
+// of L, contiguous) with Lt[k][KP] = 1/L[k][k].  Right-looking; column k is
+// broadcast through LDS; the diagonal through readlane.  Both half-waves run
+// independent matrices (or the same one, writing identical values).
 // ----------------------------------------------------------------------------
-__device__ void lds_cholesky(double (*S)[KP + 1], int t, int nthreads) {
+constexpr int LS = KP + 2;
+
+__device__ __forceinline__ void chol_rows(double (&q)[KP], double (*Lt)[LS], int r, bool upper) {
+#pragma unroll
     for (int k = 0; k < KP; ++k) {
-        __syncthreads();
-        if (t == 0) S[k][k] = sqrt(S[k][k]);
-        __syncthreads();
-        if (t > k && t < KP) S[t][k] = S[t][k] / S[k][k];
-        __syncthreads();
-        for (int e = t; e < KP * KP; e += nthreads) {
-            const int r = e / KP, c = e % KP;
-            if (r > k && c > k && c <= r) S[r][c] -= S[r][k] * S[c][k];
-        }
+        const double dkk = readsel(q[k], k, upper);
+        const double ikk = rsqrt_f64(dkk);
+        const double lkk = dkk * ikk;
+        const double lrk = (r > k) ? q[k] * ikk : (r == k ? lkk : 0.0);
+        q[k] = lrk;
+        Lt[k][r] = lrk;
+        if (r == k) Lt[k][KP] = ikk;
+#pragma unroll
+        for (int c = k + 1; c < KP; ++c) q[c] -= lrk * Lt[k][c];
+        // keep the trailing update eager: without this hipcc sinks each FMA to
+        // the step that consumes q[c] and keeps O(K^2) loaded L values live
+#pragma unroll
+        for (int c = k + 1; c < KP; ++c) asm volatile("" : "+v"(q[c]));
     }
-    __syncthreads();
 }
 
 // ============================================================================
-// k_prep: A_m and R_m = cholcov(eye(K) + (1-rho) A_m)          dc:98-100
+// k_prep: A_m = (w o Lambda_m)' Lambda_m and R_m = cholcov(eye(K) + (1-rho) A_m)   dc:98-100
+// 4 waves split the j reduction (fp64 MFMA 2x2 tiles), LDS sum, wave 0 factors.
 // ============================================================================
 __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__ Lam,
                                               const double *__restrict__ omega,
                                               double *__restrict__ A, double *__restrict__ R,
                                               double *__restrict__ Rdi) {
-    __shared__ double S[KP][KP + 1];
+    __shared__ double part[4][KP][KP + 1];
+    __shared__ double Lt[KP][LS];
     const int m = blockIdx.x;
-    const int t = threadIdx.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 15, q = lane >> 4;
     const double *L = Lam + (size_t)m * d.PP * KP;
     const double *w = omega + (size_t)m * d.PP;
-    const int b = t & 31, ag = t >> 5;
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int j = 0; j < d.P; ++j) {
-        const double wj = w[j];
-        const double lb = L[j * KP + b];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] += (L[j * KP + ag + 8 * q] * wj) * lb;  // Zmsg'*Lambda
+    d4 a00 = {0, 0, 0, 0}, a01 = a00, a10 = a00, a11 = a00;
+    for (int t = wave; t < (d.PP >> 3); t += 4) {
+        const int j = 8 * t + 2 * q;
+        const d2 wj = *reinterpret_cast<const d2 *>(w + j);
+        const double lo0 = L[j * KP + r], hi0 = L[j * KP + 16 + r];
+        const double lo1 = L[(j + 1) * KP + r], hi1 = L[(j + 1) * KP + 16 + r];
+        // A operand (w_j Lambda_ja) [Zmsg, dc:98], B operand Lambda_jb
+        const double wl0 = lo0 * wj.x, wh0 = hi0 * wj.x, wl1 = lo1 * wj.y, wh1 = hi1 * wj.y;
+        a00 = mfma16x16x4(wl0, lo0, a00); a01 = mfma16x16x4(wl0, hi0, a01);
+        a10 = mfma16x16x4(wh0, lo0, a10); a11 = mfma16x16x4(wh0, hi0, a11);
+        a00 = mfma16x16x4(wl1, lo1, a00); a01 = mfma16x16x4(wl1, hi1, a01);
+        a10 = mfma16x16x4(wh1, lo1, a10); a11 = mfma16x16x4(wh1, hi1, a11);
     }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int a = q + 4 * g;
+        part[wave][a][r] = a00[g];
+        part[wave][a][16 + r] = a01[g];
+        part[wave][16 + a][r] = a10[g];
+        part[wave][16 + a][16 + r] = a11[g];
+    }
+    __syncthreads();
     double *Am = A + (size_t)m * KP * KP;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int a = ag + 8 * q;
-        Am[a * KP + b] = acc[q];
-        // cholcov reads the upper triangle (a <= b): lower factor of S with S[b][a] = Zprec[a][b]
-        if (a <= b) S[b][a] = (a == b ? 1.0 : 0.0) + (1.0 - d.rho) * acc[q];
+    for (int e = threadIdx.x; e < KP * KP; e += 256) {
+        const int a = e / KP, b = e % KP;
+        const double v = (part[0][a][b] + part[1][a][b]) + (part[2][a][b] + part[3][a][b]);
+        Am[e] = v;
+        part[0][a][b] = v;
     }
-    lds_cholesky(S, t, 256);
+    __syncthreads();
+    if (wave != 0) return;
+    // cholcov reads the upper triangle: S[rr][c] = Zprec[c][rr] for c <= rr
+    const int rr = lane & 31;
+    const bool upper = lane >= 32;
+    double qq[KP];
+#pragma unroll
+    for (int c = 0; c < KP; ++c)
+        qq[c] = (c <= rr) ? ((c == rr ? 1.0 : 0.0) + (1.0 - d.rho) * part[0][c][rr]) : 0.0;
+    chol_rows(qq, Lt, rr, upper);
     double *Rm = R + (size_t)m * KP * KP;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int a = ag + 8 * q;
-        Rm[a * KP + b] = (a <= b) ? S[b][a] : 0.0;   // R = L', upper, R'R = Zprec
+    for (int e = lane; e < KP * KP; e += 64) {
+        const int a = e / KP, b = e % KP;
+        Rm[e] = (b >= a) ? Lt[a][b] : 0.0;        // R = L', upper, R'R = Zprec
     }
-    if (t < KP) Rdi[(size_t)m * KP + t] = 1.0 / S[t][t];
+    if (lane < KP) Rdi[(size_t)m * KP + lane] = Lt[lane][KP];
 }
 
 // ============================================================================
@@ -153,11 +199,11 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
 }
 
 // ============================================================================
-// k_zdraw: per (row i, shard m), lane = row.                    dc:101-107,121-123
+// k_zdraw: per (row i, shard m), lane = row; one shard per block, A_m and R_m
+// broadcast from LDS.                                           dc:101-107,121-123
 //   bz = sqrt(1-rho) (W_i - sqrt(rho) A X_i)            (= sqrt(1-rho) Zmsg'(Y_i - sqrt(rho) L X_i))
 //   v  = R \ bz ;  Z_i = R' \ (v + eps)                 (quirk Q2 order)
-//   S_i += W_i - sqrt(1-rho) A Z_i                       (Xmsg'(Y_i - sqrt(1-rho) L Z_i))
-// 4 shards per block (one per wave), reduced in LDS -> Sp[blockIdx.y].
+//   Sp_m,i = W_i - sqrt(1-rho) A Z_i                     (Xmsg'(Y_i - sqrt(1-rho) L Z_i))
 // ============================================================================
 __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W,
                                                const double *__restrict__ A,
@@ -166,156 +212,147 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
                                                const double *__restrict__ X,
                                                double *__restrict__ Z, double *__restrict__ Sp,
                                                DrawsDev dr, int64_t iter) {
-    __shared__ double red[2][64][KP + 1];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int m = blockIdx.y * 4 + wave;
-    const int i = blockIdx.x * 64 + lane;
-    double s[KP];
-#pragma unroll
-    for (int k = 0; k < KP; ++k) s[k] = 0.0;
-    if (m < d.G && i < d.n) {
+    __shared__ double As[KP][KP], Rs[KP][KP], Rd[KP];
+    const int m = blockIdx.y;
+    {
         const double *Am = A + (size_t)m * KP * KP;
         const double *Rm = R + (size_t)m * KP * KP;
-        const double *Rd = Rdi + (size_t)m * KP;
-        const double *Wi = W + ((size_t)m * d.NP + i) * KP;
-        const double *Xi = X + (size_t)i * KP;
-        double x[KP], t[KP];
+        for (int e = threadIdx.x; e < KP * KP; e += 256) {
+            As[e / KP][e % KP] = Am[e];
+            Rs[e / KP][e % KP] = Rm[e];
+        }
+        if (threadIdx.x < KP) Rd[threadIdx.x] = Rdi[(size_t)m * KP + threadIdx.x];
+    }
+    __syncthreads();
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= d.NP) return;
+    double *Spi = Sp + ((size_t)m * d.NP + i) * KP;
+    if (i >= d.n) {
+#pragma unroll
+        for (int k = 0; k < KP; k += 2) *reinterpret_cast<d2 *>(Spi + k) = d2{0.0, 0.0};
+        return;
+    }
+    const double *Wi = W + ((size_t)m * d.NP + i) * KP;
+    const double *Xi = X + (size_t)i * KP;
+    double x[KP], t[KP];
+#pragma unroll
+    for (int k = 0; k < KP; k += 2) {
+        const d2 v = *reinterpret_cast<const d2 *>(Xi + k);
+        x[k] = v.x;
+        x[k + 1] = v.y;
+    }
+#pragma unroll
+    for (int a = 0; a < KP; ++a) {
+        double acc = 0.0;
+#pragma unroll
+        for (int b = 0; b < KP; ++b) acc += As[a][b] * x[b];
+        t[a] = d.s1r * (Wi[a] - d.sr * acc);
+    }
+    // back substitution R v = bz (R upper)
+#pragma unroll
+    for (int a = KP - 1; a >= 0; --a) {
+        double acc = t[a];
+#pragma unroll
+        for (int b = a + 1; b < KP; ++b) acc -= Rs[a][b] * t[b];
+        t[a] = acc * Rd[a];
+    }
+    // + eps  (dc:104 normrnd(0,1,[K,1]))
+    const int mg = d.shard0 + m;
+    if (d.inject) {
+        const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + i) * d.K;
+#pragma unroll
+        for (int k = 0; k < KP; ++k)
+            if (k < d.K) t[k] += nz[k];
+    } else {
+        const Rng rng(d.seed);
 #pragma unroll
         for (int k = 0; k < KP; k += 2) {
-            const d2 v = *reinterpret_cast<const d2 *>(Xi + k);
-            x[k] = v.x;
-            x[k + 1] = v.y;
-        }
-#pragma unroll
-        for (int a = 0; a < KP; ++a) {
-            double acc = 0.0;
-#pragma unroll
-            for (int b = 0; b < KP; ++b) acc += Am[a * KP + b] * x[b];
-            t[a] = d.s1r * (Wi[a] - d.sr * acc);
-        }
-        // back substitution R v = bz (R upper)
-#pragma unroll
-        for (int a = KP - 1; a >= 0; --a) {
-            double acc = t[a];
-#pragma unroll
-            for (int b = a + 1; b < KP; ++b) acc -= Rm[a * KP + b] * t[b];
-            t[a] = acc * Rd[a];
-        }
-        // + eps  (dc:104 normrnd(0,1,[K,1]))
-        const int mg = d.shard0 + m;
-        if (d.inject) {
-            const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + i) * d.K;
-#pragma unroll
-            for (int k = 0; k < KP; ++k)
-                if (k < d.K) t[k] += nz[k];
-        } else {
-            const Rng rng(d.seed);
-#pragma unroll
-            for (int k = 0; k < KP; k += 2) {
-                if (k < d.K) {
-                    double n0, n1;
-                    rng.normal2(SITE_Z, mg, i, k >> 1, (uint32_t)iter, n0, n1);
-                    t[k] += n0;
-                    if (k + 1 < d.K) t[k + 1] += n1;
-                }
+            if (k < d.K) {
+                double n0, n1;
+                rng.normal2(SITE_Z, mg, i, k >> 1, (uint32_t)iter, n0, n1);
+                t[k] += n0;
+                if (k + 1 < d.K) t[k + 1] += n1;
             }
         }
-        // forward substitution R' z = v + eps
-#pragma unroll
-        for (int a = 0; a < KP; ++a) {
-            double acc = t[a];
-#pragma unroll
-            for (int b = 0; b < a; ++b) acc -= Rm[b * KP + a] * t[b];
-            t[a] = acc * Rd[a];
-        }
-        double *Zi = Z + ((size_t)m * d.NP + i) * KP;
-#pragma unroll
-        for (int k = 0; k < KP; k += 2) {
-            d2 v;
-            v.x = (k < d.K) ? t[k] : 0.0;
-            v.y = (k + 1 < d.K) ? t[k + 1] : 0.0;
-            *reinterpret_cast<d2 *>(Zi + k) = v;
-        }
-#pragma unroll
-        for (int a = 0; a < KP; ++a) {
-            double acc = 0.0;
-#pragma unroll
-            for (int b = 0; b < KP; ++b) acc += Am[a * KP + b] * t[b];
-            s[a] = Wi[a] - d.s1r * acc;
-        }
     }
-    // deterministic 4-wave reduction: ((s0 + s2) + (s1 + s3))
-    if (wave >= 2) {
+    // forward substitution R' z = v + eps
 #pragma unroll
-        for (int k = 0; k < KP; ++k) red[wave - 2][lane][k] = s[k];
+    for (int a = 0; a < KP; ++a) {
+        double acc = t[a];
+#pragma unroll
+        for (int b = 0; b < a; ++b) acc -= Rs[b][a] * t[b];
+        t[a] = acc * Rd[a];
     }
-    __syncthreads();
-    if (wave < 2) {
+    double *Zi = Z + ((size_t)m * d.NP + i) * KP;
 #pragma unroll
-        for (int k = 0; k < KP; ++k) s[k] += red[wave][lane][k];
+    for (int k = 0; k < KP; k += 2) {
+        d2 v;
+        v.x = (k < d.K) ? t[k] : 0.0;
+        v.y = (k + 1 < d.K) ? t[k + 1] : 0.0;
+        *reinterpret_cast<d2 *>(Zi + k) = v;
     }
-    __syncthreads();
-    if (wave == 1) {
 #pragma unroll
-        for (int k = 0; k < KP; ++k) red[0][lane][k] = s[k];
-    }
-    __syncthreads();
-    if (wave == 0 && i < d.NP) {
-        double *o = Sp + ((size_t)blockIdx.y * d.NP + i) * KP;
+    for (int a = 0; a < KP; a += 2) {
+        double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
-        for (int k = 0; k < KP; k += 2) {
-            d2 v;
-            v.x = s[k] + red[0][lane][k];
-            v.y = s[k + 1] + red[0][lane][k + 1];
-            *reinterpret_cast<d2 *>(o + k) = v;
+        for (int b = 0; b < KP; ++b) {
+            acc0 += As[a][b] * t[b];
+            acc1 += As[a + 1][b] * t[b];
         }
+        d2 v;
+        v.x = Wi[a] - d.s1r * acc0;
+        v.y = Wi[a + 1] - d.s1r * acc1;
+        *reinterpret_cast<d2 *>(Spi + a) = v;
     }
 }
 
 // ============================================================================
-// k_xred: xin[i][k] = sum_q Sp[q][i][k];  xin[NP+a][b] = sum_m A_m[a][b]     dc:113-116,121-124
+// k_xred: xin[i][k] = sum_m Sp[m][i][k];  xin[NP+a][b] = sum_m A_m[a][b]     dc:113-116,121-124
 // ============================================================================
 __global__ __launch_bounds__(256) void k_xred(Dims d, const double *__restrict__ Sp,
                                               const double *__restrict__ A,
                                               double *__restrict__ xin) {
-    const int nq = (d.G + 3) >> 2;
     const size_t total = (size_t)(d.NP + KP) * KP;
-    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total;
-         e += (size_t)gridDim.x * blockDim.x) {
-        const size_t row = e / KP;
-        double acc = 0.0;
-        if (row < (size_t)d.NP) {
-            for (int q = 0; q < nq; ++q) acc += Sp[(size_t)q * d.NP * KP + e];
-        } else {
-            const size_t off = e - (size_t)d.NP * KP;
-            for (int m = 0; m < d.G; ++m) acc += A[(size_t)m * KP * KP + off];
-        }
-        xin[e] = acc;
+    const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const size_t row = e / KP;
+    double acc = 0.0;
+    if (row < (size_t)d.NP) {
+        const size_t stride = (size_t)d.NP * KP;
+#pragma unroll 8
+        for (int m = 0; m < d.G; ++m) acc += Sp[(size_t)m * stride + e];
+    } else {
+        const size_t off = e - (size_t)d.NP * KP;
+#pragma unroll 8
+        for (int m = 0; m < d.G; ++m) acc += A[(size_t)m * KP * KP + off];
     }
+    xin[e] = acc;
 }
 
 // ============================================================================
 // k_xdraw: X rows.  Xprec = g*I + rho*sum_m A_m (all ranks), Rx = cholcov,     dc:117-128
 //   X_i = Rx' \ (Rx \ (sqrt(rho) S_i) + eps)
-// one wave per 64 rows; every block factors the KxK Xprec itself (cheap).
+// one wave per 64 rows; every block factors the KxK Xprec itself (register Cholesky).
 // ============================================================================
 __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__ xall,
                                               double *__restrict__ X, DrawsDev dr, int64_t iter) {
-    __shared__ double S[KP][KP + 1];
-    __shared__ double Rd[KP];
-    const int t = threadIdx.x;
+    __shared__ double Lt[KP][LS];
+    const int lane = threadIdx.x;
+    const int rr = lane & 31;
+    const bool upper = lane >= 32;
     const size_t stride = (size_t)(d.NP + KP) * KP;
-    for (int e = t; e < KP * KP; e += 64) {
-        const int a = e / KP, b = e % KP;
-        double v = 0.0;
-        for (int rk = 0; rk < d.nranks; ++rk) v += xall[rk * stride + (size_t)(d.NP + a) * KP + b];
-        if (a <= b) S[b][a] = (a == b ? (double)d.g : 0.0) + d.rho * v;   // upper triangle (cholcov)
+    {
+        double qq[KP];
+#pragma unroll
+        for (int c = 0; c < KP; ++c) {
+            double v = 0.0;
+            if (c <= rr)
+                for (int rk = 0; rk < d.nranks; ++rk) v += xall[rk * stride + (size_t)(d.NP + c) * KP + rr];
+            qq[c] = (c <= rr) ? ((c == rr ? (double)d.g : 0.0) + d.rho * v) : 0.0;   // upper triangle
+        }
+        chol_rows(qq, Lt, rr, upper);
     }
-    lds_cholesky(S, t, 64);
-    if (t < KP) Rd[t] = 1.0 / S[t][t];
-    __syncthreads();
-    const int i = blockIdx.x * 64 + t;
+    const int i = blockIdx.x * 64 + lane;
     if (i >= d.n) return;
     double v[KP];
 #pragma unroll
@@ -323,17 +360,21 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
     for (int rk = 0; rk < d.nranks; ++rk) {
         const double *s = xall + rk * stride + (size_t)i * KP;
 #pragma unroll
-        for (int k = 0; k < KP; ++k) v[k] += s[k];
+        for (int k = 0; k < KP; k += 2) {
+            const d2 u = *reinterpret_cast<const d2 *>(s + k);
+            v[k] += u.x;
+            v[k + 1] += u.y;
+        }
     }
 #pragma unroll
     for (int k = 0; k < KP; ++k) v[k] = d.sr * v[k];     // bx = sqrt(rho)*sumx2
-    // Rx v' = bx (Rx[a][b] = S[b][a], upper)
+    // Rx v' = bx; Rx[a][b] = L[b][a] = Lt[a][b]
 #pragma unroll
     for (int a = KP - 1; a >= 0; --a) {
         double acc = v[a];
 #pragma unroll
-        for (int b = a + 1; b < KP; ++b) acc -= S[b][a] * v[b];
-        v[a] = acc * Rd[a];
+        for (int b = a + 1; b < KP; ++b) acc -= Lt[a][b] * v[b];
+        v[a] = acc * Lt[a][KP];
     }
     if (d.inject) {
         const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + i) * d.K;
@@ -352,73 +393,88 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
             }
         }
     }
+    // Rx' x = v + eps; Rx'[a][b] = Lt[b][a]
 #pragma unroll
     for (int a = 0; a < KP; ++a) {
         double acc = v[a];
 #pragma unroll
-        for (int b = 0; b < a; ++b) acc -= S[a][b] * v[b];
-        v[a] = acc * Rd[a];
+        for (int b = 0; b < a; ++b) acc -= Lt[b][a] * v[b];
+        v[a] = acc * Lt[a][KP];
     }
     double *Xi = X + (size_t)i * KP;
 #pragma unroll
-    for (int k = 0; k < KP; ++k) Xi[k] = (k < d.K) ? v[k] : 0.0;
+    for (int k = 0; k < KP; k += 2) {
+        d2 u;
+        u.x = (k < d.K) ? v[k] : 0.0;
+        u.y = (k + 1 < d.K) ? v[k + 1] : 0.0;
+        *reinterpret_cast<d2 *>(Xi + k) = u;
+    }
 }
 
 // ============================================================================
 // k_cpass: [C_m | E_m] = [Y_m | eta_m]' eta_m    fp64 MFMA, Y pass 2      dc:133,138,141
-// one wave = (shard m, 16-column tile of [Y | eta]) x 32 k, reduction over i.
+// block = (shard m, 32-column tile of [Y | eta]); its 4 waves split the
+// reduction over rows i (memory-level parallelism), partial 32x32 tiles summed
+// in LDS in a fixed order.  eta is formed on the fly from X and Z.
 // ============================================================================
 __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict__ Y,
                                                const double *__restrict__ X,
                                                const double *__restrict__ Z,
                                                double *__restrict__ C, double *__restrict__ E) {
+    __shared__ double red[4][32][33];
     const int m = blockIdx.y;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ntY = d.PP >> 4;
-    const int nt = blockIdx.x * 4 + wave;
-    if (nt >= ntY + KP / 16) return;
-    const bool isE = nt >= ntY;
-    const int c0 = isE ? (nt - ntY) * 16 : nt * 16;
+    const int c0 = blockIdx.x * 32;
+    const bool isE = c0 >= d.PP;
     const int r = lane & 15, q = lane >> 4;
     const double *Ym = Y + (size_t)m * d.NP * d.PP + c0 + r;
     const double *Zm = Z + (size_t)m * d.NP * KP;
-    d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-    const int ns = d.NP >> 2;
+    const int nsw = d.NP >> 4;                 // k-steps (4 rows each) per wave
+    const int s0 = wave * nsw;
+    d4 a00 = {0, 0, 0, 0}, a01 = a00, a10 = a00, a11 = a00;
 #pragma unroll 4
-    for (int s = 0; s < ns; ++s) {
+    for (int s = s0; s < s0 + nsw; ++s) {
         const int i = 4 * s + q;
         const double e0 = eta_of(d.sr, d.s1r, X[i * KP + r], Zm[i * KP + r]);
         const double e1 = eta_of(d.sr, d.s1r, X[i * KP + 16 + r], Zm[i * KP + 16 + r]);
-        const double a = isE ? (c0 == 0 ? e0 : e1) : Ym[(size_t)i * d.PP];
-        acc0 = mfma16x16x4(a, e0, acc0);
-        acc1 = mfma16x16x4(a, e1, acc1);
+        double y0, y1;
+        if (isE) {
+            y0 = e0;
+            y1 = e1;
+        } else {
+            y0 = Ym[(size_t)i * d.PP];
+            y1 = Ym[(size_t)i * d.PP + 16];
+        }
+        a00 = mfma16x16x4(y0, e0, a00);
+        a01 = mfma16x16x4(y0, e1, a01);
+        a10 = mfma16x16x4(y1, e0, a10);
+        a11 = mfma16x16x4(y1, e1, a11);
     }
-    double *out = isE ? (E + (size_t)m * KP * KP) : (C + (size_t)m * d.PP * KP);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-        const int row = c0 + q + 4 * g;
-        out[row * KP + r] = acc0[g];
-        out[row * KP + 16 + r] = acc1[g];
+        const int a = q + 4 * g;
+        red[wave][a][r] = a00[g];
+        red[wave][a][16 + r] = a01[g];
+        red[wave][16 + a][r] = a10[g];
+        red[wave][16 + a][16 + r] = a11[g];
+    }
+    __syncthreads();
+    double *out = isE ? (E + (size_t)m * KP * KP) : (C + ((size_t)m * d.PP + c0) * KP);
+    for (int e = threadIdx.x; e < 32 * KP; e += 256) {
+        const int a = e / KP, b = e % KP;
+        out[e] = (red[0][a][b] + red[1][a][b]) + (red[2][a][b] + red[3][a][b]);
     }
 }
 
 // ============================================================================
 // k_lambda: loading rows.  A half-wave (32 lanes) owns one row j; lane r holds
 // row r of Q_j = diag(Plam_j) + ps_j E_m in registers.        dc:140-145 (+150,156,169-171)
-//   L = chol(Q,'lower') right-looking, column k broadcast through LDS
+//   L = chol(Q,'lower') (chol_rows)
 //   v = L \ (ps_j C_j);  Lambda_j = L' \ (v + z)             (= ylam + mlam)
 //   psi_j  = Gpsi * 1/(df/2 + 0.5 lambda^2 tau)               (dc:150, tau of the previous it.)
 //   SS_j   = yy_j - 2 lambda.C_j + lambda' E lambda  ->  ps_j = Gps * 1/(bs + 0.5 SS_j), w = 1/ps
 // 8 rows per 256-thread block; per-block column sums of psi o lambda^2 -> cpart.
 // ============================================================================
-constexpr int LS = KP + 2;   // LDS row stride: column KP holds 1/l_kk
-
-__device__ __forceinline__ double readsel(double x, int c, bool upper) {
-    const double lo = readlane_d(x, c);
-    const double hi = readlane_d(x, 32 + c);
-    return upper ? hi : lo;
-}
-
 __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict__ C,
                                                 const double *__restrict__ E,
                                                 const double *__restrict__ yy,
@@ -441,7 +497,6 @@ __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict
     const bool valid = j < d.P;
     const bool real = r < d.K;
     const size_t rowoff = ((size_t)m * d.PP + (valid ? j : 0)) * KP;
-
     {
         const double *Em = E + (size_t)m * KP * KP;
         for (int e = threadIdx.x; e < KP * KP; e += 256) Es[e / KP][e % KP] = Em[e];
@@ -459,24 +514,8 @@ __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict
     const double cjr = valid ? C[rowoff + r] : 0.0;
     double bv = psj * cjr;
 
-    // --- Cholesky
     double (*Lt)[LS] = LT[hw];
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-        const double dkk = readsel(q[k], k, upper);
-        const double lkk = sqrt(dkk);
-        const double ikk = 1.0 / lkk;
-        const double lrk = (r > k) ? q[k] * ikk : (r == k ? lkk : 0.0);
-        q[k] = lrk;
-        Lt[k][r] = lrk;
-        if (r == k) Lt[k][KP] = ikk;
-#pragma unroll
-        for (int c = k + 1; c < KP; ++c) q[c] -= lrk * Lt[k][c];
-        // keep the trailing update eager: without this hipcc sinks each FMA to
-        // the step that consumes q[c] and keeps O(K^2) loaded L values live
-#pragma unroll
-        for (int c = k + 1; c < KP; ++c) asm volatile("" : "+v"(q[c]));
-    }
+    chol_rows(q, Lt, r, upper);
     // --- forward solve L v = b   (L[r][c] = Lt[c][r])
     double vr = 0.0;
 #pragma unroll 2
@@ -506,8 +545,7 @@ __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict
     }
     if (!real) xr = 0.0;
 
-    // --- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr
-    // broadcast x through LDS (reuse column KP+1 slot of each row: LT[h][r][KP+1])
+    // --- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr; x broadcast through LT[h][r][KP+1]
     Lt[r][KP + 1] = xr;
     double ex = 0.0;
 #pragma unroll
@@ -561,14 +599,21 @@ __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict
 // ============================================================================
 // k_colsum: sloc[m][k] = sum_b cpart[m][b][k]                               dc:156 sum(mat)
 // ============================================================================
-__global__ __launch_bounds__(64) void k_colsum(Dims d, const double *__restrict__ cpart,
-                                               double *__restrict__ sloc) {
-    const int m = blockIdx.x, k = threadIdx.x;
-    if (k >= KP) return;
+__global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict__ cpart,
+                                                double *__restrict__ sloc) {
+    __shared__ double part[8][KP];
+    const int m = blockIdx.x, k = threadIdx.x & 31, grp = threadIdx.x >> 5;
     const int nb = (d.P + 7) >> 3;
     double s = 0.0;
-    for (int b = 0; b < nb; ++b) s += cpart[((size_t)m * (d.PP >> 3) + b) * KP + k];
-    sloc[(size_t)m * KP + k] = s;
+    for (int b = grp; b < nb; b += 8) s += cpart[((size_t)m * (d.PP >> 3) + b) * KP + k];
+    part[grp][k] = s;
+    __syncthreads();
+    if (threadIdx.x < KP) {
+        double t = 0.0;
+#pragma unroll
+        for (int g2 = 0; g2 < 8; ++g2) t += part[g2][threadIdx.x];
+        sloc[(size_t)m * KP + threadIdx.x] = t;
+    }
 }
 
 // ============================================================================
@@ -577,6 +622,9 @@ __global__ __launch_bounds__(64) void k_colsum(Dims d, const double *__restrict_
 //           each block re-runs shard 1's chain first (deterministic, identical).
 //   K == 1: cumprod over the K x 1 x g array runs along shards (Q5):
 //           tau_used(m) = prod_{m'<m} delta_new(m') * delta_old(m).
+// The chain over h is scalar: with T_h = sum_{l>=h} tau_l s_l of the incoming
+// tau, the reference's recomputed cumprod gives dot_h = F_h T_h where
+// F_h = prod_{h'<h} delta_new(h')/delta_old(h')  (exact; rounding-level only).
 // grid = all g shards (delta/tau replicated on every rank); local blocks also
 // refresh Plam = psi o tau'.
 // ============================================================================
@@ -589,6 +637,15 @@ __device__ __forceinline__ double wave_scan_prod(double v, int l) {
     return v;
 }
 
+__device__ __forceinline__ double wave_suffix_sum(double v, int l) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_down(v, o, 64);
+        if (l + o < 64) v += u;
+    }
+    return v;
+}
+
 __device__ double delta_G(const Dims &d, const DrawsDev &dr, int64_t iter, int mg, int h) {
     if (d.inject) return dr.Gdelta[((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + h];
     const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - h);
@@ -596,24 +653,18 @@ __device__ double delta_G(const Dims &d, const DrawsDev &dr, int64_t iter, int m
     return rng.gamma(shape, SITE_DELTA, mg, 0, h, (uint32_t)iter);
 }
 
-// runs one shard's chain; lane l holds delta_l, tau_l, s_l, G_l (l < K)
-__device__ void delta_chain(const Dims &d, int l, double &dl, double &tl, double sl, double Gl,
-                            bool own, double d0new) {
-    const bool act = l < d.K;
-    double dot = wave_sum(act ? tl * sl : 0.0);
-    const double d_1 = readlane_d(dl, 0);
-    double bd = d.bd1 + (0.5 * (1.0 / d_1)) * dot;               // dc:157
-    const double g0 = readlane_d(Gl, 0);
-    if (l == 0) dl = (1.0 / bd) * g0;                             // dc:158
-    tl = wave_scan_prod(dl, l);                                   // dc:158 cumprod
-    for (int h = 1; h < d.K; ++h) {
-        dot = wave_sum((act && l >= h) ? tl * sl : 0.0);
-        const double dref = own ? readlane_d(dl, h) : readlane_d(d0new, h);   // delta(h) (Q4)
-        bd = d.bd2 + (0.5 * (1.0 / dref)) * dot;                  // dc:161
-        const double gh = readlane_d(Gl, h);
-        if (l == h) dl = (1.0 / bd) * gh;                         // dc:163
-        tl = wave_scan_prod(dl, l);
+// lane l < K holds delta_old_l, T_l, G_l, 1/delta_old_l and 1/dref_l; returns delta_new_l
+__device__ double delta_chain(const Dims &d, int l, double T, double G, double idold, double idref) {
+    double F = 1.0, dnew = 1.0;
+    for (int h = 0; h < d.K; ++h) {
+        const double Th = readlane_d(T, h), ih = readlane_d(idref, h);
+        const double ioh = readlane_d(idold, h), Gh = readlane_d(G, h);
+        const double bd = (h == 0 ? d.bd1 : d.bd2) + (0.5 * ih) * (F * Th);   // dc:157,161
+        const double dn = (1.0 / bd) * Gh;                                      // dc:158,163
+        if (l == h) dnew = dn;
+        F = F * (dn * ioh);
     }
+    return dnew;
 }
 
 __global__ __launch_bounds__(256) void k_delta(Dims d, const double *__restrict__ sall,
@@ -630,22 +681,26 @@ __global__ __launch_bounds__(256) void k_delta(Dims d, const double *__restrict_
     if (t < 64) {
         const int l = t;
         const int lk = l < KP ? l : 0;
+        const bool act = l < d.K;
         if (d.K >= 2) {
-            double G0 = (l < d.K) ? delta_G(d, dr, iter, 0, l) : 1.0;
-            double d0 = (l < KP) ? delta_in[lk] : 1.0;
-            double t0 = (l < KP) ? tau_in[lk] : 1.0;
-            const double s0 = (l < KP) ? sall[lk] : 0.0;
-            delta_chain(d, l, d0, t0, s0, G0, true, 0.0);
-            double dm = d0, tm = t0;
+            // shard 1 (index 0) with its own pre-update delta_h
+            const double d0 = act ? delta_in[lk] : 1.0;
+            const double T0 = wave_suffix_sum(act ? tau_in[lk] * sall[lk] : 0.0, l);
+            const double G0 = act ? delta_G(d, dr, iter, 0, l) : 1.0;
+            const double id0 = 1.0 / d0;
+            const double d0new = delta_chain(d, l, T0, G0, id0, id0);
+            double dm = d0new;
             if (m != 0) {
-                const double Gm = (l < d.K) ? delta_G(d, dr, iter, m, l) : 1.0;
-                dm = (l < KP) ? delta_in[(size_t)m * KP + lk] : 1.0;
-                tm = (l < KP) ? tau_in[(size_t)m * KP + lk] : 1.0;
-                const double sm = (l < KP) ? sall[(size_t)m * KP + lk] : 0.0;
-                delta_chain(d, l, dm, tm, sm, Gm, false, d0);
+                const size_t o = (size_t)m * KP + lk;
+                const double dold = act ? delta_in[o] : 1.0;
+                const double Tm = wave_suffix_sum(act ? tau_in[o] * sall[o] : 0.0, l);
+                const double Gm = act ? delta_G(d, dr, iter, m, l) : 1.0;
+                const double idold = 1.0 / dold;
+                const double idref = (l == 0) ? idold : 1.0 / d0new;   // delta(1,:,m) | delta(h) (Q4)
+                dm = delta_chain(d, l, Tm, Gm, idold, idref);
             }
+            const double tm = wave_scan_prod(act ? dm : 1.0, l);         // tauh = cumprod(delta)
             if (l < KP) {
-                const bool act = l < d.K;
                 delta_out[(size_t)m * KP + l] = act ? dm : delta_in[(size_t)m * KP + l];
                 tau_out[(size_t)m * KP + l] = act ? tm : tau_in[(size_t)m * KP + l];
                 tnew[l] = tm;
@@ -830,8 +885,8 @@ void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s) {
     hipLaunchKernelGGL(k_wpass, dim3(cdiv(d.NP, 64), d.G), dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W);
 }
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
-    hipLaunchKernelGGL(k_zdraw, dim3(cdiv(d.NP, 64), cdiv(d.G, 4)), dim3(256), 0, s, d, b.W, b.A, b.R,
-                       b.Rdi, b.X, b.Z, b.Sp, dr, iter);
+    hipLaunchKernelGGL(k_zdraw, dim3(cdiv(d.NP, 256), d.G), dim3(256), 0, s, d, b.W, b.A, b.R, b.Rdi, b.X,
+                       b.Z, b.Sp, dr, iter);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
     const int total = (d.NP + KP) * KP;
@@ -841,8 +896,8 @@ void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
     hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 64)), dim3(64), 0, s, d, b.xall, b.X, dr, iter);
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
-    const int nt = d.PP / 16 + KP / 16;
-    hipLaunchKernelGGL(k_cpass, dim3(cdiv(nt, 4), d.G), dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E);
+    const int nt = (d.PP + KP) / 32;
+    hipLaunchKernelGGL(k_cpass, dim3(nt, d.G), dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E);
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, hipStream_t s) {
@@ -850,7 +905,7 @@ void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t ite
                        b.Lam, b.psi, b.Plam, b.ps, b.omega, b.cpart, dr, iter);
 }
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s) {
-    hipLaunchKernelGGL(k_colsum, dim3(d.G), dim3(64), 0, s, d, b.cpart, b.sloc);
+    hipLaunchKernelGGL(k_colsum, dim3(d.G), dim3(256), 0, s, d, b.cpart, b.sloc);
 }
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                   const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,

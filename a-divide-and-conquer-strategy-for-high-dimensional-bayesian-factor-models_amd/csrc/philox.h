@@ -13,7 +13,8 @@
 //
 // Standard normal: Box-Muller on two 53-bit uniforms in (0,1].
 // Standard gamma(a >= 1): Marsaglia-Tsang squeeze/rejection (every gamma shape
-// in the reference is >= 1: df/2+0.5 = 2, as+n/2, ad+P*K/2 ...).
+// in the reference is >= 1: df/2+0.5 = 2, as+n/2, ad+P*K/2 ...); shapes 1 and 2
+// (the psi site uses 2) as a sum of exponentials.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -84,6 +85,12 @@ struct Rng {
     // standard gamma(shape >= 1), Marsaglia & Tsang (2000)
     __device__ double gamma(double shape, uint32_t site, uint32_t shard, uint32_t row,
                             uint32_t idx, uint32_t iter) const {
+        if (shape == 1.0 || shape == 2.0) {
+            // integer shape: sum of shape exponentials, -log(u1 [* u2]) — exact, no rejection
+            const u32x4 a = raw(site, shard, row, 0x80000000u | ((idx & 0x7FFFFFu) << 8), iter);
+            const double u1 = u01_53(a.x, a.y);
+            return shape == 1.0 ? -log(u1) : -log(u1 * u01_53(a.z, a.w));
+        }
         const double d = shape - 1.0 / 3.0;
         const double c = 1.0 / sqrt(9.0 * d);
         double v = 1.0;
