@@ -185,7 +185,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     d.nranks = nranks; d.rank = c.rank;
     d.G = c.g / nranks;
     d.shard0 = c.rank * d.G;
-    d.NP = round_up(c.n, 16);
+    d.NP = round_up(c.n, 128);
     d.PP = round_up(c.P, 32);
     d.p = c.P * c.g;
     d.rho = c.rho; d.sr = std::sqrt(c.rho); d.s1r = std::sqrt(1.0 - c.rho);

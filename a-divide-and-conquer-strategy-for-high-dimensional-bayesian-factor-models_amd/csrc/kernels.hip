@@ -156,45 +156,85 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
     if (lane < KP) Rdi[(size_t)m * KP + lane] = Lt[lane][KP];
 }
 
+// XCD-aware block remap (bijective): hardware deals consecutive block ids
+// round-robin over the 8 XCDs; give each XCD a contiguous range of work items
+// so that blocks sharing operands (one shard's tiles) share one L2.
+__device__ __forceinline__ int xcd_remap(int b, int total) {
+    const int xcd = b & 7, slot = b >> 3;
+    const int q = total >> 3, rem = total & 7;
+    return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + slot;
+}
+
 // ============================================================================
-// k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA
-// one wave = (shard m, 16 rows i) x 32 k; reduction over j in chunks of 8:
-// lane (r = lane&15, q = lane>>4) holds Y[i0+r][8t+2q .. +1]; k-step 2t uses
-// element 0, 2t+1 element 1 (the B operand uses the same j <-> (q,e) map).
+// k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA, Y pass 1
+// one wave = (shard m, 32 rows i = 2 M-tiles) x 32 k (even / odd k N-tiles),
+// reduction over j in chunks of 8: lane (r, q) holds Y[i0+r][8t+2q .. +1] (16 B);
+// k-step 2t uses element 0, 2t+1 element 1; the B operand (w_j L[j][2r], w_j L[j][2r+1])
+// uses the same j <-> (q, e) map.  Register double-buffered prefetch of 2 chunks.
 // ============================================================================
 __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict__ Y,
                                                const double *__restrict__ Lam,
                                                const double *__restrict__ omega,
                                                double *__restrict__ W) {
-    const int m = blockIdx.y;
+    const int nrb = d.NP >> 7;                       // 128-row blocks per shard
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int m = w / nrb, rb = w % nrb;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int i0 = (blockIdx.x * 4 + wave) * 16;
-    if (i0 >= d.NP) return;
+    const int i0 = rb * 128 + wave * 32;
     const int r = lane & 15, q = lane >> 4;
-    const double *Yrow = Y + ((size_t)m * d.NP + i0 + r) * d.PP;
-    const double *L = Lam + (size_t)m * d.PP * KP;
-    const double *w = omega + (size_t)m * d.PP;
-    d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-    const int nch = d.PP >> 3;
-#pragma unroll 4
-    for (int t = 0; t < nch; ++t) {
-        const int j = 8 * t + 2 * q;
-        const d2 y = *reinterpret_cast<const d2 *>(Yrow + j);
-        const d2 wj = *reinterpret_cast<const d2 *>(w + j);
-        const double b00 = wj.x * L[j * KP + r];
-        const double b01 = wj.x * L[j * KP + 16 + r];
-        const double b10 = wj.y * L[(j + 1) * KP + r];
-        const double b11 = wj.y * L[(j + 1) * KP + 16 + r];
-        acc0 = mfma16x16x4(y.x, b00, acc0);
-        acc1 = mfma16x16x4(y.x, b01, acc1);
-        acc0 = mfma16x16x4(y.y, b10, acc0);
-        acc1 = mfma16x16x4(y.y, b11, acc1);
-    }
-    double *Wt = W + ((size_t)m * d.NP + i0) * KP;
+    const double *Y0 = Y + ((size_t)m * d.NP + i0 + r) * d.PP + 2 * q;
+    const double *Y1 = Y0 + (size_t)16 * d.PP;
+    const double *L = Lam + (size_t)m * d.PP * KP + 2 * r;
+    const double *wp = omega + (size_t)m * d.PP + 2 * q;
+    d4 acc[2][2];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        Wt[(q + 4 * g) * KP + r] = acc0[g];
-        Wt[(q + 4 * g) * KP + 16 + r] = acc1[g];
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    const int nch = d.PP >> 3;
+    d2 yA0, yA1, wA, lA0, lA1, yB0, yB1, wB, lB0, lB1;
+#define WP_LOAD(t, y0, y1, ww, l0, l1)                                              \
+    {                                                                               \
+        const int j = 8 * (t);                                                      \
+        y0 = *reinterpret_cast<const d2 *>(Y0 + j);                                 \
+        y1 = *reinterpret_cast<const d2 *>(Y1 + j);                                 \
+        ww = *reinterpret_cast<const d2 *>(wp + j);                                 \
+        l0 = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q) * KP);           \
+        l1 = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q + 1) * KP);       \
+    }
+#define WP_MMA(y0, y1, ww, l0, l1)                                                  \
+    {                                                                               \
+        const double b00 = ww.x * l0.x, b01 = ww.x * l0.y;                          \
+        const double b10 = ww.y * l1.x, b11 = ww.y * l1.y;                          \
+        acc[0][0] = mfma16x16x4(y0.x, b00, acc[0][0]);                              \
+        acc[0][1] = mfma16x16x4(y0.x, b01, acc[0][1]);                              \
+        acc[1][0] = mfma16x16x4(y1.x, b00, acc[1][0]);                              \
+        acc[1][1] = mfma16x16x4(y1.x, b01, acc[1][1]);                              \
+        acc[0][0] = mfma16x16x4(y0.y, b10, acc[0][0]);                              \
+        acc[0][1] = mfma16x16x4(y0.y, b11, acc[0][1]);                              \
+        acc[1][0] = mfma16x16x4(y1.y, b10, acc[1][0]);                              \
+        acc[1][1] = mfma16x16x4(y1.y, b11, acc[1][1]);                              \
+    }
+    WP_LOAD(0, yA0, yA1, wA, lA0, lA1);
+    for (int t = 0; t < nch; t += 2) {
+        if (t + 1 < nch) WP_LOAD(t + 1, yB0, yB1, wB, lB0, lB1);
+        WP_MMA(yA0, yA1, wA, lA0, lA1);
+        if (t + 2 < nch) WP_LOAD(t + 2, yA0, yA1, wA, lA0, lA1);
+        if (t + 1 < nch) WP_MMA(yB0, yB1, wB, lB0, lB1);
+    }
+#undef WP_LOAD
+#undef WP_MMA
+    // D row = q + 4g (row i), col = r (k = 2r + tb)
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        double *Wt = W + ((size_t)m * d.NP + i0 + 16 * a) * KP + 2 * r;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            d2 v;
+            v.x = acc[a][0][g];
+            v.y = acc[a][1][g];
+            *reinterpret_cast<d2 *>(Wt + (size_t)(q + 4 * g) * KP) = v;
+        }
     }
 }
 
@@ -337,19 +377,23 @@ __global__ __launch_bounds__(256) void k_xred(Dims d, const double *__restrict__
 __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__ xall,
                                               double *__restrict__ X, DrawsDev dr, int64_t iter) {
     __shared__ double Lt[KP][LS];
+    __shared__ double As[KP][KP + 1];
     const int lane = threadIdx.x;
     const int rr = lane & 31;
     const bool upper = lane >= 32;
     const size_t stride = (size_t)(d.NP + KP) * KP;
+    // sum_m A_m over all ranks (rank order), staged through LDS by all lanes
+    for (int e = lane; e < KP * KP; e += 64) {
+        double v = xall[(size_t)d.NP * KP + e];
+        for (int rk = 1; rk < d.nranks; ++rk) v += xall[rk * stride + (size_t)d.NP * KP + e];
+        As[e / KP][e % KP] = v;
+    }
+    __syncthreads();
     {
         double qq[KP];
 #pragma unroll
-        for (int c = 0; c < KP; ++c) {
-            double v = 0.0;
-            if (c <= rr)
-                for (int rk = 0; rk < d.nranks; ++rk) v += xall[rk * stride + (size_t)(d.NP + c) * KP + rr];
-            qq[c] = (c <= rr) ? ((c == rr ? (double)d.g : 0.0) + d.rho * v) : 0.0;   // upper triangle
-        }
+        for (int c = 0; c < KP; ++c)   // cholcov reads the upper triangle: S[rr][c] = Xprec[c][rr]
+            qq[c] = (c <= rr) ? ((c == rr ? (double)d.g : 0.0) + d.rho * As[c][rr]) : 0.0;
         chol_rows(qq, Lt, rr, upper);
     }
     const int i = blockIdx.x * 64 + lane;
@@ -414,49 +458,79 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
 // ============================================================================
 // k_cpass: [C_m | E_m] = [Y_m | eta_m]' eta_m    fp64 MFMA, Y pass 2      dc:133,138,141
 // block = (shard m, 32-column tile of [Y | eta]); its 4 waves split the
-// reduction over rows i (memory-level parallelism), partial 32x32 tiles summed
-// in LDS in a fixed order.  eta is formed on the fly from X and Z.
+// reduction over rows i, partial 32x32 tiles summed in LDS in a fixed order.
+// Lane (r, q) loads 16 B: Y[i][c0+2r .. +1] and eta[i][2r .. +1] (formed on the
+// fly from X and Z), i = 4s + q, so the MFMA tiles are even/odd columns x
+// even/odd k.  Register double-buffered prefetch, 4 k-steps per batch.
 // ============================================================================
+template <bool IS_E>
+__device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restrict__ Yp,
+                                           const double *__restrict__ Xp,
+                                           const double *__restrict__ Zp, int s0, int nsw,
+                                           int q, d4 (&acc)[2][2]) {
+    d2 yA[4], xA[4], zA[4], yB[4], xB[4], zB[4];
+    auto load = [&](int s, d2 (&y)[4], d2 (&x)[4], d2 (&z)[4]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = 4 * (s + u) + q;
+            x[u] = *reinterpret_cast<const d2 *>(Xp + (size_t)i * KP);
+            z[u] = *reinterpret_cast<const d2 *>(Zp + (size_t)i * KP);
+            if (!IS_E) y[u] = *reinterpret_cast<const d2 *>(Yp + (size_t)i * d.PP);
+        }
+    };
+    auto mma = [&](d2 (&y)[4], d2 (&x)[4], d2 (&z)[4]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double e0 = eta_of(d.sr, d.s1r, x[u].x, z[u].x);
+            const double e1 = eta_of(d.sr, d.s1r, x[u].y, z[u].y);
+            const double a0 = IS_E ? e0 : y[u].x, a1 = IS_E ? e1 : y[u].y;
+            acc[0][0] = mfma16x16x4(a0, e0, acc[0][0]);
+            acc[0][1] = mfma16x16x4(a0, e1, acc[0][1]);
+            acc[1][0] = mfma16x16x4(a1, e0, acc[1][0]);
+            acc[1][1] = mfma16x16x4(a1, e1, acc[1][1]);
+        }
+    };
+    const int nb = nsw >> 2;
+    load(s0, yA, xA, zA);
+    for (int b = 0; b < nb; b += 2) {
+        if (b + 1 < nb) load(s0 + 4 * (b + 1), yB, xB, zB);
+        mma(yA, xA, zA);
+        if (b + 2 < nb) load(s0 + 4 * (b + 2), yA, xA, zA);
+        if (b + 1 < nb) mma(yB, xB, zB);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict__ Y,
                                                const double *__restrict__ X,
                                                const double *__restrict__ Z,
                                                double *__restrict__ C, double *__restrict__ E) {
     __shared__ double red[4][32][33];
-    const int m = blockIdx.y;
+    const int nt = (d.PP + KP) >> 5;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int m = w / nt, tile = w % nt;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c0 = blockIdx.x * 32;
+    const int c0 = tile * 32;
     const bool isE = c0 >= d.PP;
     const int r = lane & 15, q = lane >> 4;
-    const double *Ym = Y + (size_t)m * d.NP * d.PP + c0 + r;
-    const double *Zm = Z + (size_t)m * d.NP * KP;
+    const double *Yp = Y + (size_t)m * d.NP * d.PP + c0 + 2 * r;
+    const double *Xp = X + 2 * r;
+    const double *Zp = Z + (size_t)m * d.NP * KP + 2 * r;
     const int nsw = d.NP >> 4;                 // k-steps (4 rows each) per wave
-    const int s0 = wave * nsw;
-    d4 a00 = {0, 0, 0, 0}, a01 = a00, a10 = a00, a11 = a00;
-#pragma unroll 4
-    for (int s = s0; s < s0 + nsw; ++s) {
-        const int i = 4 * s + q;
-        const double e0 = eta_of(d.sr, d.s1r, X[i * KP + r], Zm[i * KP + r]);
-        const double e1 = eta_of(d.sr, d.s1r, X[i * KP + 16 + r], Zm[i * KP + 16 + r]);
-        double y0, y1;
-        if (isE) {
-            y0 = e0;
-            y1 = e1;
-        } else {
-            y0 = Ym[(size_t)i * d.PP];
-            y1 = Ym[(size_t)i * d.PP + 16];
-        }
-        a00 = mfma16x16x4(y0, e0, a00);
-        a01 = mfma16x16x4(y0, e1, a01);
-        a10 = mfma16x16x4(y1, e0, a10);
-        a11 = mfma16x16x4(y1, e1, a11);
-    }
+    d4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    if (isE) cpass_wave<true>(d, Yp, Xp, Zp, wave * nsw, nsw, q, acc);
+    else cpass_wave<false>(d, Yp, Xp, Zp, wave * nsw, nsw, q, acc);
+    // D row rho = q + 4g -> column c0 + 2 rho + ta;  D col r -> k = 2r + tb
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-        const int a = q + 4 * g;
-        red[wave][a][r] = a00[g];
-        red[wave][a][16 + r] = a01[g];
-        red[wave][16 + a][r] = a10[g];
-        red[wave][16 + a][16 + r] = a11[g];
+        const int rho = q + 4 * g;
+#pragma unroll
+        for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+            for (int tb = 0; tb < 2; ++tb) red[wave][2 * rho + ta][2 * r + tb] = acc[ta][tb][g];
     }
     __syncthreads();
     double *out = isE ? (E + (size_t)m * KP * KP) : (C + ((size_t)m * d.PP + c0) * KP);
@@ -466,11 +540,44 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
     }
 }
 
+// ----------------------------------------------------------------------------
+// Packed variant for k_lambda: per half-wave LDS image Lp = [column-major packed
+// lower L (528) | 1/L_kk (32) | broadcast scratch (32)].  The forward solve
+// L v = b is fused into the factorisation (b rides along as an extra column),
+// and the next pivot is formed from the pivot lane's own registers so the LDS
+// column broadcast stays off the serial critical path.
+// ----------------------------------------------------------------------------
+constexpr int PACK = KP * (KP + 1) / 2;
+constexpr int PSTRIDE = PACK + 2 * KP;
+__host__ __device__ constexpr int pbase(int k) { return k * KP - (k * (k - 1)) / 2; }
+
+__device__ __forceinline__ void chol_rows_fwd(double (&q)[KP], double *Lp, int r, bool upper,
+                                              double bv, double &vr) {
+    double piv = readsel(q[0], 0, upper);
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const double ikk = rsqrt_f64(piv);
+        const double lkk = piv * ikk;
+        const double lrk = (r > k) ? q[k] * ikk : (r == k ? lkk : 0.0);
+        q[k] = lrk;
+        if (r >= k) Lp[pbase(k) + r - k] = lrk;          // column k of L
+        if (r == k) Lp[PACK + k] = ikk;
+        const double vk = readsel(bv, k, upper) * ikk;   // v_k = b_k / L_kk
+        if (r == k) vr = vk;
+        if (r > k) bv -= lrk * vk;
+        if (k + 1 < KP) piv = readsel(q[k + 1] - lrk * lrk, k + 1, upper);
+#pragma unroll
+        for (int c = k + 1; c < KP; ++c) q[c] -= lrk * Lp[pbase(k) + c - k];
+#pragma unroll
+        for (int c = k + 1; c < KP; ++c) asm volatile("" : "+v"(q[c]));
+    }
+}
+
 // ============================================================================
 // k_lambda: loading rows.  A half-wave (32 lanes) owns one row j; lane r holds
 // row r of Q_j = diag(Plam_j) + ps_j E_m in registers.        dc:140-145 (+150,156,169-171)
-//   L = chol(Q,'lower') (chol_rows)
-//   v = L \ (ps_j C_j);  Lambda_j = L' \ (v + z)             (= ylam + mlam)
+//   L = chol(Q,'lower'), v = L \ (ps_j C_j)   (chol_rows_fwd)
+//   Lambda_j = L' \ (v + z)                    (= ylam + mlam)
 //   psi_j  = Gpsi * 1/(df/2 + 0.5 lambda^2 tau)               (dc:150, tau of the previous it.)
 //   SS_j   = yy_j - 2 lambda.C_j + lambda' E lambda  ->  ps_j = Gps * 1/(bs + 0.5 SS_j), w = 1/ps
 // 8 rows per 256-thread block; per-block column sums of psi o lambda^2 -> cpart.
@@ -484,7 +591,7 @@ __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict
                                                 double *__restrict__ omega,
                                                 double *__restrict__ cpart, DrawsDev dr,
                                                 int64_t iter) {
-    __shared__ double LT[8][KP][LS];   // LT[h][k][c] = L[c][k]  (column k of L, contiguous)
+    __shared__ double LP[8][PSTRIDE];
     __shared__ double Es[KP][KP + 1];  // E_m, shared by the block's 8 rows (same shard)
     __shared__ double csum[8][KP];
     const int m = blockIdx.y;
@@ -512,18 +619,10 @@ __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict
     for (int c = 0; c < KP; ++c)
         if (c == r) q[c] = (real && valid) ? plam + q[c] : 1.0;
     const double cjr = valid ? C[rowoff + r] : 0.0;
-    double bv = psj * cjr;
 
-    double (*Lt)[LS] = LT[hw];
-    chol_rows(q, Lt, r, upper);
-    // --- forward solve L v = b   (L[r][c] = Lt[c][r])
+    double *Lp = LP[hw];
     double vr = 0.0;
-#pragma unroll 2
-    for (int c = 0; c < KP; ++c) {
-        const double vc = readsel(bv, c, upper) * Lt[c][KP];
-        if (r == c) vr = vc;
-        if (r > c) bv -= Lt[c][r] * vc;
-    }
+    chol_rows_fwd(q, Lp, r, upper, psj * cjr, vr);
     // --- + z  (dc:142 normrnd(0,1,K,1))
     double z = 0.0;
     if (real && valid) {
@@ -535,21 +634,22 @@ __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict
         }
     }
     double wr = vr + z;
-    // --- back solve L' x = w
+    // --- back solve L' x = w;  L[c][r] = Lp[pbase(r) + c - r]
     double xr = 0.0;
+    const int br = pbase(r) - r;
 #pragma unroll 2
     for (int c = KP - 1; c >= 0; --c) {
-        const double xc = readsel(wr, c, upper) * Lt[c][KP];
+        const double xc = readsel(wr, c, upper) * Lp[PACK + c];
         if (r == c) xr = xc;
-        if (r < c) wr -= Lt[r][c] * xc;       // L[c][r]
+        if (r < c) wr -= Lp[br + c] * xc;
     }
     if (!real) xr = 0.0;
 
-    // --- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr; x broadcast through LT[h][r][KP+1]
-    Lt[r][KP + 1] = xr;
+    // --- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr; x broadcast through the scratch slots
+    Lp[PACK + KP + r] = xr;
     double ex = 0.0;
 #pragma unroll
-    for (int c = 0; c < KP; ++c) ex += Es[c][r] * Lt[c][KP + 1];   // (E x)_r, E symmetric
+    for (int c = 0; c < KP; ++c) ex += Es[c][r] * Lp[PACK + KP + c];   // (E x)_r, E symmetric
     double contrib = xr * (ex - 2.0 * cjr);
 #pragma unroll
     for (int o = 16; o >= 1; o >>= 1) contrib += __shfl_xor(contrib, o, 32);
@@ -882,7 +982,7 @@ void launch_prep(const Dims &d, const Bufs &b, hipStream_t s) {
     hipLaunchKernelGGL(k_prep, dim3(d.G), dim3(256), 0, s, d, b.Lam, b.omega, b.A, b.R, b.Rdi);
 }
 void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s) {
-    hipLaunchKernelGGL(k_wpass, dim3(cdiv(d.NP, 64), d.G), dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W);
+    hipLaunchKernelGGL(k_wpass, dim3((d.NP / 128) * d.G), dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W);
 }
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     hipLaunchKernelGGL(k_zdraw, dim3(cdiv(d.NP, 256), d.G), dim3(256), 0, s, d, b.W, b.A, b.R, b.Rdi, b.X,
@@ -897,7 +997,7 @@ void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     const int nt = (d.PP + KP) / 32;
-    hipLaunchKernelGGL(k_cpass, dim3(nt, d.G), dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E);
+    hipLaunchKernelGGL(k_cpass, dim3(nt * d.G), dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E);
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, hipStream_t s) {
