@@ -25,8 +25,9 @@ DCFM_FLAG_INJECT_DRAWS = 0x1
 KERNEL_IDS = {
     "k_prep": 0, "k_wpass": 1, "k_zdraw": 2, "k_xred": 3, "k_xdraw": 4, "k_cpass": 5,
     "k_lambda": 6, "k_colsum": 7, "k_delta": 8, "k_save": 9, "k_assemble": 10, "rccl": 11,
+    "k_xchol": 12,
 }
-K_COUNT = 12
+K_COUNT = 13
 
 # every symbol include/dcfm.h declares
 EXPORTS = (

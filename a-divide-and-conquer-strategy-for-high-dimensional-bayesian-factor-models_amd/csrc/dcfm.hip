@@ -28,12 +28,17 @@ struct dcfm_handle {
     Dims d{};
     Bufs b{};
     DrawsDev dr{};
-    hipStream_t stream = nullptr;
-    ncclComm_t comm = nullptr;
+    hipStream_t stream = nullptr;     // main: the sweep chain
+    hipStream_t side = nullptr;       // k_prep + k_xchol, overlapping k_wpass
+    hipStream_t sasm = nullptr;       // covariance assembly, overlapping later iterations
+    ncclComm_t comm = nullptr, comm_side = nullptr, comm_asm = nullptr;
     bool comm_ok = false;
+    hipEvent_t e_lam = nullptr, e_prep = nullptr, e_batch = nullptr, e_free[2] = {nullptr, nullptr};
+    bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
+    int lb = 0;                   // Lb buffer being filled
     int B = 16;                   // saved samples per flush
-    int batch = 0;                // saved samples pending in Lb
+    int batch = 0;                // saved samples pending in Lb[lb]
     int64_t saved = 0;
     bool have_data = false, have_state = false;
     std::string err;
@@ -105,27 +110,34 @@ static hipEvent_t get_event(dcfm_handle *h) {
 struct KTimer {
     dcfm_handle *h;
     int kid;
+    hipStream_t s;
     hipEvent_t a = nullptr;
-    KTimer(dcfm_handle *h_, int k) : h(h_), kid(k) {
+    KTimer(dcfm_handle *h_, int k, hipStream_t s_) : h(h_), kid(k), s(s_) {
         if (h->prof) {
             a = get_event(h);
-            if (a) (void)hipEventRecord(a, h->stream);
+            if (a) (void)hipEventRecord(a, s);
         }
     }
     ~KTimer() {
         if (h->prof && a) {
             hipEvent_t b = get_event(h);
             if (b) {
-                (void)hipEventRecord(b, h->stream);
+                (void)hipEventRecord(b, s);
                 h->recs.push_back({kid, a, b});
             }
         }
     }
 };
 
+static void sync_all(dcfm_handle *h) {
+    (void)hipStreamSynchronize(h->stream);
+    if (h->side) (void)hipStreamSynchronize(h->side);
+    if (h->sasm) (void)hipStreamSynchronize(h->sasm);
+}
+
 static void collect_prof(dcfm_handle *h) {
     if (h->recs.empty()) return;
-    (void)hipStreamSynchronize(h->stream);
+    sync_all(h);
     for (auto &r : h->recs) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
@@ -148,7 +160,7 @@ const char *dcfm_last_error(const dcfm_handle *h) { return h ? h->err.c_str() : 
 const char *dcfm_kernel_name(int id) {
     static const char *names[DCFM_K_COUNT] = {"k_prep",  "k_wpass", "k_zdraw",  "k_xred",
                                               "k_xdraw", "k_cpass", "k_lambda", "k_colsum",
-                                              "k_delta", "k_save",  "k_assemble", "rccl"};
+                                              "k_delta", "k_save",  "k_assemble", "rccl", "k_xchol"};
     return (id >= 0 && id < DCFM_K_COUNT) ? names[id] : "?";
 }
 
@@ -179,6 +191,13 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     h->cfg.nranks = nranks;
     HIPC(h, hipSetDevice(c.device));
     HIPC(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    HIPC(h, hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    HIPC(h, hipStreamCreateWithFlags(&h->sasm, hipStreamNonBlocking));
+    HIPC(h, hipEventCreateWithFlags(&h->e_lam, hipEventDisableTiming));
+    HIPC(h, hipEventCreateWithFlags(&h->e_prep, hipEventDisableTiming));
+    HIPC(h, hipEventCreateWithFlags(&h->e_batch, hipEventDisableTiming));
+    HIPC(h, hipEventCreateWithFlags(&h->e_free[0], hipEventDisableTiming));
+    HIPC(h, hipEventCreateWithFlags(&h->e_free[1], hipEventDisableTiming));
 
     Dims &d = h->d;
     d.n = c.n; d.P = c.P; d.g = c.g; d.K = c.K;
@@ -212,18 +231,22 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     ALLOC(b.tau, 2 * g * KP);
     ALLOC(b.W, G * NP * KP);
     ALLOC(b.A, G * KP * KP);
-    ALLOC(b.R, G * KP * KP);
-    ALLOC(b.Rdi, G * KP);
+    ALLOC(b.ZM, G * 4 * KP * KP);
     ALLOC(b.Sp, G * NP * KP);
-    ALLOC(b.xin, (NP + KP) * KP);
-    if (nranks > 1) { ALLOC(b.xall, (size_t)nranks * (NP + KP) * KP); } else b.xall = b.xin;
+    ALLOC(b.xin, NP * KP);
+    if (nranks > 1) { ALLOC(b.xall, (size_t)nranks * NP * KP); } else b.xall = b.xin;
+    ALLOC(b.xa, KP * KP);
+    ALLOC(b.xa_all, (size_t)nranks * KP * KP);
+    ALLOC(b.XM, 2 * KP * KP);
     ALLOC(b.C, G * PP * KP);
     ALLOC(b.E, G * KP * KP);
     ALLOC(b.cpart, G * (PP / 8) * KP);
     ALLOC(b.sloc, G * KP);
     if (nranks > 1) { ALLOC(b.sall, g * KP); } else b.sall = b.sloc;
-    ALLOC(b.Lb, p * (size_t)b.LDB);
-    ALLOC(b.wsum, p);
+    ALLOC(b.Lb[0], p * (size_t)b.LDB);
+    ALLOC(b.Lb[1], p * (size_t)b.LDB);
+    ALLOC(b.wsum[0], p);
+    ALLOC(b.wsum[1], p);
     ALLOC(b.Sigma, p * p);
 #undef ALLOC
     // lower-triangle assembly tiles, dealt round-robin over ranks
@@ -254,12 +277,18 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
 void dcfm_destroy(dcfm_handle *h) {
     if (!h) return;
     (void)hipSetDevice(h->cfg.device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->stream) sync_all(h);
     for (auto &r : h->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : h->evpool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {h->e_lam, h->e_prep, h->e_batch, h->e_free[0], h->e_free[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (h->comm_asm) ncclCommDestroy(h->comm_asm);
+    if (h->comm_side) ncclCommDestroy(h->comm_side);
     if (h->comm) ncclCommDestroy(h->comm);
     for (void *q : h->allocs) (void)hipFree(q);
     if (h->draws_mem) (void)hipFree(h->draws_mem);
+    if (h->sasm) (void)hipStreamDestroy(h->sasm);
+    if (h->side) (void)hipStreamDestroy(h->side);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -280,6 +309,9 @@ int dcfm_comm_init(dcfm_handle *h, const uint8_t id[128]) {
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
     NCCLC(h, ncclCommInitRank(&h->comm, h->d.nranks, uid, h->d.rank));
+    // one communicator per stream so collectives on different streams never interleave
+    NCCLC(h, ncclCommSplit(h->comm, 0, h->d.rank, &h->comm_side, nullptr));
+    NCCLC(h, ncclCommSplit(h->comm, 0, h->d.rank, &h->comm_asm, nullptr));
     h->comm_ok = true;
     return DCFM_OK;
 }
@@ -376,7 +408,7 @@ int dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s) {
         return fail(h, DCFM_ERR_INVALID, "set_state: every member except eta is required");
     const Dims &d = h->d;
     HIPC(h, hipSetDevice(h->cfg.device));
-    HIPC(h, hipStreamSynchronize(h->stream));
+    sync_all(h);
     std::vector<double> v;
     int rc;
     pk_to_dev(d, s->Lambda, v); if ((rc = up(h, h->b.Lam, v))) return rc;
@@ -397,7 +429,7 @@ int dcfm_get_state(dcfm_handle *h, dcfm_state_view *o) {
     if (!h || !o) return fail(h, DCFM_ERR_INVALID, "null argument");
     const Dims &d = h->d;
     HIPC(h, hipSetDevice(h->cfg.device));
-    HIPC(h, hipStreamSynchronize(h->stream));
+    sync_all(h);
     std::vector<double> v;
     int rc;
     const size_t npk = (size_t)d.G * d.PP * KP, nnk = (size_t)d.G * d.NP * KP;
@@ -427,7 +459,7 @@ int dcfm_set_draws(dcfm_handle *h, const dcfm_draws_view *dv, int64_t first_iter
         return fail(h, DCFM_ERR_INVALID, "set_draws: all six arrays required");
     const Dims &d = h->d;
     HIPC(h, hipSetDevice(h->cfg.device));
-    HIPC(h, hipStreamSynchronize(h->stream));
+    sync_all(h);
     const size_t T = n_iter;
     const size_t nNZ = (size_t)d.K * d.n * d.g * T, nNX = (size_t)d.K * d.n * T,
                  nNL = (size_t)d.K * d.P * d.g * T, nPsi = (size_t)d.P * d.K * d.g * T,
@@ -451,27 +483,36 @@ int dcfm_set_draws(dcfm_handle *h, const dcfm_draws_view *dv, int64_t first_iter
     return DCFM_OK;
 }
 
+// Hand the filled Lb[lb] batch to the assembly stream (overlaps the next iterations).
 static int flush_batch(dcfm_handle *h) {
     if (h->batch == 0) return DCFM_OK;
     Dims &d = h->d;
     Bufs &b = h->b;
+    const int lb = h->lb;
+    HIPC(h, hipEventRecord(h->e_batch, h->stream));
+    HIPC(h, hipStreamWaitEvent(h->sasm, h->e_batch, 0));
     if (d.nranks > 1) {
-        KTimer t(h, DCFM_K_COMM);
+        KTimer t(h, DCFM_K_COMM, h->sasm);
         const size_t rows = (size_t)d.G * d.P;
         NCCLC(h, ncclGroupStart());
-        NCCLC(h, ncclAllGather(b.Lb + (size_t)d.rank * rows * b.LDB, b.Lb, rows * b.LDB, ncclDouble, h->comm, h->stream));
-        NCCLC(h, ncclAllGather(b.wsum + (size_t)d.rank * rows, b.wsum, rows, ncclDouble, h->comm, h->stream));
+        NCCLC(h, ncclAllGather(b.Lb[lb] + (size_t)d.rank * rows * b.LDB, b.Lb[lb], rows * b.LDB, ncclDouble,
+                               h->comm_asm, h->sasm));
+        NCCLC(h, ncclAllGather(b.wsum[lb] + (size_t)d.rank * rows, b.wsum[lb], rows, ncclDouble, h->comm_asm,
+                               h->sasm));
         NCCLC(h, ncclGroupEnd());
     }
     const int kext = round_up(h->batch * d.K, 8);
     const double effsamp = (double)h->cfg.mcmc / (double)h->cfg.thin;   // dc:45 (Q8)
     {
-        KTimer t(h, DCFM_K_ASSEMBLE);
-        launch_assemble(d, b, kext, 1.0 / effsamp, h->stream);
+        KTimer t(h, DCFM_K_ASSEMBLE, h->sasm);
+        launch_assemble(d, b, b.Lb[lb], b.wsum[lb], kext, 1.0 / effsamp, h->sasm);
     }
     HIPC(h, hipGetLastError());
-    HIPC(h, hipMemsetAsync(b.Lb, 0, (size_t)d.p * b.LDB * sizeof(double), h->stream));
-    HIPC(h, hipMemsetAsync(b.wsum, 0, (size_t)d.p * sizeof(double), h->stream));
+    HIPC(h, hipMemsetAsync(b.Lb[lb], 0, (size_t)d.p * b.LDB * sizeof(double), h->sasm));
+    HIPC(h, hipMemsetAsync(b.wsum[lb], 0, (size_t)d.p * sizeof(double), h->sasm));
+    HIPC(h, hipEventRecord(h->e_free[lb], h->sasm));
+    h->asm_pending[lb] = true;
+    h->lb ^= 1;
     h->batch = 0;
     return DCFM_OK;
 }
@@ -490,34 +531,51 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
                         (long long)first_iter, (long long)(first_iter + n_iter));
     }
     HIPC(h, hipSetDevice(h->cfg.device));
-    hipStream_t s = h->stream;
+    hipStream_t s = h->stream, ss = h->side;
     const size_t nkg = (size_t)d.g * KP;
+    HIPC(h, hipEventRecord(h->e_lam, s));      // Lambda/omega of the previous iteration are final
     for (int64_t it = first_iter; it < first_iter + n_iter; ++it) {
-        { KTimer t(h, DCFM_K_PREP);   launch_prep(d, b, s); }
-        { KTimer t(h, DCFM_K_WPASS);  launch_wpass(d, b, s); }
-        { KTimer t(h, DCFM_K_ZDRAW);  launch_zdraw(d, b, h->dr, it, s); }
-        { KTimer t(h, DCFM_K_XRED);   launch_xred(d, b, s); }
+        // side stream: A_m, R_m, Rx from this iteration's incoming Lambda, omega (dc:98-100,112-118)
+        HIPC(h, hipStreamWaitEvent(ss, h->e_lam, 0));
+        { KTimer t(h, DCFM_K_PREP, ss); launch_prep(d, b, ss); }
+        { KTimer t(h, DCFM_K_XCHOL, ss); launch_asum(d, b, ss); }
         if (d.nranks > 1) {
-            KTimer t(h, DCFM_K_COMM);
-            NCCLC(h, ncclAllGather(b.xin, b.xall, (size_t)(d.NP + KP) * KP, ncclDouble, h->comm, s));
+            KTimer t(h, DCFM_K_COMM, ss);
+            NCCLC(h, ncclAllGather(b.xa, b.xa_all, (size_t)KP * KP, ncclDouble, h->comm_side, ss));
         }
-        { KTimer t(h, DCFM_K_XDRAW);  launch_xdraw(d, b, h->dr, it, s); }
-        { KTimer t(h, DCFM_K_CPASS);  launch_cpass(d, b, s); }
-        { KTimer t(h, DCFM_K_LAMBDA); launch_lambda(d, b, h->dr, it, b.tau + h->cur * nkg, s); }
-        { KTimer t(h, DCFM_K_COLSUM); launch_colsum(d, b, s); }
+        { KTimer t(h, DCFM_K_XCHOL, ss); launch_xchol(d, b, ss); }
+        HIPC(h, hipEventRecord(h->e_prep, ss));
+        // main stream
+        { KTimer t(h, DCFM_K_WPASS, s);  launch_wpass(d, b, s); }
+        HIPC(h, hipStreamWaitEvent(s, h->e_prep, 0));
+        { KTimer t(h, DCFM_K_ZDRAW, s);  launch_zdraw(d, b, h->dr, it, s); }
+        { KTimer t(h, DCFM_K_XRED, s);   launch_xred(d, b, s); }
         if (d.nranks > 1) {
-            KTimer t(h, DCFM_K_COMM);
+            KTimer t(h, DCFM_K_COMM, s);
+            NCCLC(h, ncclAllGather(b.xin, b.xall, (size_t)d.NP * KP, ncclDouble, h->comm, s));
+        }
+        { KTimer t(h, DCFM_K_XDRAW, s);  launch_xdraw(d, b, h->dr, it, s); }
+        { KTimer t(h, DCFM_K_CPASS, s);  launch_cpass(d, b, s); }
+        { KTimer t(h, DCFM_K_LAMBDA, s); launch_lambda(d, b, h->dr, it, b.tau + h->cur * nkg, s); }
+        HIPC(h, hipEventRecord(h->e_lam, s));
+        { KTimer t(h, DCFM_K_COLSUM, s); launch_colsum(d, b, s); }
+        if (d.nranks > 1) {
+            KTimer t(h, DCFM_K_COMM, s);
             NCCLC(h, ncclAllGather(b.sloc, b.sall, (size_t)d.G * KP, ncclDouble, h->comm, s));
         }
         {
-            KTimer t(h, DCFM_K_DELTA);
+            KTimer t(h, DCFM_K_DELTA, s);
             launch_delta(d, b, h->dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
                          b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);
         }
         h->cur ^= 1;
         HIPC(h, hipGetLastError());
         if (it % h->cfg.thin == 0 && it > h->cfg.burnin) {                // dc:180
-            { KTimer t(h, DCFM_K_SAVE); launch_save(d, b, h->batch, s); }
+            if (h->batch == 0 && h->asm_pending[h->lb]) {                 // buffer still being assembled
+                HIPC(h, hipStreamWaitEvent(s, h->e_free[h->lb], 0));
+                h->asm_pending[h->lb] = false;
+            }
+            { KTimer t(h, DCFM_K_SAVE, s); launch_save(d, b, b.Lb[h->lb], b.wsum[h->lb], h->batch, s); }
             HIPC(h, hipGetLastError());
             h->batch += 1;
             h->saved += 1;
@@ -537,6 +595,8 @@ int dcfm_synchronize(dcfm_handle *h) {
     if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
     HIPC(h, hipSetDevice(h->cfg.device));
     HIPC(h, hipStreamSynchronize(h->stream));
+    HIPC(h, hipStreamSynchronize(h->side));
+    HIPC(h, hipStreamSynchronize(h->sasm));
     return DCFM_OK;
 }
 
@@ -549,11 +609,12 @@ int dcfm_get_sigma(dcfm_handle *h, double *out) {
     const size_t pp = (size_t)d.p * d.p;
     double *tmp = nullptr;
     void *q = nullptr;
+    sync_all(h);
     HIPC(h, hipMalloc(&q, pp * sizeof(double)));
     tmp = static_cast<double *>(q);
     int rc = DCFM_OK;
     if (d.nranks > 1) {
-        ncclResult_t r = ncclAllReduce(h->b.Sigma, tmp, pp, ncclDouble, ncclSum, h->comm, h->stream);
+        ncclResult_t r = ncclAllReduce(h->b.Sigma, tmp, pp, ncclDouble, ncclSum, h->comm_asm, h->stream);
         if (r != ncclSuccess) rc = fail(h, DCFM_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
     } else {
         hipError_t e = hipMemcpyAsync(tmp, h->b.Sigma, pp * sizeof(double), hipMemcpyDeviceToDevice, h->stream);

@@ -10,15 +10,15 @@
 //   delta, tau [2][g][KP] replicated on every rank, double-buffered per iteration
 //   W      [G][NP][KP]   W_m = Y_m (omega o Lambda_m)                    (k_wpass)
 //   A      [G][KP][KP]   A_m = Lambda_m' diag(omega) Lambda_m             (k_prep)
-//   R      [G][KP][KP]   cholcov(I + (1-rho) A_m), upper, identity-padded (k_prep)
-//   Sp     [ceil(G/4)][NP][KP]  per-4-shard partial of sum_m (W_m - sqrt(1-rho) A_m Z_m')
-//   xin    [NP+KP][KP]   local sum over shards of Sp (rows < NP) and A (rows >= NP)
-//   xall   [nranks][NP+KP][KP]  all-gathered xin (== xin when nranks == 1)
+//   ZM     [G][4][KP][KP] Z-draw operators {M1, M2, U, NA} of shard m         (k_prep)
+//   Sp     [G][NP][KP]   per-shard X message W_m - sqrt(1-rho) A_m Z_m'   (k_zdraw)
+//   xin    [NP][KP]      local sum over shards of Sp;  xall [nranks][NP][KP] all-gathered (== xin if 1 rank)
+//   xa, xa_all [nranks][KP][KP]  per-rank sum of A_m (gathered);  XM [2][KP][KP] X-draw operators {Tx, Ux} (k_xchol)
 //   C      [G][PP][KP]   C_m = Y_m' eta_m  (k_cpass);  E [G][KP][KP] = eta_m' eta_m
 //   cpart  [G][PP/8][KP] per-8-row partial column sums of psi o Lambda^2 (k_lambda)
 //   sloc   [G][KP], sall [g][KP]  column sums (all-gathered)
-//   Lb     [p][LDB]      saved Lambda rows of the current assembly batch, sample s at cols s*K..
-//   wsum   [p]           sum of saved omega of the batch
+//   Lb     [2][p][LDB]   saved Lambda rows of an assembly batch (double-buffered), sample s at cols s*K..
+//   wsum   [2][p]        sum of saved omega of the batch
 //   Sigma  [p][p]        lower triangle accumulated (each rank: its tiles), mirrored on get
 #pragma once
 #include <hip/hip_runtime.h>
@@ -49,8 +49,9 @@ struct DrawsDev {
 
 struct Bufs {
     double *Y, *yy, *Lam, *omega, *ps, *psi, *Plam, *X, *Z, *delta, *tau;
-    double *W, *A, *R, *Rdi, *Sp, *xin, *xall, *C, *E, *cpart, *sloc, *sall;
-    double *Lb, *wsum, *Sigma;
+    double *W, *A, *ZM, *Sp, *xin, *xall, *C, *E, *cpart, *sloc, *sall;
+    double *Lb[2], *wsum[2], *Sigma;
+    double *xa, *xa_all, *XM;          // per-rank sum of A, gathered sums, X-draw operators
     int2 *tiles;
     int ntiles, LDB;
 };
@@ -60,6 +61,8 @@ void launch_prep(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s);
+void launch_asum(const Dims &d, const Bufs &b, hipStream_t s);
+void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
@@ -68,8 +71,9 @@ void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                   const double *delta_in, const double *tau_in, double *delta_out,
                   double *tau_out, hipStream_t s);
-void launch_save(const Dims &d, const Bufs &b, int slot, hipStream_t s);
-void launch_assemble(const Dims &d, const Bufs &b, int kext, double inv_eff, hipStream_t s);
+void launch_save(const Dims &d, const Bufs &b, double *Lb, double *wsum, int slot, hipStream_t s);
+void launch_assemble(const Dims &d, const Bufs &b, const double *Lb, const double *wsum, int kext,
+                     double inv_eff, hipStream_t s);
 void launch_mirror(double *S, int p, hipStream_t s);
 void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s);
 void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,

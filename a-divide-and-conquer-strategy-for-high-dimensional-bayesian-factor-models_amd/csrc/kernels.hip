@@ -3,115 +3,59 @@
 // covariance assembly.  fp64 throughout (the reference is double precision).
 //
 // Kernel map (per iteration, in order)                         reference lines
+//   side stream (overlaps k_wpass):
 //   k_prep     A_m = Lambda' diag(w) Lambda (MFMA), R_m = cholcov(I+(1-rho)A_m)  dc:98-100,114-115
+//   k_xchol    Xprec = g I + rho sum_m A_m, Rx = cholcov   [+ RCCL all-gather]  dc:112-118
+//   main stream:
 //   k_wpass    W_m = Y_m (w o Lambda_m)           fp64 MFMA, Y pass 1      dc:102-103,122-123
 //   k_zdraw    Z rows: R\ , R'\ , noise; per-shard (W - s1r A Z')          dc:101-107,121-124
-//   k_xred     sum over local shards (+ sum_m A_m)                         dc:112-116,120-124
+//   k_xred     sum over local shards                                       dc:120-124
 //   [RCCL all-gather across ranks]
-//   k_xdraw    Xprec = gI + rho sum A, cholcov, X rows                     dc:117-128
+//   k_xdraw    X rows                                                      dc:119-128
 //   k_cpass    C_m = Y_m' eta_m, E_m = eta_m' eta_m  fp64 MFMA, Y pass 2   dc:133,138,141
 //   k_lambda   per loading row: Q, chol, 3 solves, Lambda_j; psi_j;        dc:140-145,150,
 //              SS_j via identity, ps_j, omega_j; column sums of psi o L^2  dc:156,169-171
 //   k_colsum   per-shard column sums                                       dc:156
 //   [RCCL all-gather across ranks]
 //   k_delta    MGP chain (quirks Q4/Q5) for all shards, Plam refresh       dc:155-165,175-177
-//   saved iterations: k_save (+ RCCL all-gather at flush), k_assemble      dc:180-195
+//   saved iterations: k_save; per batch on the assembly stream (overlapping
+//   the following iterations): [RCCL all-gather], k_assemble            dc:180-195
 //
 // The residual pass of dc:169-170 needs no third read of Y: with C_j = eta'Y_j
 // and E = eta'eta already computed for the loading draw,
 //   SS_j = sum_i (Y_ij - eta_i Lambda_j')^2 = yy_j - 2 Lambda_j.C_j + Lambda_j E Lambda_j'.
 #include "dcfm_internal.h"
 #include "philox.h"
+#include "linalg.h"
 
 #include <algorithm>
 
 namespace dcfm {
 
-typedef double d4 __attribute__((ext_vector_type(4)));
-typedef double d2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ d4 mfma16x16x4(double a, double b, d4 c) {
-    // v_mfma_f64_16x16x4_f64: A[i=lane&15][k=lane>>4], B[k=lane>>4][j=lane&15],
-    // C/D: col = lane&15, row = (lane>>4) + 4*reg
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ double readlane_d(double x, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
-    return __hiloint2double(hi, lo);
-}
-
-// value of x held by lane c of this lane's half-wave
-__device__ __forceinline__ double readsel(double x, int c, bool upper) {
-    const double lo = readlane_d(x, c);
-    const double hi = readlane_d(x, 32 + c);
-    return upper ? hi : lo;
-}
-
-// 1/sqrt(x) to full fp64 precision: hardware estimate + 2 Newton steps
-__device__ __forceinline__ double rsqrt_f64(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-        const double e = fma(-x * y, y, 1.0);
-        y = fma(0.5 * y, e, y);
-    }
-    return y;
-}
-
-// eta = sqrt(rho) X + sqrt(1-rho) Z    (dc:81,133) — one definition for every use
-__device__ __forceinline__ double eta_of(double sr, double s1r, double x, double z) {
-    return sr * x + s1r * z;
-}
-
-// ----------------------------------------------------------------------------
-// Register Cholesky of a KP x KP SPD matrix per half-wave (32 lanes).
-// Lane r = lane & 31 holds row r in q[] (entries c <= r are read).  On return
-// q[c] = L[r][c] (0 for c > r) and the LDS image Lt[k][c] = L[c][k] (column k
-// of L, contiguous) with Lt[k][KP] = 1/L[k][k].  Right-looking; column k is
-// broadcast through LDS; the diagonal through readlane.  Both half-waves run
-// independent matrices (or the same one, writing identical values).
-// ----------------------------------------------------------------------------
-constexpr int LS = KP + 2;
-
-__device__ __forceinline__ void chol_rows(double (&q)[KP], double (*Lt)[LS], int r, bool upper) {
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-        const double dkk = readsel(q[k], k, upper);
-        const double ikk = rsqrt_f64(dkk);
-        const double lkk = dkk * ikk;
-        const double lrk = (r > k) ? q[k] * ikk : (r == k ? lkk : 0.0);
-        q[k] = lrk;
-        Lt[k][r] = lrk;
-        if (r == k) Lt[k][KP] = ikk;
-#pragma unroll
-        for (int c = k + 1; c < KP; ++c) q[c] -= lrk * Lt[k][c];
-        // keep the trailing update eager: without this hipcc sinks each FMA to
-        // the step that consumes q[c] and keeps O(K^2) loaded L values live
-#pragma unroll
-        for (int c = k + 1; c < KP; ++c) asm volatile("" : "+v"(q[c]));
-    }
-}
+// device helpers (MFMA, lane broadcast, rsqrt, register Cholesky): linalg.h
 
 // ============================================================================
-// k_prep: A_m = (w o Lambda_m)' Lambda_m and R_m = cholcov(eye(K) + (1-rho) A_m)   dc:98-100
-// 4 waves split the j reduction (fp64 MFMA 2x2 tiles), LDS sum, wave 0 factors.
+// k_prep: A_m = (w o Lambda_m)' Lambda_m and the Z-draw operators of shard m    dc:98-107
+//   L = chol(Zprec) lower, Zprec = eye(K) + (1-rho) A_m (cholcov's R = L')
+//   U = L^{-1} = R^{-T},  T = U U' = R^{-T} R^{-1}   (quirk Q2: the reference's mean
+//   R'\(R\bz) is T bz, its noise R'\z is U z), so with bz = sqrt(1-rho)(W - sqrt(rho) A x):
+//     Z = M1 W + M2 x + U eps,   M1 = sqrt(1-rho) T,  M2 = -sqrt(1-rho) sqrt(rho) T A
+//     S = W + NA Z,              NA = -sqrt(1-rho) A
+// ZM[m] = {M1, M2, U, NA}.  4 waves split the j reduction of A (fp64 MFMA 2x2 tiles).
 // ============================================================================
 __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__ Lam,
                                               const double *__restrict__ omega,
-                                              double *__restrict__ A, double *__restrict__ R,
-                                              double *__restrict__ Rdi) {
-    __shared__ double part[4][KP][KP + 1];
-    __shared__ double Lt[KP][LS];
+                                              double *__restrict__ A, double *__restrict__ ZM) {
+    __shared__ double part[4][KP][KP + 1];     // partial A per wave; later A, U, T
+    __shared__ __attribute__((aligned(16))) double Lp[P2STRIDE];
     const int m = blockIdx.x;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const int r = lane & 15, q = lane >> 4;
     const double *L = Lam + (size_t)m * d.PP * KP;
     const double *w = omega + (size_t)m * d.PP;
     d4 a00 = {0, 0, 0, 0}, a01 = a00, a10 = a00, a11 = a00;
-    for (int t = wave; t < (d.PP >> 3); t += 4) {
-        const int j = 8 * t + 2 * q;
+    for (int tt = wave; tt < (d.PP >> 3); tt += 4) {
+        const int j = 8 * tt + 2 * q;
         const d2 wj = *reinterpret_cast<const d2 *>(w + j);
         const double lo0 = L[j * KP + r], hi0 = L[j * KP + 16 + r];
         const double lo1 = L[(j + 1) * KP + r], hi1 = L[(j + 1) * KP + 16 + r];
@@ -132,28 +76,55 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
     }
     __syncthreads();
     double *Am = A + (size_t)m * KP * KP;
-    for (int e = threadIdx.x; e < KP * KP; e += 256) {
-        const int a = e / KP, b = e % KP;
-        const double v = (part[0][a][b] + part[1][a][b]) + (part[2][a][b] + part[3][a][b]);
-        Am[e] = v;
-        part[0][a][b] = v;
+    double *Zm = ZM + (size_t)m * 4 * KP * KP;
+    double av[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = t + 256 * u, a = e / KP, b = e % KP;
+        av[u] = (part[0][a][b] + part[1][a][b]) + (part[2][a][b] + part[3][a][b]);
+        Am[e] = av[u];
+        Zm[3 * KP * KP + e] = -d.s1r * av[u];                       // NA
     }
     __syncthreads();
-    if (wave != 0) return;
-    // cholcov reads the upper triangle: S[rr][c] = Zprec[c][rr] for c <= rr
-    const int rr = lane & 31;
-    const bool upper = lane >= 32;
-    double qq[KP];
 #pragma unroll
-    for (int c = 0; c < KP; ++c)
-        qq[c] = (c <= rr) ? ((c == rr ? 1.0 : 0.0) + (1.0 - d.rho) * part[0][c][rr]) : 0.0;
-    chol_rows(qq, Lt, rr, upper);
-    double *Rm = R + (size_t)m * KP * KP;
-    for (int e = lane; e < KP * KP; e += 64) {
-        const int a = e / KP, b = e % KP;
-        Rm[e] = (b >= a) ? Lt[a][b] : 0.0;        // R = L', upper, R'R = Zprec
+    for (int u = 0; u < 4; ++u) {
+        const int e = t + 256 * u;
+        part[0][e / KP][e % KP] = av[u];                            // A
     }
-    if (lane < KP) Rdi[(size_t)m * KP + lane] = Lt[lane][KP];
+    __syncthreads();
+    if (wave == 0) {
+        // cholcov reads the upper triangle: S[rr][c] = Zprec[c][rr] for c <= rr
+        const int rr = lane & 31;
+        double qq[KP];
+#pragma unroll
+        for (int c = 0; c < KP; ++c)
+            qq[c] = (c <= rr) ? ((c == rr ? 1.0 : 0.0) + (1.0 - d.rho) * part[0][c][rr]) : 0.0;
+        double vr = 0.0;
+        chol2_rows<false>(qq, Lp, rr, lane >= 32, 0.0, vr);
+    }
+    __syncthreads();
+    lower_inverse2(Lp, part[1], t);                                 // U -> part[1]
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {                                   // T = U U' -> part[2]
+        const int e = t + 256 * u, a = e / KP, c = e % KP;
+        double acc = 0.0;
+#pragma unroll
+        for (int b = 0; b < KP; ++b) acc += part[1][a][b] * part[1][c][b];
+        part[2][a][c] = acc;
+        Zm[e] = d.s1r * acc;                                        // M1
+        Zm[2 * KP * KP + e] = part[1][a][c];                        // U
+    }
+    __syncthreads();
+    const double s2 = -d.s1r * d.sr;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {                                   // M2 = -s1r sr T A
+        const int e = t + 256 * u, a = e / KP, c = e % KP;
+        double acc = 0.0;
+#pragma unroll
+        for (int b = 0; b < KP; ++b) acc += part[2][a][b] * part[0][b][c];
+        Zm[KP * KP + e] = s2 * acc;
+    }
 }
 
 // XCD-aware block remap (bijective): hardware deals consecutive block ids
@@ -239,220 +210,245 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
 }
 
 // ============================================================================
-// k_zdraw: per (row i, shard m), lane = row; one shard per block, A_m and R_m
-// broadcast from LDS.                                           dc:101-107,121-123
-//   bz = sqrt(1-rho) (W_i - sqrt(rho) A X_i)            (= sqrt(1-rho) Zmsg'(Y_i - sqrt(rho) L X_i))
-//   v  = R \ bz ;  Z_i = R' \ (v + eps)                 (quirk Q2 order)
-//   Sp_m,i = W_i - sqrt(1-rho) A Z_i                     (Xmsg'(Y_i - sqrt(1-rho) L Z_i))
+// k_zdraw: Z draw and per-shard X message as fp64 MFMA chains.   dc:101-107,121-123
+//   Z' = M1 W' + M2 X' + U eps'      (k_prep operators; columns = rows i)
+//   S' = W' + NA Z'                  (S_i = Xmsg'(Y_i - sqrt(1-rho) L Z_i))
+// block = (shard m, 128 rows), 4 waves x 2 tiles of 16 rows.  Operand lane map:
+// lane (c = lane&15, q = lane>>4) holds W[i0+c][8t+2q .. +1] (k-steps 2t+e);
+// the f64 C/D layout of Z' (row = q + 4r) is directly the B operand of the
+// NA Z' product (k-step r), so nothing crosses LDS.
 // ============================================================================
 __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W,
-                                               const double *__restrict__ A,
-                                               const double *__restrict__ R,
-                                               const double *__restrict__ Rdi,
+                                               const double *__restrict__ ZM,
                                                const double *__restrict__ X,
                                                double *__restrict__ Z, double *__restrict__ Sp,
                                                DrawsDev dr, int64_t iter) {
-    __shared__ double As[KP][KP], Rs[KP][KP], Rd[KP];
-    const int m = blockIdx.y;
+    __shared__ double Ms[4][KP][KP + 1];     // M1, M2, U, NA
+    const int nrb = d.NP >> 7;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int m = w / nrb, rb = w % nrb;
     {
-        const double *Am = A + (size_t)m * KP * KP;
-        const double *Rm = R + (size_t)m * KP * KP;
-        for (int e = threadIdx.x; e < KP * KP; e += 256) {
-            As[e / KP][e % KP] = Am[e];
-            Rs[e / KP][e % KP] = Rm[e];
+        const double *Zm = ZM + (size_t)m * 4 * KP * KP;
+        for (int e = threadIdx.x; e < 4 * KP * KP; e += 256) {
+            const int mat = e / (KP * KP), rem = e % (KP * KP);
+            Ms[mat][rem / KP][rem % KP] = Zm[e];
         }
-        if (threadIdx.x < KP) Rd[threadIdx.x] = Rdi[(size_t)m * KP + threadIdx.x];
     }
     __syncthreads();
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= d.NP) return;
-    double *Spi = Sp + ((size_t)m * d.NP + i) * KP;
-    if (i >= d.n) {
-#pragma unroll
-        for (int k = 0; k < KP; k += 2) *reinterpret_cast<d2 *>(Spi + k) = d2{0.0, 0.0};
-        return;
-    }
-    const double *Wi = W + ((size_t)m * d.NP + i) * KP;
-    const double *Xi = X + (size_t)i * KP;
-    double x[KP], t[KP];
-#pragma unroll
-    for (int k = 0; k < KP; k += 2) {
-        const d2 v = *reinterpret_cast<const d2 *>(Xi + k);
-        x[k] = v.x;
-        x[k + 1] = v.y;
-    }
-#pragma unroll
-    for (int a = 0; a < KP; ++a) {
-        double acc = 0.0;
-#pragma unroll
-        for (int b = 0; b < KP; ++b) acc += As[a][b] * x[b];
-        t[a] = d.s1r * (Wi[a] - d.sr * acc);
-    }
-    // back substitution R v = bz (R upper)
-#pragma unroll
-    for (int a = KP - 1; a >= 0; --a) {
-        double acc = t[a];
-#pragma unroll
-        for (int b = a + 1; b < KP; ++b) acc -= Rs[a][b] * t[b];
-        t[a] = acc * Rd[a];
-    }
-    // + eps  (dc:104 normrnd(0,1,[K,1]))
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, q = lane >> 4;
     const int mg = d.shard0 + m;
-    if (d.inject) {
-        const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + i) * d.K;
+#pragma unroll 1
+    for (int tile = 0; tile < 2; ++tile) {
+        const int i0 = rb * 128 + wave * 32 + tile * 16;
+        const int i = i0 + c;
+        const bool live = i < d.n;
+        const double *Wi = W + ((size_t)m * d.NP + i) * KP + 2 * q;
+        const double *Xi = X + (size_t)i * KP + 2 * q;
+        d2 wv[4], xv[4], ev[4];
 #pragma unroll
-        for (int k = 0; k < KP; ++k)
-            if (k < d.K) t[k] += nz[k];
-    } else {
-        const Rng rng(d.seed);
+        for (int t = 0; t < 4; ++t) {
+            wv[t] = *reinterpret_cast<const d2 *>(Wi + 8 * t);
+            xv[t] = *reinterpret_cast<const d2 *>(Xi + 8 * t);
+        }
+        // eps[i][kk], kk = 8t + 2q + e   (dc:104 normrnd, pair index 4t + q)
+        if (d.inject) {
+            const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K;
 #pragma unroll
-        for (int k = 0; k < KP; k += 2) {
-            if (k < d.K) {
-                double n0, n1;
-                rng.normal2(SITE_Z, mg, i, k >> 1, (uint32_t)iter, n0, n1);
-                t[k] += n0;
-                if (k + 1 < d.K) t[k + 1] += n1;
+            for (int t = 0; t < 4; ++t) {
+                const int kk = 8 * t + 2 * q;
+                ev[t].x = (live && kk < d.K) ? nz[kk] : 0.0;
+                ev[t].y = (live && kk + 1 < d.K) ? nz[kk + 1] : 0.0;
+            }
+        } else {
+            const Rng rng(d.seed);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int kk = 8 * t + 2 * q;
+                double n0 = 0.0, n1 = 0.0;
+                if (live && kk < d.K) rng.normal2(SITE_Z, mg, i, kk >> 1, (uint32_t)iter, n0, n1);
+                ev[t].x = n0;
+                ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
             }
         }
-    }
-    // forward substitution R' z = v + eps
+        d4 az[2], as[2];
+        az[0] = az[1] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int a = 0; a < KP; ++a) {
-        double acc = t[a];
+        for (int t = 0; t < 4; ++t) {
 #pragma unroll
-        for (int b = 0; b < a; ++b) acc -= Rs[b][a] * t[b];
-        t[a] = acc * Rd[a];
-    }
-    double *Zi = Z + ((size_t)m * d.NP + i) * KP;
+            for (int e = 0; e < 2; ++e) {
+                const int kk = 8 * t + 2 * q + e;
+                const double we = e ? wv[t].y : wv[t].x, xe = e ? xv[t].y : xv[t].x;
+                const double ee = e ? ev[t].y : ev[t].x;
 #pragma unroll
-    for (int k = 0; k < KP; k += 2) {
-        d2 v;
-        v.x = (k < d.K) ? t[k] : 0.0;
-        v.y = (k + 1 < d.K) ? t[k + 1] : 0.0;
-        *reinterpret_cast<d2 *>(Zi + k) = v;
-    }
-#pragma unroll
-    for (int a = 0; a < KP; a += 2) {
-        double acc0 = 0.0, acc1 = 0.0;
-#pragma unroll
-        for (int b = 0; b < KP; ++b) {
-            acc0 += As[a][b] * t[b];
-            acc1 += As[a + 1][b] * t[b];
+                for (int mt = 0; mt < 2; ++mt) {
+                    az[mt] = mfma16x16x4(Ms[0][16 * mt + c][kk], we, az[mt]);
+                    az[mt] = mfma16x16x4(Ms[1][16 * mt + c][kk], xe, az[mt]);
+                    az[mt] = mfma16x16x4(Ms[2][16 * mt + c][kk], ee, az[mt]);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);   // bound the hoisting of operand reads
         }
-        d2 v;
-        v.x = Wi[a] - d.s1r * acc0;
-        v.y = Wi[a + 1] - d.s1r * acc1;
-        *reinterpret_cast<d2 *>(Spi + a) = v;
+        // S' = W' + NA Z'; accumulator starts from W in the C/D layout
+        const double *Wr = W + ((size_t)m * d.NP + i) * KP;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) as[mt][g] = Wr[16 * mt + q + 4 * g];
+#pragma unroll
+        for (int mt2 = 0; mt2 < 2; ++mt2)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int kk = 16 * mt2 + 4 * g + q;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) as[mt] = mfma16x16x4(Ms[3][16 * mt + c][kk], az[mt2][g], as[mt]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        double *Zr = Z + ((size_t)m * d.NP + i) * KP;
+        double *Sr = Sp + ((size_t)m * d.NP + i) * KP;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int k = 16 * mt + q + 4 * g;
+                if (live) Zr[k] = (k < d.K) ? az[mt][g] : 0.0;
+                Sr[k] = live ? as[mt][g] : 0.0;
+            }
     }
 }
 
 // ============================================================================
-// k_xred: xin[i][k] = sum_m Sp[m][i][k];  xin[NP+a][b] = sum_m A_m[a][b]     dc:113-116,121-124
+// k_xred: xin[i][k] = sum_m Sp[m][i][k]  (local shards, fixed order)     dc:120-124
 // ============================================================================
 __global__ __launch_bounds__(256) void k_xred(Dims d, const double *__restrict__ Sp,
-                                              const double *__restrict__ A,
                                               double *__restrict__ xin) {
-    const size_t total = (size_t)(d.NP + KP) * KP;
+    const size_t total = (size_t)d.NP * KP;
     const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (e >= total) return;
-    const size_t row = e / KP;
     double acc = 0.0;
-    if (row < (size_t)d.NP) {
-        const size_t stride = (size_t)d.NP * KP;
 #pragma unroll 8
-        for (int m = 0; m < d.G; ++m) acc += Sp[(size_t)m * stride + e];
-    } else {
-        const size_t off = e - (size_t)d.NP * KP;
-#pragma unroll 8
-        for (int m = 0; m < d.G; ++m) acc += A[(size_t)m * KP * KP + off];
-    }
+    for (int m = 0; m < d.G; ++m) acc += Sp[(size_t)m * total + e];
     xin[e] = acc;
 }
 
 // ============================================================================
-// k_xdraw: X rows.  Xprec = g*I + rho*sum_m A_m (all ranks), Rx = cholcov,     dc:117-128
-//   X_i = Rx' \ (Rx \ (sqrt(rho) S_i) + eps)
-// one wave per 64 rows; every block factors the KxK Xprec itself (register Cholesky).
+// k_asum: xa = sum_m A_m over local shards (fixed order), one thread per element.   dc:113-116
 // ============================================================================
-__global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__ xall,
-                                              double *__restrict__ X, DrawsDev dr, int64_t iter) {
-    __shared__ double Lt[KP][LS];
-    __shared__ double As[KP][KP + 1];
+__global__ __launch_bounds__(256) void k_asum(Dims d, const double *__restrict__ A,
+                                              double *__restrict__ xa) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= KP * KP) return;
+    double v = 0.0;
+#pragma unroll 8
+    for (int m = 0; m < d.G; ++m) v += A[(size_t)m * KP * KP + e];
+    xa[e] = v;
+}
+
+// ============================================================================
+// k_xchol: Xprec = g*I + rho*sum A (dc:117) and Rx = cholcov(Xprec) (dc:118), on the
+// side stream.  Sums the per-rank sums xa_all in rank order (nranks == 1: xa itself)
+// and writes the X-draw operators XM = {Tx = sqrt(rho) Ux Ux', Ux = Rx^{-T}}.
+// ============================================================================
+__global__ __launch_bounds__(64) void k_xchol(Dims d, const double *__restrict__ xa_all,
+                                              double *__restrict__ XM) {
+    __shared__ __attribute__((aligned(16))) double Lp[P2STRIDE];
+    __shared__ double As[KP][KP + 1], Us[KP][KP + 1];
     const int lane = threadIdx.x;
-    const int rr = lane & 31;
-    const bool upper = lane >= 32;
-    const size_t stride = (size_t)(d.NP + KP) * KP;
-    // sum_m A_m over all ranks (rank order), staged through LDS by all lanes
     for (int e = lane; e < KP * KP; e += 64) {
-        double v = xall[(size_t)d.NP * KP + e];
-        for (int rk = 1; rk < d.nranks; ++rk) v += xall[rk * stride + (size_t)d.NP * KP + e];
+        double v = xa_all[e];
+        for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * KP * KP + e];
         As[e / KP][e % KP] = v;
     }
     __syncthreads();
     {
+        const int rr = lane & 31;
         double qq[KP];
 #pragma unroll
         for (int c = 0; c < KP; ++c)   // cholcov reads the upper triangle: S[rr][c] = Xprec[c][rr]
             qq[c] = (c <= rr) ? ((c == rr ? (double)d.g : 0.0) + d.rho * As[c][rr]) : 0.0;
-        chol_rows(qq, Lt, rr, upper);
+        double vr = 0.0;
+        chol2_rows<false>(qq, Lp, rr, lane >= 32, 0.0, vr);
     }
-    const int i = blockIdx.x * 64 + lane;
-    if (i >= d.n) return;
-    double v[KP];
+    __syncthreads();
+    lower_inverse2(Lp, Us, lane);          // Ux = Lx^{-1} = Rx^{-T}
+    __syncthreads();
+    // X = Rx^{-T}(Rx^{-1} sqrt(rho) S + eps) = Tx S + Ux eps,  Tx = sqrt(rho) Ux Ux'
+    for (int e = lane; e < KP * KP; e += 64) {
+        const int a = e / KP, c = e % KP;
+        double acc = 0.0;
 #pragma unroll
-    for (int k = 0; k < KP; ++k) v[k] = 0.0;
-    for (int rk = 0; rk < d.nranks; ++rk) {
-        const double *s = xall + rk * stride + (size_t)i * KP;
-#pragma unroll
-        for (int k = 0; k < KP; k += 2) {
-            const d2 u = *reinterpret_cast<const d2 *>(s + k);
-            v[k] += u.x;
-            v[k + 1] += u.y;
-        }
+        for (int b = 0; b < KP; ++b) acc += Us[a][b] * Us[c][b];
+        XM[e] = d.sr * acc;
+        XM[KP * KP + e] = Us[a][c];
     }
+}
+
+// ============================================================================
+// k_xdraw: X' = Tx S' + Ux eps' as fp64 MFMA (operators from k_xchol); S summed over
+// ranks in rank order.  One wave per 16 rows.                                 dc:119-128
+// ============================================================================
+__global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__ xall,
+                                              const double *__restrict__ XM,
+                                              double *__restrict__ X, DrawsDev dr, int64_t iter) {
+    __shared__ double Ms[2][KP][KP + 1];
+    for (int e = threadIdx.x; e < 2 * KP * KP; e += 64) {
+        const int mat = e / (KP * KP), rem = e % (KP * KP);
+        Ms[mat][rem / KP][rem % KP] = XM[e];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x, c = lane & 15, q = lane >> 4;
+    const int i0 = blockIdx.x * 16, i = i0 + c;
+    const bool live = i < d.n;
+    const size_t stride = (size_t)d.NP * KP;
+    d2 sv[4], ev[4];
 #pragma unroll
-    for (int k = 0; k < KP; ++k) v[k] = d.sr * v[k];     // bx = sqrt(rho)*sumx2
-    // Rx v' = bx; Rx[a][b] = L[b][a] = Lt[a][b]
-#pragma unroll
-    for (int a = KP - 1; a >= 0; --a) {
-        double acc = v[a];
-#pragma unroll
-        for (int b = a + 1; b < KP; ++b) acc -= Lt[a][b] * v[b];
-        v[a] = acc * Lt[a][KP];
+    for (int t = 0; t < 4; ++t) {
+        sv[t] = *reinterpret_cast<const d2 *>(xall + (size_t)i * KP + 8 * t + 2 * q);
+        for (int rk = 1; rk < d.nranks; ++rk)
+            sv[t] += *reinterpret_cast<const d2 *>(xall + rk * stride + (size_t)i * KP + 8 * t + 2 * q);
     }
     if (d.inject) {
-        const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + i) * d.K;
+        const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K;
 #pragma unroll
-        for (int k = 0; k < KP; ++k)
-            if (k < d.K) v[k] += nx[k];
+        for (int t = 0; t < 4; ++t) {
+            const int kk = 8 * t + 2 * q;
+            ev[t].x = (live && kk < d.K) ? nx[kk] : 0.0;
+            ev[t].y = (live && kk + 1 < d.K) ? nx[kk + 1] : 0.0;
+        }
     } else {
         const Rng rng(d.seed);
 #pragma unroll
-        for (int k = 0; k < KP; k += 2) {
-            if (k < d.K) {
-                double n0, n1;
-                rng.normal2(SITE_X, 0, i, k >> 1, (uint32_t)iter, n0, n1);
-                v[k] += n0;
-                if (k + 1 < d.K) v[k + 1] += n1;
-            }
+        for (int t = 0; t < 4; ++t) {
+            const int kk = 8 * t + 2 * q;
+            double n0 = 0.0, n1 = 0.0;
+            if (live && kk < d.K) rng.normal2(SITE_X, 0, i, kk >> 1, (uint32_t)iter, n0, n1);
+            ev[t].x = n0;
+            ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
         }
     }
-    // Rx' x = v + eps; Rx'[a][b] = Lt[b][a]
+    d4 ax[2];
+    ax[0] = ax[1] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int a = 0; a < KP; ++a) {
-        double acc = v[a];
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int b = 0; b < a; ++b) acc -= Lt[b][a] * v[b];
-        v[a] = acc * Lt[a][KP];
-    }
-    double *Xi = X + (size_t)i * KP;
+        for (int e = 0; e < 2; ++e) {
+            const int kk = 8 * t + 2 * q + e;
+            const double se = e ? sv[t].y : sv[t].x, ee = e ? ev[t].y : ev[t].x;
 #pragma unroll
-    for (int k = 0; k < KP; k += 2) {
-        d2 u;
-        u.x = (k < d.K) ? v[k] : 0.0;
-        u.y = (k + 1 < d.K) ? v[k + 1] : 0.0;
-        *reinterpret_cast<d2 *>(Xi + k) = u;
-    }
+            for (int mt = 0; mt < 2; ++mt) {
+                ax[mt] = mfma16x16x4(Ms[0][16 * mt + c][kk], se, ax[mt]);
+                ax[mt] = mfma16x16x4(Ms[1][16 * mt + c][kk], ee, ax[mt]);
+            }
+        }
+    if (!live) return;
+    double *Xr = X + (size_t)i * KP;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int k = 16 * mt + q + 4 * g;
+            Xr[k] = (k < d.K) ? ax[mt][g] : 0.0;
+        }
 }
 
 // ============================================================================
@@ -540,39 +536,6 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
     }
 }
 
-// ----------------------------------------------------------------------------
-// Packed variant for k_lambda: per half-wave LDS image Lp = [column-major packed
-// lower L (528) | 1/L_kk (32) | broadcast scratch (32)].  The forward solve
-// L v = b is fused into the factorisation (b rides along as an extra column),
-// and the next pivot is formed from the pivot lane's own registers so the LDS
-// column broadcast stays off the serial critical path.
-// ----------------------------------------------------------------------------
-constexpr int PACK = KP * (KP + 1) / 2;
-constexpr int PSTRIDE = PACK + 2 * KP;
-__host__ __device__ constexpr int pbase(int k) { return k * KP - (k * (k - 1)) / 2; }
-
-__device__ __forceinline__ void chol_rows_fwd(double (&q)[KP], double *Lp, int r, bool upper,
-                                              double bv, double &vr) {
-    double piv = readsel(q[0], 0, upper);
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-        const double ikk = rsqrt_f64(piv);
-        const double lkk = piv * ikk;
-        const double lrk = (r > k) ? q[k] * ikk : (r == k ? lkk : 0.0);
-        q[k] = lrk;
-        if (r >= k) Lp[pbase(k) + r - k] = lrk;          // column k of L
-        if (r == k) Lp[PACK + k] = ikk;
-        const double vk = readsel(bv, k, upper) * ikk;   // v_k = b_k / L_kk
-        if (r == k) vr = vk;
-        if (r > k) bv -= lrk * vk;
-        if (k + 1 < KP) piv = readsel(q[k + 1] - lrk * lrk, k + 1, upper);
-#pragma unroll
-        for (int c = k + 1; c < KP; ++c) q[c] -= lrk * Lp[pbase(k) + c - k];
-#pragma unroll
-        for (int c = k + 1; c < KP; ++c) asm volatile("" : "+v"(q[c]));
-    }
-}
-
 // ============================================================================
 // k_lambda: loading rows.  A half-wave (32 lanes) owns one row j; lane r holds
 // row r of Q_j = diag(Plam_j) + ps_j E_m in registers.        dc:140-145 (+150,156,169-171)
@@ -591,7 +554,7 @@ __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict
                                                 double *__restrict__ omega,
                                                 double *__restrict__ cpart, DrawsDev dr,
                                                 int64_t iter) {
-    __shared__ double LP[8][PSTRIDE];
+    __shared__ __attribute__((aligned(16))) double LP[8][P2STRIDE];
     __shared__ double Es[KP][KP + 1];  // E_m, shared by the block's 8 rows (same shard)
     __shared__ double csum[8][KP];
     const int m = blockIdx.y;
@@ -622,7 +585,7 @@ __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict
 
     double *Lp = LP[hw];
     double vr = 0.0;
-    chol_rows_fwd(q, Lp, r, upper, psj * cjr, vr);
+    chol2_rows<true>(q, Lp, r, upper, psj * cjr, vr);
     // --- + z  (dc:142 normrnd(0,1,K,1))
     double z = 0.0;
     if (real && valid) {
@@ -634,22 +597,26 @@ __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict
         }
     }
     double wr = vr + z;
-    // --- back solve L' x = w;  L[c][r] = Lp[pbase(r) + c - r]
+    // --- back solve L' x = w, two rows per step;  L[c][r] = Lp[p2idx(c, r)]
     double xr = 0.0;
-    const int br = pbase(r) - r;
+    const int br = pb2(r >> 1) - 2 * (r & ~1) + (r & 1);     // L[c][r] at br + 2c
 #pragma unroll 2
-    for (int c = KP - 1; c >= 0; --c) {
-        const double xc = readsel(wr, c, upper) * Lp[PACK + c];
+    for (int c = KP - 1; c >= 1; c -= 2) {
+        // x_c = w_c / L_cc ; x_{c-1} = (w_{c-1} - L[c][c-1] x_c) / L_{c-1,c-1}
+        const double xc = readsel(wr, c, upper) * Lp[PACK2 + c];
+        const double lcc1 = Lp[p2idx(c, c - 1)];
+        const double xc1 = (readsel(wr, c - 1, upper) - lcc1 * xc) * Lp[PACK2 + c - 1];
         if (r == c) xr = xc;
-        if (r < c) wr -= Lp[br + c] * xc;
+        if (r == c - 1) xr = xc1;
+        if (r < c - 1) wr -= Lp[br + 2 * c] * xc + Lp[br + 2 * (c - 1)] * xc1;
     }
     if (!real) xr = 0.0;
 
     // --- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr; x broadcast through the scratch slots
-    Lp[PACK + KP + r] = xr;
+    Lp[PACK2 + KP + r] = xr;
     double ex = 0.0;
 #pragma unroll
-    for (int c = 0; c < KP; ++c) ex += Es[c][r] * Lp[PACK + KP + c];   // (E x)_r, E symmetric
+    for (int c = 0; c < KP; ++c) ex += Es[c][r] * Lp[PACK2 + KP + c];   // (E x)_r, E symmetric
     double contrib = xr * (ex - 2.0 * cjr);
 #pragma unroll
     for (int o = 16; o >= 1; o >>= 1) contrib += __shfl_xor(contrib, o, 32);
@@ -979,21 +946,27 @@ __global__ __launch_bounds__(256) void k_rng_fill(uint64_t seed, int kind, doubl
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 void launch_prep(const Dims &d, const Bufs &b, hipStream_t s) {
-    hipLaunchKernelGGL(k_prep, dim3(d.G), dim3(256), 0, s, d, b.Lam, b.omega, b.A, b.R, b.Rdi);
+    hipLaunchKernelGGL(k_prep, dim3(d.G), dim3(256), 0, s, d, b.Lam, b.omega, b.A, b.ZM);
 }
 void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s) {
     hipLaunchKernelGGL(k_wpass, dim3((d.NP / 128) * d.G), dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W);
 }
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
-    hipLaunchKernelGGL(k_zdraw, dim3(cdiv(d.NP, 256), d.G), dim3(256), 0, s, d, b.W, b.A, b.R, b.Rdi, b.X,
-                       b.Z, b.Sp, dr, iter);
+    hipLaunchKernelGGL(k_zdraw, dim3((d.NP / 128) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
+                       dr, iter);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
-    const int total = (d.NP + KP) * KP;
-    hipLaunchKernelGGL(k_xred, dim3(cdiv(total, 256)), dim3(256), 0, s, d, b.Sp, b.A, b.xin);
+    const int total = d.NP * KP;
+    hipLaunchKernelGGL(k_xred, dim3(cdiv(total, 256)), dim3(256), 0, s, d, b.Sp, b.xin);
+}
+void launch_asum(const Dims &d, const Bufs &b, hipStream_t s) {
+    hipLaunchKernelGGL(k_asum, dim3(KP * KP / 256), dim3(256), 0, s, d, b.A, b.xa);
+}
+void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
+    hipLaunchKernelGGL(k_xchol, dim3(1), dim3(64), 0, s, d, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
 }
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
-    hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 64)), dim3(64), 0, s, d, b.xall, b.X, dr, iter);
+    hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(64), 0, s, d, b.xall, b.XM, b.X, dr, iter);
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     const int nt = (d.PP + KP) / 32;
@@ -1013,15 +986,16 @@ void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
     hipLaunchKernelGGL(k_delta, dim3(d.g), dim3(256), 0, s, d, b.sall, delta_in, tau_in, delta_out,
                        tau_out, b.psi, b.Plam, dr, iter);
 }
-void launch_save(const Dims &d, const Bufs &b, int slot, hipStream_t s) {
+void launch_save(const Dims &d, const Bufs &b, double *Lb, double *wsum, int slot, hipStream_t s) {
     const size_t total = (size_t)d.G * d.P * d.K;
     const int grid = (int)std::min<size_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(k_save, dim3(grid), dim3(256), 0, s, d, b.Lam, b.omega, b.Lb, b.wsum, b.LDB, slot);
+    hipLaunchKernelGGL(k_save, dim3(grid), dim3(256), 0, s, d, b.Lam, b.omega, Lb, wsum, b.LDB, slot);
 }
-void launch_assemble(const Dims &d, const Bufs &b, int kext, double inv_eff, hipStream_t s) {
+void launch_assemble(const Dims &d, const Bufs &b, const double *Lb, const double *wsum, int kext,
+                     double inv_eff, hipStream_t s) {
     if (b.ntiles == 0) return;
-    hipLaunchKernelGGL(k_assemble, dim3(b.ntiles), dim3(256), 0, s, d, b.Lb, b.LDB, kext, b.wsum,
-                       inv_eff, b.tiles, b.Sigma);
+    hipLaunchKernelGGL(k_assemble, dim3(b.ntiles), dim3(256), 0, s, d, Lb, b.LDB, kext, wsum, inv_eff,
+                       b.tiles, b.Sigma);
 }
 void launch_mirror(double *S, int p, hipStream_t s) {
     const int nt = cdiv(p, 32);

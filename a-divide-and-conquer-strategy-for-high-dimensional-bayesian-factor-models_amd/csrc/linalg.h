@@ -1,0 +1,220 @@
+// Device helpers shared by the sweep kernels (and tools/ microbenchmarks):
+// fp64 MFMA wrapper, half-wave lane broadcast, fp64 rsqrt, and the per-half-wave
+// register Cholesky factorisations used for the K x K systems of dc:100,118,142.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "dcfm_internal.h"
+
+namespace dcfm {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ d4 mfma16x16x4(double a, double b, d4 c) {
+    // v_mfma_f64_16x16x4_f64: A[i=lane&15][k=lane>>4], B[k=lane>>4][j=lane&15],
+    // C/D: col = lane&15, row = (lane>>4) + 4*reg
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+    return __hiloint2double(hi, lo);
+}
+
+// value of x held by lane c of this lane's half-wave
+__device__ __forceinline__ double readsel(double x, int c, bool upper) {
+    const double lo = readlane_d(x, c);
+    const double hi = readlane_d(x, 32 + c);
+    return upper ? hi : lo;
+}
+
+// 1/sqrt(x) to full fp64 precision: hardware estimate + 2 Newton steps
+__device__ __forceinline__ double rsqrt_f64(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const double e = fma(-x * y, y, 1.0);
+        y = fma(0.5 * y, e, y);
+    }
+    return y;
+}
+
+// eta = sqrt(rho) X + sqrt(1-rho) Z    (dc:81,133) — one definition for every use
+__device__ __forceinline__ double eta_of(double sr, double s1r, double x, double z) {
+    return sr * x + s1r * z;
+}
+
+// ----------------------------------------------------------------------------
+// Register Cholesky of a KP x KP SPD matrix per half-wave (32 lanes).
+// Lane r = lane & 31 holds row r in q[] (entries c <= r are read).  On return
+// q[c] = L[r][c] (0 for c > r) and the LDS image Lt[k][c] = L[c][k] (column k
+// of L, contiguous) with Lt[k][KP] = 1/L[k][k].  Right-looking; column k is
+// broadcast through LDS; the diagonal through readlane.  Both half-waves run
+// independent matrices (or the same one, writing identical values).
+// ----------------------------------------------------------------------------
+constexpr int LS = KP + 2;
+
+__device__ __forceinline__ void chol_rows(double (&q)[KP], double (*Lt)[LS], int r, bool upper) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const double dkk = readsel(q[k], k, upper);
+        const double ikk = rsqrt_f64(dkk);
+        const double lkk = dkk * ikk;
+        const double lrk = (r > k) ? q[k] * ikk : (r == k ? lkk : 0.0);
+        q[k] = lrk;
+        Lt[k][r] = lrk;
+        if (r == k) Lt[k][KP] = ikk;
+#pragma unroll
+        for (int c = k + 1; c < KP; ++c) q[c] -= lrk * Lt[k][c];
+        // keep the trailing update eager: without this hipcc sinks each FMA to
+        // the step that consumes q[c] and keeps O(K^2) loaded L values live
+#pragma unroll
+        for (int c = k + 1; c < KP; ++c) asm volatile("" : "+v"(q[c]));
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Packed variant for k_lambda: per half-wave LDS image Lp = [column-major packed
+// lower L (528) | 1/L_kk (32) | broadcast scratch (32)].  The forward solve
+// L v = b is fused into the factorisation (b rides along as an extra column),
+// and the next pivot is formed from the pivot lane's own registers so the LDS
+// column broadcast stays off the serial critical path.
+// ----------------------------------------------------------------------------
+constexpr int PACK = KP * (KP + 1) / 2;
+constexpr int PSTRIDE = PACK + 2 * KP;
+__host__ __device__ constexpr int pbase(int k) { return k * KP - (k * (k - 1)) / 2; }
+
+__device__ __forceinline__ void chol_rows_fwd(double (&q)[KP], double *Lp, int r, bool upper,
+                                              double bv, double &vr) {
+    double piv = readsel(q[0], 0, upper);
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const double ikk = rsqrt_f64(piv);
+        const double lkk = piv * ikk;
+        const double lrk = (r > k) ? q[k] * ikk : (r == k ? lkk : 0.0);
+        q[k] = lrk;
+        if (r >= k) Lp[pbase(k) + r - k] = lrk;          // column k of L
+        if (r == k) Lp[PACK + k] = ikk;
+        const double vk = readsel(bv, k, upper) * ikk;   // v_k = b_k / L_kk
+        if (r == k) vr = vk;
+        if (r > k) bv -= lrk * vk;
+        if (k + 1 < KP) piv = readsel(q[k + 1] - lrk * lrk, k + 1, upper);
+#pragma unroll
+        for (int c = k + 1; c < KP; ++c) q[c] -= lrk * Lp[pbase(k) + c - k];
+#pragma unroll
+        for (int c = k + 1; c < KP; ++c) asm volatile("" : "+v"(q[c]));
+    }
+}
+
+// ----------------------------------------------------------------------------
+// 2-column-blocked register Cholesky (16 serial steps instead of 32).
+// Layout of the LDS image P (pair-packed lower L): column pair j = (2j, 2j+1),
+// rows c >= 2j, entry (c, e) at pb2(j) + 2 (c - 2j) + e, so L[c][2j] and
+// L[c][2j+1] are one 16-byte read; then KP slots of 1/L[k][k] and KP scratch.
+// Lane r = lane & 31 of each half-wave holds row r in q[] (entries c <= r read).
+// Optional fused forward solve: bv holds b_r; vr returns (L^{-1} b)_r.
+// ----------------------------------------------------------------------------
+__host__ __device__ constexpr int pb2(int j) { return 64 * j - 2 * j * (j - 1); }
+constexpr int PACK2 = pb2(KP / 2);
+constexpr int P2STRIDE = PACK2 + 2 * KP;
+__device__ __forceinline__ int p2idx(int c, int k) { return pb2(k >> 1) + 2 * (c - (k & ~1)) + (k & 1); }
+
+template <bool FWD>
+__device__ __forceinline__ void chol2_rows(double (&q)[KP], double *P, int r, bool upper, double bv,
+                                           double &vr) {
+#pragma unroll
+    for (int j = 0; j < KP / 2; ++j) {
+        const int k = 2 * j;
+        // 2x2 diagonal block, factored redundantly in every lane
+        const double a = readsel(q[k], k, upper);
+        const double b = readsel(q[k], k + 1, upper);
+        const double c2 = readsel(q[k + 1], k + 1, upper);
+        const double i00 = rsqrt_f64(a);
+        const double l00 = a * i00;
+        const double l10 = b * i00;
+        const double d11 = c2 - l10 * l10;
+        const double i11 = rsqrt_f64(d11);
+        const double l11 = d11 * i11;
+        double lr0, lr1;
+        if (r > k + 1) {
+            lr0 = q[k] * i00;
+            lr1 = (q[k + 1] - lr0 * l10) * i11;
+        } else if (r == k + 1) {
+            lr0 = l10;
+            lr1 = l11;
+        } else if (r == k) {
+            lr0 = l00;
+            lr1 = 0.0;
+        } else {
+            lr0 = 0.0;
+            lr1 = 0.0;
+        }
+        q[k] = lr0;
+        q[k + 1] = lr1;
+        if (r >= k) {
+            d2 v;
+            v.x = lr0;
+            v.y = lr1;
+            *reinterpret_cast<d2 *>(P + pb2(j) + 2 * (r - k)) = v;
+        }
+        if (r == k) {
+            d2 v;
+            v.x = i00;
+            v.y = i11;
+            *reinterpret_cast<d2 *>(P + PACK2 + k) = v;
+        }
+        if (FWD) {   // v_k = b_k / L_kk ; v_{k+1} = (b_{k+1} - L_{k+1,k} v_k) / L_{k+1,k+1}
+            const double v0 = readsel(bv, k, upper) * i00;
+            const double v1 = (readsel(bv, k + 1, upper) - l10 * v0) * i11;
+            if (r == k) vr = v0;
+            if (r == k + 1) vr = v1;
+            if (r > k + 1) bv -= lr0 * v0 + lr1 * v1;
+        }
+#pragma unroll
+        for (int c = k + 2; c < KP; ++c) {
+            const d2 lc = *reinterpret_cast<const d2 *>(P + pb2(j) + 2 * (c - k));
+            q[c] -= lr0 * lc.x + lr1 * lc.y;
+        }
+#pragma unroll
+        for (int c = k + 2; c < KP; ++c) asm volatile("" : "+v"(q[c]));
+    }
+}
+
+// U = L^{-1} from the pair-packed image P of chol2_rows: lane j (threads 0..31)
+// forward-substitutes column j; result in Us[a][j].
+__device__ __forceinline__ void lower_inverse2(const double *P, double (*Us)[KP + 1], int t) {
+    if (t >= KP) return;
+    const int j = t;
+    double u[KP];
+#pragma unroll
+    for (int a = 0; a < KP; ++a) {
+        double acc = (a == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int b = 0; b < a; ++b) acc -= P[pb2(b >> 1) + 2 * (a - (b & ~1)) + (b & 1)] * u[b];
+        u[a] = acc * P[PACK2 + a];
+    }
+#pragma unroll
+    for (int a = 0; a < KP; ++a) Us[a][j] = u[a];
+}
+
+// ----------------------------------------------------------------------------
+// U = L^{-1} from the LDS image Lt of a lower Cholesky factor (chol_rows): lane j
+// (threads 0..31) forward-substitutes column j; result in Us[a][j].
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ void lower_inverse(const double (*Lt)[LS], double (*Us)[KP + 1], int t) {
+    if (t >= KP) return;
+    const int j = t;
+    double u[KP];
+#pragma unroll
+    for (int a = 0; a < KP; ++a) {
+        double acc = (a == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int b = 0; b < a; ++b) acc -= Lt[b][a] * u[b];    // L[a][b] = Lt[b][a]
+        u[a] = acc * Lt[a][KP];
+    }
+#pragma unroll
+    for (int a = 0; a < KP; ++a) Us[a][j] = u[a];
+}
+
+}  // namespace dcfm

@@ -147,7 +147,8 @@ int64_t dcfm_saved_samples(const dcfm_handle *h);
 #define DCFM_K_SAVE     9
 #define DCFM_K_ASSEMBLE 10
 #define DCFM_K_COMM     11
-#define DCFM_K_COUNT    12
+#define DCFM_K_XCHOL    12
+#define DCFM_K_COUNT    13
 int  dcfm_set_profiling(dcfm_handle *h, int enable);
 int  dcfm_get_kernel_stats(dcfm_handle *h, double ms[DCFM_K_COUNT], int64_t launches[DCFM_K_COUNT]);
 const char *dcfm_kernel_name(int id);
