@@ -170,8 +170,8 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     const dcfm_config &c = *cfg;
     if (c.n < 1 || c.P < 1 || c.g < 1 || c.K < 1)
         return fail(nullptr, DCFM_ERR_INVALID, "n, P, g, K must be >= 1");
-    if (c.K > KP)
-        return fail(nullptr, DCFM_ERR_UNSUPPORTED, "K = %d > %d not supported by this build", c.K, KP);
+    if (c.K > KP_MAX)
+        return fail(nullptr, DCFM_ERR_UNSUPPORTED, "K = %d > %d not supported by this build", c.K, KP_MAX);
     if (!(c.rho >= 0.0 && c.rho <= 1.0)) return fail(nullptr, DCFM_ERR_INVALID, "rho must be in [0,1]");
     if (c.thin < 1 || c.mcmc < 0 || c.burnin < 0)
         return fail(nullptr, DCFM_ERR_INVALID, "thin >= 1, mcmc >= 0, burnin >= 0 required");
@@ -179,7 +179,6 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     if (c.rank < 0 || c.rank >= nranks) return fail(nullptr, DCFM_ERR_INVALID, "bad rank");
     if (c.g % nranks)
         return fail(nullptr, DCFM_ERR_UNSUPPORTED, "g = %d not divisible by nranks = %d", c.g, nranks);
-    if ((int64_t)c.P * c.g > 2000000000LL / 1) {}
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev < 1)
@@ -207,6 +206,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     d.NP = round_up(c.n, 128);
     d.PP = round_up(c.P, 32);
     d.p = c.P * c.g;
+    d.kp = c.K <= 32 ? 32 : (c.K <= 64 ? 64 : 128);
     d.rho = c.rho; d.sr = std::sqrt(c.rho); d.s1r = std::sqrt(1.0 - c.rho);
     d.as_ = c.as_; d.bs = c.bs; d.df = c.df; d.ad1 = c.ad1; d.bd1 = c.bd1; d.ad2 = c.ad2; d.bd2 = c.bd2;
     d.seed = c.seed;
@@ -214,7 +214,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     h->B = c.asm_batch > 0 ? c.asm_batch : 16;
 
     Bufs &b = h->b;
-    const size_t G = d.G, NP = d.NP, PP = d.PP, g = d.g, p = d.p;
+    const size_t G = d.G, NP = d.NP, PP = d.PP, g = d.g, p = d.p, KP = d.kp;
     b.LDB = round_up(h->B * d.K, 16);
     int rc = DCFM_OK;
 #define ALLOC(ptr, n) if ((rc = dalloc(h, &(ptr), (n))) != DCFM_OK) { int r2 = rc; std::string m = h->err; dcfm_destroy(h); g_err = m; return r2; }
@@ -240,7 +240,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     ALLOC(b.XM, 2 * KP * KP);
     ALLOC(b.C, G * PP * KP);
     ALLOC(b.E, G * KP * KP);
-    ALLOC(b.cpart, G * (PP / 8) * KP);
+    ALLOC(b.cpart, G * PP * KP);
     ALLOC(b.sloc, G * KP);
     if (nranks > 1) { ALLOC(b.sall, g * KP); } else b.sall = b.sloc;
     ALLOC(b.Lb[0], p * (size_t)b.LDB);
@@ -345,6 +345,7 @@ int dcfm_set_data(dcfm_handle *h, const double *Yd) {
 
 // P x K x G col-major (j,k,m) at j + P*k + P*K*m  <->  dev [m][j][k] (PP x KP)
 static void pk_to_dev(const Dims &d, const double *src, std::vector<double> &dst) {
+    const int KP = d.kp;
     dst.assign((size_t)d.G * d.PP * KP, 0.0);
     for (int m = 0; m < d.G; ++m)
         for (int k = 0; k < d.K; ++k)
@@ -352,6 +353,7 @@ static void pk_to_dev(const Dims &d, const double *src, std::vector<double> &dst
                 dst[((size_t)m * d.PP + j) * KP + k] = src[(size_t)j + (size_t)d.P * k + (size_t)d.P * d.K * m];
 }
 static void pk_from_dev(const Dims &d, const std::vector<double> &src, double *dst) {
+    const int KP = d.kp;
     for (int m = 0; m < d.G; ++m)
         for (int k = 0; k < d.K; ++k)
             for (int j = 0; j < d.P; ++j)
@@ -359,6 +361,7 @@ static void pk_from_dev(const Dims &d, const std::vector<double> &src, double *d
 }
 // n x K x G col-major (i,k,m) <-> dev [m][i][k] (NP x KP)
 static void nk_to_dev(const Dims &d, const double *src, int G, std::vector<double> &dst) {
+    const int KP = d.kp;
     dst.assign((size_t)G * d.NP * KP, 0.0);
     for (int m = 0; m < G; ++m)
         for (int k = 0; k < d.K; ++k)
@@ -366,6 +369,7 @@ static void nk_to_dev(const Dims &d, const double *src, int G, std::vector<doubl
                 dst[((size_t)m * d.NP + i) * KP + k] = src[(size_t)i + (size_t)d.n * k + (size_t)d.n * d.K * m];
 }
 static void nk_from_dev(const Dims &d, const std::vector<double> &src, int G, double *dst) {
+    const int KP = d.kp;
     for (int m = 0; m < G; ++m)
         for (int k = 0; k < d.K; ++k)
             for (int i = 0; i < d.n; ++i)
@@ -383,11 +387,13 @@ static void p_from_dev(const Dims &d, const std::vector<double> &src, double *ds
 }
 // K x 1 x g col-major (k,m) <-> dev [m][k] (KP), pads 1
 static void k_to_dev(const Dims &d, const double *src, std::vector<double> &dst) {
+    const int KP = d.kp;
     dst.assign((size_t)d.g * KP, 1.0);
     for (int m = 0; m < d.g; ++m)
         for (int k = 0; k < d.K; ++k) dst[(size_t)m * KP + k] = src[(size_t)k + (size_t)d.K * m];
 }
 static void k_from_dev(const Dims &d, const std::vector<double> &src, double *dst) {
+    const int KP = d.kp;
     for (int m = 0; m < d.g; ++m)
         for (int k = 0; k < d.K; ++k) dst[(size_t)k + (size_t)d.K * m] = src[(size_t)m * KP + k];
 }
@@ -432,6 +438,7 @@ int dcfm_get_state(dcfm_handle *h, dcfm_state_view *o) {
     sync_all(h);
     std::vector<double> v;
     int rc;
+    const size_t KP = d.kp;
     const size_t npk = (size_t)d.G * d.PP * KP, nnk = (size_t)d.G * d.NP * KP;
     if (o->Lambda) { if ((rc = down(h, v, h->b.Lam, npk))) return rc; pk_from_dev(d, v, o->Lambda); }
     if (o->psi) { if ((rc = down(h, v, h->b.psi, npk))) return rc; pk_from_dev(d, v, o->psi); }
@@ -532,6 +539,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     }
     HIPC(h, hipSetDevice(h->cfg.device));
     hipStream_t s = h->stream, ss = h->side;
+    const size_t KP = d.kp;
     const size_t nkg = (size_t)d.g * KP;
     HIPC(h, hipEventRecord(h->e_lam, s));      // Lambda/omega of the previous iteration are final
     for (int64_t it = first_iter; it < first_iter + n_iter; ++it) {

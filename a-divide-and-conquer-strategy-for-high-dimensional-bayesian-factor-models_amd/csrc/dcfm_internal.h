@@ -1,22 +1,23 @@
 // Internal layout + kernel launch declarations for libdcfm (MI355X / gfx950).
 //
-// HBM layout (C order, last index fastest), G = local shards, mg = global shard:
+// HBM layout (C order, last index fastest), G = local shards, mg = global shard,
+// KW = d.kp = the padded factor width (32 for K <= 32, 64 for K <= 64, 128 for K <= 128):
 //   Y      [G][NP][PP]   standardised data, rows i padded to NP (x16), cols j to PP (x16), zeros
 //   yy     [G][PP]       sum_i Y_ij^2 (set_data)                -> residual SS identity
-//   Lam    [G][PP][KP]   loadings, k padded to KP = 32 with zeros
+//   Lam    [G][PP][KW]   loadings, k padded to KW with zeros
 //   omega  [G][PP]       diag(Omega);   ps [G][PP]
-//   psi    [G][PP][KP];  Plam [G][PP][KP]
-//   X      [NP][KP]      replicated;    Z [G][NP][KP]
-//   delta, tau [2][g][KP] replicated on every rank, double-buffered per iteration
-//   W      [G][NP][KP]   W_m = Y_m (omega o Lambda_m)                    (k_wpass)
-//   A      [G][KP][KP]   A_m = Lambda_m' diag(omega) Lambda_m             (k_prep)
-//   ZM     [G][4][KP][KP] Z-draw operators {M1, M2, U, NA} of shard m         (k_prep)
-//   Sp     [G][NP][KP]   per-shard X message W_m - sqrt(1-rho) A_m Z_m'   (k_zdraw)
-//   xin    [NP][KP]      local sum over shards of Sp;  xall [nranks][NP][KP] all-gathered (== xin if 1 rank)
-//   xa, xa_all [nranks][KP][KP]  per-rank sum of A_m (gathered);  XM [2][KP][KP] X-draw operators {Tx, Ux} (k_xchol)
-//   C      [G][PP][KP]   C_m = Y_m' eta_m  (k_cpass);  E [G][KP][KP] = eta_m' eta_m
-//   cpart  [G][PP/8][KP] per-8-row partial column sums of psi o Lambda^2 (k_lambda)
-//   sloc   [G][KP], sall [g][KP]  column sums (all-gathered)
+//   psi    [G][PP][KW];  Plam [G][PP][KW]
+//   X      [NP][KW]      replicated;    Z [G][NP][KW]
+//   delta, tau [2][g][KW] replicated on every rank, double-buffered per iteration
+//   W      [G][NP][KW]   W_m = Y_m (omega o Lambda_m)                    (k_wpass)
+//   A      [G][KW][KW]   A_m = Lambda_m' diag(omega) Lambda_m             (k_prep)
+//   ZM     [G][4][KW][KW] Z-draw operators {M1, M2, U, NA} of shard m         (k_prep)
+//   Sp     [G][NP][KW]   per-shard X message W_m - sqrt(1-rho) A_m Z_m'   (k_zdraw)
+//   xin    [NP][KW]      local sum over shards of Sp;  xall [nranks][NP][KW] all-gathered (== xin if 1 rank)
+//   xa, xa_all [nranks][KW][KW]  per-rank sum of A_m (gathered);  XM [2][KW][KW] X-draw operators {Tx, Ux} (k_xchol)
+//   C      [G][PP][KW]   C_m = Y_m' eta_m  (k_cpass);  E [G][KW][KW] = eta_m' eta_m
+//   cpart  [G][PP/8][KW] (KW = 32) or [G][PP][KW] (wide) per-8-row partial column sums of psi o Lambda^2 (k_lambda)
+//   sloc   [G][KW], sall [g][KW]  column sums (all-gathered)
 //   Lb     [2][p][LDB]   saved Lambda rows of an assembly batch (double-buffered), sample s at cols s*K..
 //   wsum   [2][p]        sum of saved omega of the batch
 //   Sigma  [p][p]        lower triangle accumulated (each rank: its tiles), mirrored on get
@@ -26,7 +27,8 @@
 
 namespace dcfm {
 
-constexpr int KP = 32;         // padded factor count (K <= 32 in this build)
+constexpr int KP = 32;         // padded factor width of the narrow (K <= 32) kernels
+constexpr int KP_MAX = 128;    // widest supported padding (K <= 128, config c4 has K = 100)
 constexpr int ASM_TILE = 128;  // covariance-assembly output tile
 
 struct Dims {
@@ -35,6 +37,7 @@ struct Dims {
     int shard0;                 // first global shard of this rank
     int nranks, rank;
     int p;                      // P * g
+    int kp;                     // padded factor width KW of every [..][KW] array: 32, 64 or 128
     double rho, sr, s1r;        // rho, sqrt(rho), sqrt(1-rho)
     double as_, bs, df, ad1, bd1, ad2, bd2;
     uint64_t seed;
@@ -78,5 +81,18 @@ void launch_mirror(double *S, int p, hipStream_t s);
 void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s);
 void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,
                      int64_t count, double *out, hipStream_t s);
+
+// wide-factor kernels (kp = 64 / 128; kernels_wide.hip), dispatched from the launchers above
+namespace wide {
+void launch_prep(const Dims &d, const Bufs &b, hipStream_t s);
+void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
+void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
+void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
+void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *tau_cur,
+                   hipStream_t s);
+void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s);
+void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
+                  const double *tau_in, double *delta_out, double *tau_out, hipStream_t s);
+}  // namespace wide
 
 }  // namespace dcfm

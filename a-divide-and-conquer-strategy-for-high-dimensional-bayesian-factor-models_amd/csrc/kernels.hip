@@ -127,22 +127,15 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
     }
 }
 
-// XCD-aware block remap (bijective): hardware deals consecutive block ids
-// round-robin over the 8 XCDs; give each XCD a contiguous range of work items
-// so that blocks sharing operands (one shard's tiles) share one L2.
-__device__ __forceinline__ int xcd_remap(int b, int total) {
-    const int xcd = b & 7, slot = b >> 3;
-    const int q = total >> 3, rem = total & 7;
-    return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + slot;
-}
-
 // ============================================================================
 // k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA, Y pass 1
-// one wave = (shard m, 32 rows i = 2 M-tiles) x 32 k (even / odd k N-tiles),
+// one wave = (shard m, 32 rows i = 2 M-tiles) x 32 k (even / odd k N-tiles) of
+// column tile kt = blockIdx.y (KW/32 tiles; the wide layouts re-read Y from L2/MALL),
 // reduction over j in chunks of 8: lane (r, q) holds Y[i0+r][8t+2q .. +1] (16 B);
 // k-step 2t uses element 0, 2t+1 element 1; the B operand (w_j L[j][2r], w_j L[j][2r+1])
 // uses the same j <-> (q, e) map.  Register double-buffered prefetch of 2 chunks.
 // ============================================================================
+template <int KW>
 __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict__ Y,
                                                const double *__restrict__ Lam,
                                                const double *__restrict__ omega,
@@ -155,7 +148,8 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
     const int r = lane & 15, q = lane >> 4;
     const double *Y0 = Y + ((size_t)m * d.NP + i0 + r) * d.PP + 2 * q;
     const double *Y1 = Y0 + (size_t)16 * d.PP;
-    const double *L = Lam + (size_t)m * d.PP * KP + 2 * r;
+    const int kt = blockIdx.y;
+    const double *L = Lam + (size_t)m * d.PP * KW + 32 * kt + 2 * r;
     const double *wp = omega + (size_t)m * d.PP + 2 * q;
     d4 acc[2][2];
 #pragma unroll
@@ -170,8 +164,8 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
         y0 = *reinterpret_cast<const d2 *>(Y0 + j);                                 \
         y1 = *reinterpret_cast<const d2 *>(Y1 + j);                                 \
         ww = *reinterpret_cast<const d2 *>(wp + j);                                 \
-        l0 = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q) * KP);           \
-        l1 = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q + 1) * KP);       \
+        l0 = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q) * KW);           \
+        l1 = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q + 1) * KW);       \
     }
 #define WP_MMA(y0, y1, ww, l0, l1)                                                  \
     {                                                                               \
@@ -198,13 +192,13 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
     // D row = q + 4g (row i), col = r (k = 2r + tb)
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-        double *Wt = W + ((size_t)m * d.NP + i0 + 16 * a) * KP + 2 * r;
+        double *Wt = W + ((size_t)m * d.NP + i0 + 16 * a) * KW + 32 * kt + 2 * r;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             d2 v;
             v.x = acc[a][0][g];
             v.y = acc[a][1][g];
-            *reinterpret_cast<d2 *>(Wt + (size_t)(q + 4 * g) * KP) = v;
+            *reinterpret_cast<d2 *>(Wt + (size_t)(q + 4 * g) * KW) = v;
         }
     }
 }
@@ -322,7 +316,7 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
 // ============================================================================
 __global__ __launch_bounds__(256) void k_xred(Dims d, const double *__restrict__ Sp,
                                               double *__restrict__ xin) {
-    const size_t total = (size_t)d.NP * KP;
+    const size_t total = (size_t)d.NP * d.kp;
     const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (e >= total) return;
     double acc = 0.0;
@@ -337,10 +331,11 @@ __global__ __launch_bounds__(256) void k_xred(Dims d, const double *__restrict__
 __global__ __launch_bounds__(256) void k_asum(Dims d, const double *__restrict__ A,
                                               double *__restrict__ xa) {
     const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= KP * KP) return;
+    const int kk = d.kp * d.kp;
+    if (e >= kk) return;
     double v = 0.0;
 #pragma unroll 8
-    for (int m = 0; m < d.G; ++m) v += A[(size_t)m * KP * KP + e];
+    for (int m = 0; m < d.G; ++m) v += A[(size_t)m * kk + e];
     xa[e] = v;
 }
 
@@ -453,25 +448,38 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
 
 // ============================================================================
 // k_cpass: [C_m | E_m] = [Y_m | eta_m]' eta_m    fp64 MFMA, Y pass 2      dc:133,138,141
-// block = (shard m, 32-column tile of [Y | eta]); its 4 waves split the
-// reduction over rows i, partial 32x32 tiles summed in LDS in a fixed order.
+// block = (shard m, 32-column tile of [Y | eta]) x (32-column tile kt of eta,
+// blockIdx.y); its 4 waves split the reduction over rows i, partial 32x32 tiles
+// summed in LDS in a fixed order.
 // Lane (r, q) loads 16 B: Y[i][c0+2r .. +1] and eta[i][2r .. +1] (formed on the
 // fly from X and Z), i = 4s + q, so the MFMA tiles are even/odd columns x
 // even/odd k.  Register double-buffered prefetch, 4 k-steps per batch.
 // ============================================================================
-template <bool IS_E>
+// IS_E: the A operand is eta itself, columns te*32.. (Yp = nullptr; Xa/Za point at
+// them); SAME_T: te == kt, so the A operand is the B operand (no extra loads).
+template <int KW, bool IS_E, bool SAME_T>
 __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restrict__ Yp,
                                            const double *__restrict__ Xp,
-                                           const double *__restrict__ Zp, int s0, int nsw,
+                                           const double *__restrict__ Zp,
+                                           const double *__restrict__ Xa,
+                                           const double *__restrict__ Za, int s0, int nsw,
                                            int q, d4 (&acc)[2][2]) {
+    constexpr bool EXTRA = IS_E && !SAME_T;
     d2 yA[4], xA[4], zA[4], yB[4], xB[4], zB[4];
     auto load = [&](int s, d2 (&y)[4], d2 (&x)[4], d2 (&z)[4]) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int i = 4 * (s + u) + q;
-            x[u] = *reinterpret_cast<const d2 *>(Xp + (size_t)i * KP);
-            z[u] = *reinterpret_cast<const d2 *>(Zp + (size_t)i * KP);
-            if (!IS_E) y[u] = *reinterpret_cast<const d2 *>(Yp + (size_t)i * d.PP);
+            x[u] = *reinterpret_cast<const d2 *>(Xp + (size_t)i * KW);
+            z[u] = *reinterpret_cast<const d2 *>(Zp + (size_t)i * KW);
+            if (!IS_E) {
+                y[u] = *reinterpret_cast<const d2 *>(Yp + (size_t)i * d.PP);
+            } else if (EXTRA) {   // eta of tile te, formed into y
+                const d2 xa = *reinterpret_cast<const d2 *>(Xa + (size_t)i * KW);
+                const d2 za = *reinterpret_cast<const d2 *>(Za + (size_t)i * KW);
+                y[u].x = eta_of(d.sr, d.s1r, xa.x, za.x);
+                y[u].y = eta_of(d.sr, d.s1r, xa.y, za.y);
+            }
         }
     };
     auto mma = [&](d2 (&y)[4], d2 (&x)[4], d2 (&z)[4]) {
@@ -479,7 +487,7 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
         for (int u = 0; u < 4; ++u) {
             const double e0 = eta_of(d.sr, d.s1r, x[u].x, z[u].x);
             const double e1 = eta_of(d.sr, d.s1r, x[u].y, z[u].y);
-            const double a0 = IS_E ? e0 : y[u].x, a1 = IS_E ? e1 : y[u].y;
+            const double a0 = (IS_E && SAME_T) ? e0 : y[u].x, a1 = (IS_E && SAME_T) ? e1 : y[u].y;
             acc[0][0] = mfma16x16x4(a0, e0, acc[0][0]);
             acc[0][1] = mfma16x16x4(a0, e1, acc[0][1]);
             acc[1][0] = mfma16x16x4(a1, e0, acc[1][0]);
@@ -496,29 +504,35 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
     }
 }
 
+template <int KW>
 __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict__ Y,
                                                const double *__restrict__ X,
                                                const double *__restrict__ Z,
                                                double *__restrict__ C, double *__restrict__ E) {
     __shared__ double red[4][32][33];
-    const int nt = (d.PP + KP) >> 5;
+    const int nt = (d.PP + KW) >> 5;
     const int w = xcd_remap(blockIdx.x, gridDim.x);
     const int m = w / nt, tile = w % nt;
+    const int kt = blockIdx.y;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c0 = tile * 32;
     const bool isE = c0 >= d.PP;
+    const int te = isE ? (c0 - d.PP) >> 5 : 0;
     const int r = lane & 15, q = lane >> 4;
     const double *Yp = Y + (size_t)m * d.NP * d.PP + c0 + 2 * r;
-    const double *Xp = X + 2 * r;
-    const double *Zp = Z + (size_t)m * d.NP * KP + 2 * r;
+    const double *Xp = X + 32 * kt + 2 * r;
+    const double *Zp = Z + (size_t)m * d.NP * KW + 32 * kt + 2 * r;
+    const double *Xa = X + 32 * te + 2 * r;
+    const double *Za = Z + (size_t)m * d.NP * KW + 32 * te + 2 * r;
     const int nsw = d.NP >> 4;                 // k-steps (4 rows each) per wave
     d4 acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-    if (isE) cpass_wave<true>(d, Yp, Xp, Zp, wave * nsw, nsw, q, acc);
-    else cpass_wave<false>(d, Yp, Xp, Zp, wave * nsw, nsw, q, acc);
+    if (!isE) cpass_wave<KW, false, false>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc);
+    else if (te == kt) cpass_wave<KW, true, true>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc);
+    else cpass_wave<KW, true, false>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc);
     // D row rho = q + 4g -> column c0 + 2 rho + ta;  D col r -> k = 2r + tb
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -529,10 +543,11 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
             for (int tb = 0; tb < 2; ++tb) red[wave][2 * rho + ta][2 * r + tb] = acc[ta][tb][g];
     }
     __syncthreads();
-    double *out = isE ? (E + (size_t)m * KP * KP) : (C + ((size_t)m * d.PP + c0) * KP);
-    for (int e = threadIdx.x; e < 32 * KP; e += 256) {
-        const int a = e / KP, b = e % KP;
-        out[e] = (red[0][a][b] + red[1][a][b]) + (red[2][a][b] + red[3][a][b]);
+    double *out = isE ? (E + (size_t)m * KW * KW + (size_t)(32 * te) * KW + 32 * kt)
+                      : (C + ((size_t)m * d.PP + c0) * KW + 32 * kt);
+    for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+        const int a = e >> 5, b = e & 31;
+        out[(size_t)a * KW + b] = (red[0][a][b] + red[1][a][b]) + (red[2][a][b] + red[3][a][b]);
     }
 }
 
@@ -695,30 +710,6 @@ __global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict
 // grid = all g shards (delta/tau replicated on every rank); local blocks also
 // refresh Plam = psi o tau'.
 // ============================================================================
-__device__ __forceinline__ double wave_scan_prod(double v, int l) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double u = __shfl_up(v, o, 64);
-        if (l >= o) v *= u;
-    }
-    return v;
-}
-
-__device__ __forceinline__ double wave_suffix_sum(double v, int l) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double u = __shfl_down(v, o, 64);
-        if (l + o < 64) v += u;
-    }
-    return v;
-}
-
-__device__ double delta_G(const Dims &d, const DrawsDev &dr, int64_t iter, int mg, int h) {
-    if (d.inject) return dr.Gdelta[((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + h];
-    const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - h);
-    const Rng rng(d.seed);
-    return rng.gamma(shape, SITE_DELTA, mg, 0, h, (uint32_t)iter);
-}
 
 // lane l < K holds delta_old_l, T_l, G_l, 1/delta_old_l and 1/dref_l; returns delta_new_l
 __device__ double delta_chain(const Dims &d, int l, double T, double G, double idold, double idref) {
@@ -816,7 +807,7 @@ __global__ __launch_bounds__(256) void k_save(Dims d, const double *__restrict__
         const size_t jm = e / d.K;
         const int j = jm % d.P, m = jm / d.P;
         const size_t a = (size_t)(d.shard0 + m) * d.P + j;
-        Lb[a * LDB + (size_t)slot * d.K + k] = Lam[((size_t)m * d.PP + j) * KP + k];
+        Lb[a * LDB + (size_t)slot * d.K + k] = Lam[((size_t)m * d.PP + j) * d.kp + k];
         if (k == 0) wsum[a] += omega[(size_t)m * d.PP + j];
     }
 }
@@ -920,10 +911,10 @@ __global__ __launch_bounds__(256) void k_mirror(double *__restrict__ S, int p) {
 
 __global__ __launch_bounds__(256) void k_eta(Dims d, const double *__restrict__ X,
                                              const double *__restrict__ Z, double *__restrict__ eta) {
-    const size_t total = (size_t)d.G * d.NP * KP;
+    const size_t total = (size_t)d.G * d.NP * d.kp;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total;
          e += (size_t)gridDim.x * blockDim.x) {
-        const size_t ik = e % ((size_t)d.NP * KP);
+        const size_t ik = e % ((size_t)d.NP * d.kp);
         eta[e] = eta_of(d.sr, d.s1r, X[ik], Z[e]);
     }
 }
@@ -945,44 +936,62 @@ __global__ __launch_bounds__(256) void k_rng_fill(uint64_t seed, int kind, doubl
 // ============================================================================
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// kp == 32: the register-blocked narrow kernels of this file; kp = 64 / 128: the
+// wide kernels of kernels_wide.hip (wide::).  Layout-generic kernels are templated.
 void launch_prep(const Dims &d, const Bufs &b, hipStream_t s) {
+    if (d.kp != KP) return wide::launch_prep(d, b, s);
     hipLaunchKernelGGL(k_prep, dim3(d.G), dim3(256), 0, s, d, b.Lam, b.omega, b.A, b.ZM);
 }
 void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s) {
-    hipLaunchKernelGGL(k_wpass, dim3((d.NP / 128) * d.G), dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W);
+    const dim3 grid((d.NP / 128) * d.G, d.kp / 32);
+    switch (d.kp) {
+    case 32: hipLaunchKernelGGL(k_wpass<32>, grid, dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W); break;
+    case 64: hipLaunchKernelGGL(k_wpass<64>, grid, dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W); break;
+    default: hipLaunchKernelGGL(k_wpass<128>, grid, dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W); break;
+    }
 }
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+    if (d.kp != KP) return wide::launch_zdraw(d, b, dr, iter, s);
     hipLaunchKernelGGL(k_zdraw, dim3((d.NP / 128) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
                        dr, iter);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
-    const int total = d.NP * KP;
+    const int total = d.NP * d.kp;
     hipLaunchKernelGGL(k_xred, dim3(cdiv(total, 256)), dim3(256), 0, s, d, b.Sp, b.xin);
 }
 void launch_asum(const Dims &d, const Bufs &b, hipStream_t s) {
-    hipLaunchKernelGGL(k_asum, dim3(KP * KP / 256), dim3(256), 0, s, d, b.A, b.xa);
+    hipLaunchKernelGGL(k_asum, dim3(cdiv(d.kp * d.kp, 256)), dim3(256), 0, s, d, b.A, b.xa);
 }
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
+    if (d.kp != KP) return wide::launch_xchol(d, b, s);
     hipLaunchKernelGGL(k_xchol, dim3(1), dim3(64), 0, s, d, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
 }
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+    if (d.kp != KP) return wide::launch_xdraw(d, b, dr, iter, s);
     hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(64), 0, s, d, b.xall, b.XM, b.X, dr, iter);
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
-    const int nt = (d.PP + KP) / 32;
-    hipLaunchKernelGGL(k_cpass, dim3(nt * d.G), dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E);
+    const dim3 grid(((d.PP + d.kp) / 32) * d.G, d.kp / 32);
+    switch (d.kp) {
+    case 32: hipLaunchKernelGGL(k_cpass<32>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
+    case 64: hipLaunchKernelGGL(k_cpass<64>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
+    default: hipLaunchKernelGGL(k_cpass<128>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
+    }
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, hipStream_t s) {
+    if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, s);
     hipLaunchKernelGGL(k_lambda, dim3(cdiv(d.P, 8), d.G), dim3(256), 0, s, d, b.C, b.E, b.yy, tau_cur,
                        b.Lam, b.psi, b.Plam, b.ps, b.omega, b.cpart, dr, iter);
 }
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s) {
+    if (d.kp != KP) return wide::launch_colsum(d, b, s);
     hipLaunchKernelGGL(k_colsum, dim3(d.G), dim3(256), 0, s, d, b.cpart, b.sloc);
 }
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                   const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
                   hipStream_t s) {
+    if (d.kp != KP) return wide::launch_delta(d, b, dr, iter, delta_in, tau_in, delta_out, tau_out, s);
     hipLaunchKernelGGL(k_delta, dim3(d.g), dim3(256), 0, s, d, b.sall, delta_in, tau_in, delta_out,
                        tau_out, b.psi, b.Plam, dr, iter);
 }
@@ -1002,7 +1011,7 @@ void launch_mirror(double *S, int p, hipStream_t s) {
     hipLaunchKernelGGL(k_mirror, dim3(nt, nt), dim3(256), 0, s, S, p);
 }
 void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s) {
-    const size_t total = (size_t)d.G * d.NP * KP;
+    const size_t total = (size_t)d.G * d.NP * d.kp;
     const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
     hipLaunchKernelGGL(k_eta, dim3(grid), dim3(256), 0, s, d, b.X, b.Z, eta_out);
 }

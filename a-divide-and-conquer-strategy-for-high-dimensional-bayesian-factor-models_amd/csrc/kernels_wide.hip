@@ -1,0 +1,761 @@
+// Wide-factor kernels (K = 33 .. 128, padded width KW = 64 or 128) for the Gibbs
+// sweep of divideconquer.m:90-178.  Config c4 of BASELINE.json (p = 10,000,
+// n = 2,000, K = 100) runs here; K <= 32 uses the register-blocked narrow
+// kernels of kernels.hip.  The layout-generic kernels (k_wpass, k_cpass, k_xred,
+// k_asum, k_save, k_assemble) are shared and templated on KW in kernels.hip.
+//
+// Kernel map (same dataflow as the narrow path)                reference lines
+//   k_gram     A_m = Lambda' diag(w) Lambda, 32x32 tiles, fp64 MFMA    dc:98-99,114-115
+//   k_prep     Zprec chol (LDS, packed), U = L^-1, T = U U',           dc:100-107
+//              Z-draw operators {M1, M2, U, NA} of shard m
+//   k_xchol    Xprec = g I + rho sum A, chol, {Tx, Ux}                  dc:117-118
+//   k_zdraw    Z' = M1 W' + M2 X' + U eps'; S' = W' + NA Z'  fp64 MFMA  dc:101-107,121-123
+//   k_xdraw    X' = Tx S' + Ux eps'                           fp64 MFMA  dc:119-128
+//   k_lambda   one workgroup per loading row j: register-blocked        dc:140-145,150,
+//              Cholesky of Q_j (8x8 blocks per thread), fused forward   dc:156,169-171
+//              solve, blocked back solve; psi, SS identity, ps, omega
+//   k_colsum   column sums of psi o Lambda^2                            dc:156
+//   k_delta    MGP chain over up to 128 factors (2 per lane), Plam      dc:155-165,175-177
+#include "dcfm_internal.h"
+#include "philox.h"
+#include "linalg.h"
+
+namespace dcfm {
+namespace wide {
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// packed lower column-major storage of an N x N matrix: (r, c), r >= c, at cbp(N, c) + r - c
+__device__ __forceinline__ int cbp(int N, int c) { return c * N - (c * (c - 1)) / 2; }
+
+// ----------------------------------------------------------------------------
+// Workgroup (256 threads) Cholesky of a packed SPD matrix in LDS, right-looking,
+// column by column (the K x K systems of dc:100,118 — g+1 per iteration, off the
+// critical path).  On return A holds L (packed) and dinv[k] = 1/L_kk.
+// ----------------------------------------------------------------------------
+__device__ void wg_chol_packed(double *A, double *dinv, int N) {
+    const int t = threadIdx.x, tr = t & 15, tc = t >> 4;
+    for (int k = 0; k < N; ++k) {
+        const int ck = cbp(N, k);
+        const double piv = A[ck];
+        const double ikk = rsqrt_f64(piv);
+        __syncthreads();
+        if (t == 0) {
+            A[ck] = piv * ikk;
+            dinv[k] = ikk;
+        }
+        for (int r = k + 1 + t; r < N; r += 256) A[ck + r - k] *= ikk;
+        __syncthreads();
+        for (int c = k + 1 + tc; c < N; c += 16) {
+            const double lc = A[ck + c - k];
+            const int cc = cbp(N, c);
+            for (int r = c + tr; r < N; r += 16) A[cc + r - c] -= A[ck + r - k] * lc;
+        }
+        __syncthreads();
+    }
+}
+
+// U = L^{-1} (packed, same layout): thread j forward-substitutes column j.
+__device__ void wg_lower_inverse_packed(const double *L, const double *dinv, double *U, int N) {
+    for (int j = threadIdx.x; j < N; j += blockDim.x) {
+        const int cj = cbp(N, j);
+        for (int a = j; a < N; ++a) {
+            double acc = (a == j) ? 1.0 : 0.0;
+            for (int b = j; b < a; ++b) acc -= L[cbp(N, b) + a - b] * U[cj + b - j];
+            U[cj + a - j] = acc * dinv[a];
+        }
+    }
+    __syncthreads();
+}
+
+// T = U U' (symmetric) into packed Tpk, from packed lower U
+__device__ void wg_uut_packed(const double *U, double *Tpk, int N) {
+    const int tot = N * (N + 1) / 2;
+    for (int e = threadIdx.x; e < tot; e += blockDim.x) {
+        // e -> (a, c), a >= c, column-major packed
+        int c = 0;
+        while (cbp(N, c + 1) <= e) ++c;
+        const int a = c + (e - cbp(N, c));
+        double acc = 0.0;
+        for (int b = 0; b <= c; ++b) acc += U[cbp(N, b) + a - b] * U[cbp(N, b) + c - b];
+        Tpk[e] = acc;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ double packed_sym(const double *S, int N, int a, int c) {
+    return a >= c ? S[cbp(N, c) + a - c] : S[cbp(N, a) + c - a];
+}
+__device__ __forceinline__ double packed_low(const double *L, int N, int a, int c) {
+    return a >= c ? L[cbp(N, c) + a - c] : 0.0;
+}
+
+// ============================================================================
+// k_gram: A_m = (w o Lambda_m)' Lambda_m, 32x32 tile (ta, tb) per block; the 4
+// waves split the rows j, partial tiles summed in LDS in a fixed order.  dc:98-99
+// Lane (r, q), k-step s: rows j = j0 + 4s + q; A operand w_j L[j][32ta+2r+ea],
+// B operand L[j][32tb+2r+eb]  ->  acc[ea][eb][g] = A[32ta+2(q+4g)+ea][32tb+2r+eb].
+// ============================================================================
+template <int KW>
+__global__ __launch_bounds__(256) void k_gram(Dims d, const double *__restrict__ Lam,
+                                              const double *__restrict__ omega, double *__restrict__ A) {
+    constexpr int KT = KW / 32;
+    __shared__ double red[4][32][33];
+    const int m = blockIdx.y, ta = blockIdx.x / KT, tb = blockIdx.x % KT;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 15, q = lane >> 4;
+    const double *L = Lam + (size_t)m * d.PP * KW;
+    const double *w = omega + (size_t)m * d.PP;
+    const int rows = d.PP >> 2, j0 = wave * rows;
+    d4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int s = 0; s < rows; s += 4) {
+        const int j = j0 + s + q;
+        const double wj = w[j];
+        const d2 la = *reinterpret_cast<const d2 *>(L + (size_t)j * KW + 32 * ta + 2 * r);
+        const d2 lb = *reinterpret_cast<const d2 *>(L + (size_t)j * KW + 32 * tb + 2 * r);
+        const double a0 = la.x * wj, a1 = la.y * wj;
+        acc[0][0] = mfma16x16x4(a0, lb.x, acc[0][0]);
+        acc[0][1] = mfma16x16x4(a0, lb.y, acc[0][1]);
+        acc[1][0] = mfma16x16x4(a1, lb.x, acc[1][0]);
+        acc[1][1] = mfma16x16x4(a1, lb.y, acc[1][1]);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int ea = 0; ea < 2; ++ea)
+#pragma unroll
+            for (int eb = 0; eb < 2; ++eb) red[wave][2 * (q + 4 * g) + ea][2 * r + eb] = acc[ea][eb][g];
+    __syncthreads();
+    double *out = A + (size_t)m * KW * KW + (size_t)(32 * ta) * KW + 32 * tb;
+    for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+        const int a = e >> 5, b = e & 31;
+        out[(size_t)a * KW + b] = (red[0][a][b] + red[1][a][b]) + (red[2][a][b] + red[3][a][b]);
+    }
+}
+
+// ============================================================================
+// k_prep: Z-draw operators of shard m (one block per local shard).        dc:100-107
+//   R = cholcov(Zprec), Zprec = I + (1-rho) A_m; cholcov reads the upper triangle,
+//   so the lower factor L = R' is the Cholesky of S[r][c] = Zprec[c][r] (c <= r).
+//   U = L^{-1}, T = U U';  ZM = {M1 = s1r T, M2 = -s1r sr T A, U, NA = -s1r A}
+//   (the reference's R'\(R\bz) + R'\z is T bz + U z, quirk Q2).  Padding (>= K) is 0.
+// ============================================================================
+template <int KW>
+__global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__ A, double *__restrict__ ZM) {
+    constexpr int PK = KW * (KW + 1) / 2;
+    __shared__ double S1[PK], S2[PK], dinv[KW];
+    const int m = blockIdx.x, N = d.K, t = threadIdx.x;
+    const double *Am = A + (size_t)m * KW * KW;
+    for (int c = 0; c < N; ++c)
+        for (int r = c + t; r < N; r += 256) S1[cbp(N, c) + r - c] = (r == c ? 1.0 : 0.0) + (1.0 - d.rho) * Am[(size_t)c * KW + r];
+    __syncthreads();
+    wg_chol_packed(S1, dinv, N);
+    wg_lower_inverse_packed(S1, dinv, S2, N);   // U -> S2
+    wg_uut_packed(S2, S1, N);                   // T -> S1 (L no longer needed)
+    double *Zm = ZM + (size_t)m * 4 * KW * KW;
+    const double s2 = -d.s1r * d.sr;
+    for (int e = t; e < KW * KW; e += 256) {
+        const int a = e / KW, c = e % KW;
+        double m1 = 0.0, m2 = 0.0, u = 0.0, na = 0.0;
+        if (a < N && c < N) {
+            m1 = d.s1r * packed_sym(S1, N, a, c);
+            u = packed_low(S2, N, a, c);
+            na = -d.s1r * Am[e];
+            double acc = 0.0;
+            for (int b = 0; b < N; ++b) acc += packed_sym(S1, N, a, b) * Am[(size_t)b * KW + c];
+            m2 = s2 * acc;
+        }
+        Zm[e] = m1;
+        Zm[(size_t)KW * KW + e] = m2;
+        Zm[(size_t)2 * KW * KW + e] = u;
+        Zm[(size_t)3 * KW * KW + e] = na;
+    }
+}
+
+// ============================================================================
+// k_xchol: Xprec = g I + rho sum_m A_m (dc:117, summed over ranks in rank order),
+// Rx = cholcov(Xprec) (dc:118); XM = {Tx = sqrt(rho) Ux Ux', Ux = Rx^{-T}}.
+// ============================================================================
+template <int KW>
+__global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict__ xa_all, double *__restrict__ XM) {
+    constexpr int PK = KW * (KW + 1) / 2;
+    __shared__ double S1[PK], S2[PK], dinv[KW];
+    const int N = d.K, t = threadIdx.x;
+    for (int c = 0; c < N; ++c)
+        for (int r = c + t; r < N; r += 256) {
+            const size_t e = (size_t)c * KW + r;   // upper triangle: Xprec[c][r]
+            double v = xa_all[e];
+            for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * KW * KW + e];
+            S1[cbp(N, c) + r - c] = (r == c ? (double)d.g : 0.0) + d.rho * v;
+        }
+    __syncthreads();
+    wg_chol_packed(S1, dinv, N);
+    wg_lower_inverse_packed(S1, dinv, S2, N);
+    wg_uut_packed(S2, S1, N);
+    for (int e = t; e < KW * KW; e += 256) {
+        const int a = e / KW, c = e % KW;
+        const bool in = a < N && c < N;
+        XM[e] = in ? d.sr * packed_sym(S1, N, a, c) : 0.0;
+        XM[(size_t)KW * KW + e] = in ? packed_low(S2, N, a, c) : 0.0;
+    }
+}
+
+// standard normals eps[i][kk], eps[i][kk+1] of a Z / X row (kk even)       dc:104,126
+__device__ __forceinline__ d2 row_normals(const Dims &d, const double *inj, bool live, int site, int mg, int i,
+                                          int kk, int64_t iter) {
+    d2 ev = {0.0, 0.0};
+    if (!live || kk >= d.K) return ev;
+    if (d.inject) {
+        ev.x = inj[kk];
+        ev.y = (kk + 1 < d.K) ? inj[kk + 1] : 0.0;
+    } else {
+        const Rng rng(d.seed);
+        double n0, n1;
+        rng.normal2(site, mg, i, kk >> 1, (uint32_t)iter, n0, n1);
+        ev.x = n0;
+        ev.y = (kk + 1 < d.K) ? n1 : 0.0;
+    }
+    return ev;
+}
+
+// ============================================================================
+// k_zdraw: per (shard m, 64 rows), one wave per 16 rows i.                  dc:101-107,121-123
+//   Z' = M1 W' + M2 X' + U eps'   (KW x 16, MT = KW/16 MFMA tiles, operators from L2)
+//   S' = W' + NA Z'               the C/D layout of Z' (row = q + 4g) is the B operand
+// ============================================================================
+template <int KW>
+__global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W, const double *__restrict__ ZM,
+                                               const double *__restrict__ X, double *__restrict__ Z,
+                                               double *__restrict__ Sp, DrawsDev dr, int64_t iter) {
+    constexpr int MT = KW / 16;
+    const int nrb = d.NP >> 6;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int m = w / nrb, rb = w % nrb;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, q = lane >> 4;
+    const int mg = d.shard0 + m;
+    const int i = rb * 64 + wave * 16 + c;
+    const bool live = i < d.n;
+    const double *M1 = ZM + (size_t)m * 4 * KW * KW, *M2 = M1 + KW * KW, *U = M2 + KW * KW, *NA = U + KW * KW;
+    const double *Wi = W + ((size_t)m * d.NP + i) * KW;
+    const double *Xi = X + (size_t)i * KW;
+    const double *nz = d.inject ? dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K
+                                : nullptr;
+    d4 az[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) az[mt] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 2
+    for (int t = 0; t < KW / 8; ++t) {
+        const int kk = 8 * t + 2 * q;
+        const d2 wv = *reinterpret_cast<const d2 *>(Wi + kk);
+        const d2 xv = *reinterpret_cast<const d2 *>(Xi + kk);
+        const d2 ev = row_normals(d, nz, live, SITE_Z, mg, i, kk, iter);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const size_t o = (size_t)(16 * mt + c) * KW + kk;
+            const d2 a1 = *reinterpret_cast<const d2 *>(M1 + o);
+            const d2 a2 = *reinterpret_cast<const d2 *>(M2 + o);
+            const d2 a3 = *reinterpret_cast<const d2 *>(U + o);
+            az[mt] = mfma16x16x4(a1.x, wv.x, az[mt]);
+            az[mt] = mfma16x16x4(a2.x, xv.x, az[mt]);
+            az[mt] = mfma16x16x4(a3.x, ev.x, az[mt]);
+            az[mt] = mfma16x16x4(a1.y, wv.y, az[mt]);
+            az[mt] = mfma16x16x4(a2.y, xv.y, az[mt]);
+            az[mt] = mfma16x16x4(a3.y, ev.y, az[mt]);
+        }
+    }
+    d4 as[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) as[mt][g] = Wi[16 * mt + q + 4 * g];
+#pragma unroll
+    for (int mt2 = 0; mt2 < MT; ++mt2)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int kk = 16 * mt2 + 4 * g + q;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+                as[mt] = mfma16x16x4(NA[(size_t)(16 * mt + c) * KW + kk], az[mt2][g], as[mt]);
+        }
+    double *Zr = Z + ((size_t)m * d.NP + i) * KW;
+    double *Sr = Sp + ((size_t)m * d.NP + i) * KW;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int k = 16 * mt + q + 4 * g;
+            if (live) Zr[k] = (k < d.K) ? az[mt][g] : 0.0;
+            Sr[k] = live ? as[mt][g] : 0.0;
+        }
+}
+
+// ============================================================================
+// k_xdraw: X' = Tx S' + Ux eps' (S summed over ranks in rank order), one wave per
+// 16 rows.                                                                   dc:119-128
+// ============================================================================
+template <int KW>
+__global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__ xall, const double *__restrict__ XM,
+                                              double *__restrict__ X, DrawsDev dr, int64_t iter) {
+    constexpr int MT = KW / 16;
+    const int lane = threadIdx.x, c = lane & 15, q = lane >> 4;
+    const int i = blockIdx.x * 16 + c;
+    const bool live = i < d.n;
+    const size_t stride = (size_t)d.NP * KW;
+    const double *Tx = XM, *Ux = XM + KW * KW;
+    const double *nx = d.inject ? dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K : nullptr;
+    d4 ax[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) ax[mt] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < KW / 8; ++t) {
+        const int kk = 8 * t + 2 * q;
+        d2 sv = *reinterpret_cast<const d2 *>(xall + (size_t)i * KW + kk);
+        for (int rk = 1; rk < d.nranks; ++rk)
+            sv += *reinterpret_cast<const d2 *>(xall + rk * stride + (size_t)i * KW + kk);
+        const d2 ev = row_normals(d, nx, live, SITE_X, 0, i, kk, iter);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const size_t o = (size_t)(16 * mt + c) * KW + kk;
+            const d2 a1 = *reinterpret_cast<const d2 *>(Tx + o);
+            const d2 a2 = *reinterpret_cast<const d2 *>(Ux + o);
+            ax[mt] = mfma16x16x4(a1.x, sv.x, ax[mt]);
+            ax[mt] = mfma16x16x4(a2.x, ev.x, ax[mt]);
+            ax[mt] = mfma16x16x4(a1.y, sv.y, ax[mt]);
+            ax[mt] = mfma16x16x4(a2.y, ev.y, ax[mt]);
+        }
+    }
+    if (!live) return;
+    double *Xr = X + (size_t)i * KW;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int k = 16 * mt + q + 4 * g;
+            Xr[k] = (k < d.K) ? ax[mt][g] : 0.0;
+        }
+}
+
+// ============================================================================
+// k_lambda: one workgroup per loading row j of shard m.               dc:140-145 (+150,156,169-171)
+//   Q_j = diag(Plam_j) + ps_j E_m (lower triangle read, as chol(...,'lower')),
+//   distributed as 8x8 register blocks over the nb = ceil(K/8) block rows:
+//     wave 0, threads 0..NB-1     diagonal blocks (J, J)
+//     wave 0, threads 32..32+NB-1 the right-hand side b = ps_j C_j as an extra
+//                                  block row: the forward solve L v = b rides
+//                                  along the factorisation (v_k = b_k / L_kk)
+//     waves 1.., threads 64..      off-diagonal blocks (I, J), I > J
+//   Right-looking: per pivot k the owners of block column k/8 scale column k into
+//   LDS, everyone with columns > k applies the rank-1 update from registers.
+//   Then Lambda_j = L' \ (v + z) (blocked back solve, z = normrnd dc:142),
+//   psi_j (dc:150), SS_j = yy_j - 2 x.C_j + x'E x, ps_j, omega_j (dc:169-171).
+//   Rows r >= K inside the last block are an identity pad.
+// ============================================================================
+constexpr int lambda_threads(int KW) { return 64 + ((KW / 8) * (KW / 8 - 1) / 2 + 63) / 64 * 64; }
+
+template <int KW>
+__global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
+    Dims d, const double *__restrict__ C, const double *__restrict__ E, const double *__restrict__ yy,
+    const double *__restrict__ tau_cur, const double *__restrict__ Plam, double *__restrict__ Lam,
+    double *__restrict__ psi, double *__restrict__ ps, double *__restrict__ omega, double *__restrict__ cpart,
+    DrawsDev dr, int64_t iter) {
+    constexpr int NB = KW / 8;
+    __shared__ __attribute__((aligned(16))) double col[KW + 8];   // pivot column; col[KW] = v_k
+    __shared__ __attribute__((aligned(16))) double sw[KW], sx[KW];
+    __shared__ double ikk[KW];
+    __shared__ double red[4];
+    const int j = blockIdx.x, m = blockIdx.y, mg = d.shard0 + m;
+    const int t = threadIdx.x, K = d.K;
+    const int nb = (K + 7) >> 3, nd = 8 * nb;
+    // role: 0 diagonal block, 1 right-hand side, 2 off-diagonal block, 3 idle
+    int role = 3, I = 0, J = 0;
+    if (t < 32) {
+        if (t < nb) { role = 0; I = J = t; }
+    } else if (t < 64) {
+        if (t - 32 < nb) { role = 1; J = t - 32; I = NB; }
+    } else {
+        int o = t - 64, jj = 0;
+        while (jj < NB - 1 && o >= NB - 1 - jj) { o -= NB - 1 - jj; ++jj; }
+        if (jj < NB - 1) {
+            J = jj;
+            I = jj + 1 + o;
+            if (I < nb) role = 2;
+        }
+    }
+    const double *Em = E + (size_t)m * KW * KW;
+    const size_t rowoff = ((size_t)m * d.PP + j) * KW;
+    const double psj = ps[(size_t)m * d.PP + j];
+    double a[8][8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int v = 0; v < 8; ++v) a[u][v] = 0.0;
+    if (role == 0 || role == 2) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                const int r = 8 * I + u, c = 8 * J + v;
+                double val;
+                if (r < K && c < K) {
+                    val = psj * Em[(size_t)r * KW + c];                  // ps_j * eta2 (dc:141)
+                    if (r == c) val = Plam[rowoff + r] + val;            // diag(Plam_j) + ...
+                } else {
+                    val = (r == c) ? 1.0 : 0.0;
+                }
+                a[u][v] = val;
+            }
+        if (role == 0 && I == 0) ikk[0] = rsqrt_f64(a[0][0]);
+    } else if (role == 1) {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            const int c = 8 * J + v;
+            a[0][v] = (c < K) ? psj * C[rowoff + c] : 0.0;                // blam (dc:141)
+        }
+    }
+    __syncthreads();
+    // ---- factorisation with fused forward solve (dc:142 chol, dc:143 Llam \ blam)
+    for (int Jk = 0; Jk < nb; ++Jk) {
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+            const int k = 8 * Jk + kk;
+            if (J == Jk && role != 3) {
+                const double ik = ikk[k];
+                if (role == 0) {
+                    a[kk][kk] *= ik;
+#pragma unroll
+                    for (int u = kk + 1; u < 8; ++u) {
+                        a[u][kk] *= ik;
+                        col[8 * J + u] = a[u][kk];
+                    }
+                } else if (role == 2) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        a[u][kk] *= ik;
+                        col[8 * I + u] = a[u][kk];
+                    }
+                } else {
+                    a[0][kk] *= ik;
+                    col[KW] = a[0][kk];
+                }
+            }
+            __syncthreads();
+            if (role != 3 && J >= Jk) {
+                const bool same = (J == Jk);
+                double lc[8];
+#pragma unroll
+                for (int v = 0; v < 8; v += 2) {
+                    const d2 x2 = *reinterpret_cast<const d2 *>(col + 8 * J + v);
+                    lc[v] = x2.x;
+                    lc[v + 1] = x2.y;
+                }
+                if (role == 0) {
+#pragma unroll
+                    for (int v = 0; v < 8; ++v)
+                        if (!same || v > kk) {
+#pragma unroll
+                            for (int u = v; u < 8; ++u) a[u][v] -= lc[u] * lc[v];
+                        }
+                } else if (role == 2) {
+                    double lr[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u += 2) {
+                        const d2 x2 = *reinterpret_cast<const d2 *>(col + 8 * I + u);
+                        lr[u] = x2.x;
+                        lr[u + 1] = x2.y;
+                    }
+#pragma unroll
+                    for (int v = 0; v < 8; ++v)
+                        if (!same || v > kk) {
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) a[u][v] -= lr[u] * lc[v];
+                        }
+                } else {
+                    const double lb = col[KW];
+#pragma unroll
+                    for (int v = 0; v < 8; ++v)
+                        if (!same || v > kk) a[0][v] -= lb * lc[v];
+                }
+            }
+            if (role == 0) {   // next pivot, from the owner's own registers
+                if (kk < 7) {
+                    if (J == Jk && k + 1 < nd) ikk[k + 1] = rsqrt_f64(a[kk + 1 < 8 ? kk + 1 : 7][kk + 1 < 8 ? kk + 1 : 7]);
+                } else if (J == Jk + 1) {
+                    ikk[k + 1] = rsqrt_f64(a[0][0]);
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // ---- w = v + z   (dc:142 normrnd; dc:143-144: Lambda_j = L' \ (v + z))
+    if (role == 1) {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            const int c = 8 * J + v;
+            double z = 0.0;
+            if (c < K) {
+                if (d.inject) {
+                    z = dr.NL[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + c];
+                } else {
+                    const Rng rng(d.seed);
+                    z = rng.normal(SITE_LAMBDA, mg, j, c, (uint32_t)iter);
+                }
+            }
+            sw[c] = a[0][v] + z;
+        }
+    }
+    __syncthreads();
+    // ---- blocked back solve L' x = w, block rows from the bottom
+    for (int Jb = nb - 1; Jb >= 0; --Jb) {
+        if (role == 0 && J == Jb) {
+            double wv[8];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) wv[v] = sw[8 * J + v];
+#pragma unroll
+            for (int v = 7; v >= 0; --v) {
+                const double xv = wv[v] * ikk[8 * J + v];
+                sx[8 * J + v] = xv;
+#pragma unroll
+                for (int u = 0; u < v; ++u) wv[u] -= a[v][u] * xv;
+            }
+        }
+        __syncthreads();
+        if (role == 2 && I == Jb) {
+            double xl[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) xl[u] = sx[8 * I + u];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                double acc = sw[8 * J + v];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc -= a[u][v] * xl[u];
+                sw[8 * J + v] = acc;
+            }
+        }
+        __syncthreads();
+    }
+    // ---- epilogue: Lambda_j, psi_j (dc:150), SS identity and ps_j (dc:169-171)
+    double contrib = 0.0;
+    if (t < KW) {
+        const int r = t;
+        const double xr = (r < K) ? sx[r] : 0.0;
+        const double cjr = C[rowoff + r];
+        double ex = 0.0;
+        for (int c = 0; c < K; ++c) ex += Em[(size_t)c * KW + r] * sx[c];   // (E x)_r
+        contrib = xr * (ex - 2.0 * cjr);
+        double psir = 0.0;
+        if (r < K) {
+            const double tr = tau_cur[(size_t)mg * KW + r];
+            const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xr * xr * tr));
+            double G;
+            if (d.inject) {
+                G = dr.Gpsi[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + r) * d.P + j];
+            } else {
+                const Rng rng(d.seed);
+                G = rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, mg, j, r, (uint32_t)iter);
+            }
+            psir = scale * G;
+            psi[rowoff + r] = psir;
+        }
+        Lam[rowoff + r] = xr;
+        cpart[rowoff + r] = psir * (xr * xr);          // mat = psijh .* Lambda.^2 (dc:156)
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) contrib += __shfl_xor(contrib, o, 64);
+    if ((t & 63) == 0) red[t >> 6] = contrib;
+    __syncthreads();
+    if (t == 0) {
+        double s = 0.0;
+        for (int w = 0; w < (KW + 63) / 64; ++w) s += red[w];
+        const double SS = yy[(size_t)m * d.PP + j] + s;
+        double G;
+        if (d.inject) {
+            G = dr.Gps[((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j];
+        } else {
+            const Rng rng(d.seed);
+            G = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg, j, 0, (uint32_t)iter);
+        }
+        const double psn = (1.0 / (d.bs + 0.5 * SS)) * G;     // dc:170
+        ps[(size_t)m * d.PP + j] = psn;
+        omega[(size_t)m * d.PP + j] = 1.0 / psn;              // dc:171 (Q1)
+    }
+}
+
+// ============================================================================
+// k_colsum: sloc[m][k] = sum_{j<P} cpart[m][j][k], fixed order          dc:156 sum(mat)
+// ============================================================================
+template <int KW>
+__global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict__ cpart, double *__restrict__ sloc) {
+    constexpr int NG = 256 / KW;
+    __shared__ double part[NG][KW];
+    const int m = blockIdx.x, k = threadIdx.x % KW, grp = threadIdx.x / KW;
+    double s = 0.0;
+    for (int j = grp; j < d.P; j += NG) s += cpart[((size_t)m * d.PP + j) * KW + k];
+    part[grp][k] = s;
+    __syncthreads();
+    if (threadIdx.x < KW) {
+        double tt = 0.0;
+#pragma unroll
+        for (int g2 = 0; g2 < NG; ++g2) tt += part[g2][threadIdx.x];
+        sloc[(size_t)m * KW + threadIdx.x] = tt;
+    }
+}
+
+// ============================================================================
+// k_delta: multiplicative-gamma-process chain for K in 33..128 (NV = KW/64
+// factors per lane: index l + 64 s).  Same algebra as the narrow kernel: every
+// shard's h >= 2 step reads shard 1's already-updated delta_h (quirk Q4), the
+// recomputed cumprod is the scalar factor F_h (dc:155-165); then Plam = psi o tau'
+// (dc:175-177) for local shards.  (K == 1, quirk Q5, is narrow-only.)
+// ============================================================================
+template <int NV>
+__device__ __forceinline__ void suffix_sum_nv(double (&v)[NV], int l) {
+    v[NV - 1] = wave_suffix_sum(v[NV - 1], l);
+    if (NV == 2) v[0] = wave_suffix_sum(v[0], l) + readlane_d(v[NV - 1], 0);
+}
+template <int NV>
+__device__ __forceinline__ void scan_prod_nv(double (&v)[NV], int l) {
+    v[0] = wave_scan_prod(v[0], l);
+    if (NV == 2) v[NV - 1] = wave_scan_prod(v[NV - 1], l) * readlane_d(v[0], 63);
+}
+template <int NV>
+__device__ void delta_chain_nv(const Dims &d, int l, const double (&T)[NV], const double (&G)[NV],
+                               const double (&idold)[NV], const double (&idref)[NV], double (&dnew)[NV]) {
+    double F = 1.0;
+#pragma unroll
+    for (int s = 0; s < NV; ++s) dnew[s] = 1.0;
+    for (int h = 0; h < d.K; ++h) {
+        const bool hi = (NV == 2) && h >= 64;
+        const int hl = h & 63;
+        const double Th = readlane_d(hi ? T[NV - 1] : T[0], hl), ih = readlane_d(hi ? idref[NV - 1] : idref[0], hl);
+        const double ioh = readlane_d(hi ? idold[NV - 1] : idold[0], hl), Gh = readlane_d(hi ? G[NV - 1] : G[0], hl);
+        const double bd = (h == 0 ? d.bd1 : d.bd2) + (0.5 * ih) * (F * Th);   // dc:157,161
+        const double dn = (1.0 / bd) * Gh;                                      // dc:158,163
+        if (l == hl) {
+            if (hi) dnew[NV - 1] = dn;
+            else dnew[0] = dn;
+        }
+        F = F * (dn * ioh);
+    }
+}
+
+template <int KW>
+__global__ __launch_bounds__(256) void k_delta(Dims d, const double *__restrict__ sall,
+                                               const double *__restrict__ delta_in, const double *__restrict__ tau_in,
+                                               double *__restrict__ delta_out, double *__restrict__ tau_out,
+                                               const double *__restrict__ psi, double *__restrict__ Plam, DrawsDev dr,
+                                               int64_t iter) {
+    constexpr int NV = KW / 64;
+    __shared__ double tnew[KW];
+    const int m = blockIdx.x;   // global shard
+    const int t = threadIdx.x;
+    if (t < 64) {
+        const int l = t;
+        double d0[NV], T0[NV], G0[NV], id0[NV], d0new[NV];
+#pragma unroll
+        for (int s = 0; s < NV; ++s) {
+            const int idx = l + 64 * s;
+            const bool act = idx < d.K;
+            d0[s] = act ? delta_in[idx] : 1.0;
+            T0[s] = act ? tau_in[idx] * sall[idx] : 0.0;
+            G0[s] = act ? delta_G(d, dr, iter, 0, idx) : 1.0;
+            id0[s] = 1.0 / d0[s];
+        }
+        suffix_sum_nv<NV>(T0, l);
+        delta_chain_nv<NV>(d, l, T0, G0, id0, id0, d0new);   // shard 1, its own pre-update delta_h
+        double dm[NV];
+#pragma unroll
+        for (int s = 0; s < NV; ++s) dm[s] = d0new[s];
+        if (m != 0) {
+            double Tm[NV], Gm[NV], idold[NV], idref[NV];
+#pragma unroll
+            for (int s = 0; s < NV; ++s) {
+                const int idx = l + 64 * s;
+                const bool act = idx < d.K;
+                const size_t o = (size_t)m * KW + idx;
+                const double dold = act ? delta_in[o] : 1.0;
+                Tm[s] = act ? tau_in[o] * sall[o] : 0.0;
+                Gm[s] = act ? delta_G(d, dr, iter, m, idx) : 1.0;
+                idold[s] = 1.0 / dold;
+                idref[s] = (idx == 0) ? idold[s] : 1.0 / d0new[s];   // delta(1,:,m) | delta(h) (Q4)
+            }
+            suffix_sum_nv<NV>(Tm, l);
+            delta_chain_nv<NV>(d, l, Tm, Gm, idold, idref, dm);
+        }
+        double tm[NV];
+#pragma unroll
+        for (int s = 0; s < NV; ++s) tm[s] = (l + 64 * s < d.K) ? dm[s] : 1.0;
+        scan_prod_nv<NV>(tm, l);                                     // tauh = cumprod(delta)
+#pragma unroll
+        for (int s = 0; s < NV; ++s) {
+            const int idx = l + 64 * s;
+            const bool act = idx < d.K;
+            const size_t o = (size_t)m * KW + idx;
+            delta_out[o] = act ? dm[s] : delta_in[o];
+            tau_out[o] = act ? tm[s] : tau_in[o];
+            tnew[idx] = tm[s];
+        }
+    }
+    __syncthreads();
+    const int ml = m - d.shard0;
+    if (ml < 0 || ml >= d.G) return;
+    const size_t base = (size_t)ml * d.PP * KW;
+    for (int e = t; e < d.P * KW; e += 256) {
+        const int k = e % KW;
+        if (k < d.K) Plam[base + e] = psi[base + e] * tnew[k];   // dc:176
+    }
+}
+
+// ============================================================================
+// launchers (kernels.hip dispatches here when d.kp != 32)
+// ============================================================================
+#define WIDE_DISPATCH(KWV, CALL)        \
+    do {                                \
+        if ((KWV) == 64) {              \
+            constexpr int KW = 64;      \
+            CALL;                       \
+        } else {                        \
+            constexpr int KW = 128;     \
+            CALL;                       \
+        }                               \
+    } while (0)
+
+void launch_prep(const Dims &d, const Bufs &b, hipStream_t s) {
+    WIDE_DISPATCH(d.kp, {
+        hipLaunchKernelGGL(k_gram<KW>, dim3((KW / 32) * (KW / 32), d.G), dim3(256), 0, s, d, b.Lam, b.omega, b.A);
+        hipLaunchKernelGGL(k_prep<KW>, dim3(d.G), dim3(256), 0, s, d, b.A, b.ZM);
+    });
+}
+void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_xchol<KW>, dim3(1), dim3(256), 0, s, d,
+                                           d.nranks > 1 ? b.xa_all : b.xa, b.XM));
+}
+void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_zdraw<KW>, dim3((d.NP / 64) * d.G), dim3(256), 0, s, d, b.W, b.ZM,
+                                           b.X, b.Z, b.Sp, dr, iter));
+}
+void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_xdraw<KW>, dim3(cdiv(d.n, 16)), dim3(64), 0, s, d, b.xall, b.XM, b.X,
+                                           dr, iter));
+}
+void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *tau_cur,
+                   hipStream_t s) {
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_lambda<KW>, dim3(d.P, d.G), dim3(lambda_threads(KW)), 0, s, d, b.C,
+                                           b.E, b.yy, tau_cur, b.Plam, b.Lam, b.psi, b.ps, b.omega, b.cpart, dr,
+                                           iter));
+}
+void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s) {
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_colsum<KW>, dim3(d.G), dim3(256), 0, s, d, b.cpart, b.sloc));
+}
+void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
+                  const double *tau_in, double *delta_out, double *tau_out, hipStream_t s) {
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_delta<KW>, dim3(d.g), dim3(256), 0, s, d, b.sall, delta_in, tau_in,
+                                           delta_out, tau_out, b.psi, b.Plam, dr, iter));
+}
+#undef WIDE_DISPATCH
+
+}  // namespace wide
+}  // namespace dcfm

@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "dcfm_internal.h"
+#include "philox.h"
 
 namespace dcfm {
 
@@ -38,6 +39,41 @@ __device__ __forceinline__ double rsqrt_f64(double x) {
         y = fma(0.5 * y, e, y);
     }
     return y;
+}
+
+// XCD-aware block remap (bijective): hardware deals consecutive block ids
+// round-robin over the 8 XCDs; give each XCD a contiguous range of work items
+// so that blocks sharing operands (one shard's tiles) share one L2.
+__device__ __forceinline__ int xcd_remap(int b, int total) {
+    const int xcd = b & 7, slot = b >> 3;
+    const int q = total >> 3, rem = total & 7;
+    return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + slot;
+}
+
+__device__ __forceinline__ double wave_scan_prod(double v, int l) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_up(v, o, 64);
+        if (l >= o) v *= u;
+    }
+    return v;
+}
+
+__device__ __forceinline__ double wave_suffix_sum(double v, int l) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_down(v, o, 64);
+        if (l + o < 64) v += u;
+    }
+    return v;
+}
+
+// standard gamma of the delta site, h = 0-based factor index (dc:158,163)
+__device__ inline double delta_G(const Dims &d, const DrawsDev &dr, int64_t iter, int mg, int h) {
+    if (d.inject) return dr.Gdelta[((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + h];
+    const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - h);
+    const Rng rng(d.seed);
+    return rng.gamma(shape, SITE_DELTA, mg, 0, h, (uint32_t)iter);
 }
 
 // eta = sqrt(rho) X + sqrt(1-rho) Z    (dc:81,133) — one definition for every use

@@ -70,7 +70,7 @@ def _create(dcfm, **kw):
 
 def test_create_validates_before_touching_a_device(dcfm):
     from dcfm_amd import _abi
-    assert _create(dcfm, K=33)[0] == _abi.DCFM_ERR_UNSUPPORTED
+    assert _create(dcfm, K=129)[0] == _abi.DCFM_ERR_UNSUPPORTED
     assert _create(dcfm, g=3, nranks=2)[0] == _abi.DCFM_ERR_UNSUPPORTED
     assert _create(dcfm, rho=1.5)[0] == _abi.DCFM_ERR_INVALID
     assert _create(dcfm, thin=0)[0] == _abi.DCFM_ERR_INVALID

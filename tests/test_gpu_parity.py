@@ -24,6 +24,16 @@ CASES = {
     "K32_max": (50, 128, 2, 32, 0, 2, 1),
     "thin_not_dividing": (30, 40, 4, 3, 1, 5, 2),           # quirk Q8
     "many_shards": (20, 96, 12, 3, 0, 3, 1),                # G not a multiple of 4
+    # wide-factor path (kernels_wide.hip): K > 32 is padded to KW = 64 or 128.
+    # n > K throughout: with n < K, E = eta'eta is rank deficient, Q_j's condition
+    # number reaches ~1e11 and any two implementations (even the two CPU oracle
+    # flavours) drift apart chaotically after one iteration — not a parity regime.
+    "K33_wide64": (40, 99, 3, 33, 0, 2, 1),
+    "K40_ragged": (45, 141, 3, 40, 1, 2, 1),                # n, P ragged; burnin
+    "K64_full64": (70, 128, 2, 64, 0, 2, 1),
+    "K100_c4_shape": (120, 200, 2, 100, 0, 2, 1),           # c4's truncation (BASELINE configs[3])
+    "K128_max": (150, 256, 2, 128, 0, 2, 1),
+    "many_shards_wide": (50, 480, 12, 40, 0, 2, 1),
 }
 
 
