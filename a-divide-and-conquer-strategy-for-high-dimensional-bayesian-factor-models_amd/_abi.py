@@ -25,16 +25,17 @@ DCFM_FLAG_INJECT_DRAWS = 0x1
 KERNEL_IDS = {
     "k_prep": 0, "k_wpass": 1, "k_zdraw": 2, "k_xred": 3, "k_xdraw": 4, "k_cpass": 5,
     "k_lambda": 6, "k_colsum": 7, "k_delta": 8, "k_save": 9, "k_assemble": 10, "rccl": 11,
-    "k_xchol": 12,
+    "k_xchol": 12, "k_draws": 13,
 }
-K_COUNT = 13
+K_COUNT = 14
 
 # every symbol include/dcfm.h declares
 EXPORTS = (
     "dcfm_create", "dcfm_destroy", "dcfm_last_error", "dcfm_abi_version",
     "dcfm_comm_unique_id", "dcfm_comm_init", "dcfm_set_data", "dcfm_set_state",
     "dcfm_set_draws", "dcfm_run", "dcfm_synchronize", "dcfm_get_state", "dcfm_get_sigma",
-    "dcfm_saved_samples", "dcfm_set_profiling", "dcfm_get_kernel_stats", "dcfm_kernel_name",
+    "dcfm_saved_samples", "dcfm_set_profiling", "dcfm_set_profiling_mask", "dcfm_get_kernel_stats",
+    "dcfm_kernel_name",
     "dcfm_rng_fill",
 )
 
@@ -100,6 +101,7 @@ def load_library(path: Path | None = None):
         "dcfm_get_sigma": (C.c_int, [vp, _DP]),
         "dcfm_saved_samples": (C.c_int64, [vp]),
         "dcfm_set_profiling": (C.c_int, [vp, C.c_int]),
+        "dcfm_set_profiling_mask": (C.c_int, [vp, C.c_uint32]),
         "dcfm_get_kernel_stats": (C.c_int, [vp, _DP, C.POINTER(C.c_int64)]),
         "dcfm_kernel_name": (C.c_char_p, [C.c_int]),
         "dcfm_rng_fill": (C.c_int, [C.c_int, C.c_uint64, C.c_int, C.c_double, C.c_int32, C.c_int32,

@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -33,7 +34,9 @@ struct dcfm_handle {
     hipStream_t sasm = nullptr;       // covariance assembly, overlapping later iterations
     ncclComm_t comm = nullptr, comm_side = nullptr, comm_asm = nullptr;
     bool comm_ok = false;
-    hipEvent_t e_lam = nullptr, e_prep = nullptr, e_batch = nullptr, e_free[2] = {nullptr, nullptr};
+    hipEvent_t e_lam = nullptr, e_prep = nullptr, e_xchol = nullptr, e_batch = nullptr,
+               e_free[2] = {nullptr, nullptr};
+    bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
     bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
     int lb = 0;                   // Lb buffer being filled
@@ -44,7 +47,13 @@ struct dcfm_handle {
     std::string err;
     std::vector<void *> allocs;
     double *draws_mem = nullptr;
+    // on-device Philox draws (no INJECT): three iteration slots, generated one
+    // iteration ahead on the side stream; a slot is valid for the iteration it was
+    // generated for whatever the state (the stream is counter-based)
+    DrawsDev gen[3] = {};
+    int64_t gen_iter[3] = {-1, -1, -1};
     bool prof = false;
+    uint32_t prof_mask = 0;       // kernel ids (bit DCFM_K_*) timed with events
     std::vector<ProfRec> recs;
     std::vector<hipEvent_t> evpool;
     double kms[DCFM_K_COUNT] = {};
@@ -113,7 +122,7 @@ struct KTimer {
     hipStream_t s;
     hipEvent_t a = nullptr;
     KTimer(dcfm_handle *h_, int k, hipStream_t s_) : h(h_), kid(k), s(s_) {
-        if (h->prof) {
+        if (h->prof && (h->prof_mask >> k & 1u)) {
             a = get_event(h);
             if (a) (void)hipEventRecord(a, s);
         }
@@ -160,7 +169,8 @@ const char *dcfm_last_error(const dcfm_handle *h) { return h ? h->err.c_str() : 
 const char *dcfm_kernel_name(int id) {
     static const char *names[DCFM_K_COUNT] = {"k_prep",  "k_wpass", "k_zdraw",  "k_xred",
                                               "k_xdraw", "k_cpass", "k_lambda", "k_colsum",
-                                              "k_delta", "k_save",  "k_assemble", "rccl", "k_xchol"};
+                                              "k_delta", "k_save",  "k_assemble", "rccl", "k_xchol",
+                                              "k_draws"};
     return (id >= 0 && id < DCFM_K_COUNT) ? names[id] : "?";
 }
 
@@ -190,10 +200,18 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     h->cfg.nranks = nranks;
     HIPC(h, hipSetDevice(c.device));
     HIPC(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-    HIPC(h, hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-    HIPC(h, hipStreamCreateWithFlags(&h->sasm, hipStreamNonBlocking));
+    {   // DCFM_SERIALIZE=1: one stream for everything (isolated per-kernel timings)
+        const char *ser = std::getenv("DCFM_SERIALIZE");
+        if (ser && ser[0] == '1') {
+            h->side = h->sasm = h->stream;
+        } else {
+            HIPC(h, hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+            HIPC(h, hipStreamCreateWithFlags(&h->sasm, hipStreamNonBlocking));
+        }
+    }
     HIPC(h, hipEventCreateWithFlags(&h->e_lam, hipEventDisableTiming));
     HIPC(h, hipEventCreateWithFlags(&h->e_prep, hipEventDisableTiming));
+    HIPC(h, hipEventCreateWithFlags(&h->e_xchol, hipEventDisableTiming));
     HIPC(h, hipEventCreateWithFlags(&h->e_batch, hipEventDisableTiming));
     HIPC(h, hipEventCreateWithFlags(&h->e_free[0], hipEventDisableTiming));
     HIPC(h, hipEventCreateWithFlags(&h->e_free[1], hipEventDisableTiming));
@@ -248,6 +266,23 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     ALLOC(b.wsum[0], p);
     ALLOC(b.wsum[1], p);
     ALLOC(b.Sigma, p * p);
+    if (!d.inject) {
+        const size_t K = c.K, n = c.n, P = c.P;
+        const size_t nz = K * n * g, nx = K * n, nl = K * P * g, gpsi = P * K * g, gdel = K * g, gps = P * g;
+        double *gm = nullptr;
+        ALLOC(gm, 3 * (nz + nx + nl + gpsi + gdel + gps));
+        for (int sl = 0; sl < 3; ++sl) {
+            DrawsDev &G = h->gen[sl];
+            G.NZ = gm; gm += nz;
+            G.NX = gm; gm += nx;
+            G.NL = gm; gm += nl;
+            G.Gpsi = gm; gm += gpsi;
+            G.Gdelta = gm; gm += gdel;
+            G.Gps = gm; gm += gps;
+            G.first_iter = -1;
+            G.n_iter = 1;
+        }
+    }
 #undef ALLOC
     // lower-triangle assembly tiles, dealt round-robin over ranks
     {
@@ -280,15 +315,15 @@ void dcfm_destroy(dcfm_handle *h) {
     if (h->stream) sync_all(h);
     for (auto &r : h->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : h->evpool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {h->e_lam, h->e_prep, h->e_batch, h->e_free[0], h->e_free[1]})
+    for (hipEvent_t e : {h->e_lam, h->e_prep, h->e_xchol, h->e_batch, h->e_free[0], h->e_free[1]})
         if (e) (void)hipEventDestroy(e);
     if (h->comm_asm) ncclCommDestroy(h->comm_asm);
     if (h->comm_side) ncclCommDestroy(h->comm_side);
     if (h->comm) ncclCommDestroy(h->comm);
     for (void *q : h->allocs) (void)hipFree(q);
     if (h->draws_mem) (void)hipFree(h->draws_mem);
-    if (h->sasm) (void)hipStreamDestroy(h->sasm);
-    if (h->side) (void)hipStreamDestroy(h->side);
+    if (h->sasm && h->sasm != h->stream) (void)hipStreamDestroy(h->sasm);
+    if (h->side && h->side != h->stream) (void)hipStreamDestroy(h->side);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -427,6 +462,7 @@ int dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s) {
     h->cur = 0;
     k_to_dev(d, s->delta, v);   if ((rc = up(h, h->b.delta, v))) return rc;
     k_to_dev(d, s->tauh, v);    if ((rc = up(h, h->b.tau, v))) return rc;
+    h->plam_valid = true;
     h->have_state = true;
     return DCFM_OK;
 }
@@ -442,7 +478,22 @@ int dcfm_get_state(dcfm_handle *h, dcfm_state_view *o) {
     const size_t npk = (size_t)d.G * d.PP * KP, nnk = (size_t)d.G * d.NP * KP;
     if (o->Lambda) { if ((rc = down(h, v, h->b.Lam, npk))) return rc; pk_from_dev(d, v, o->Lambda); }
     if (o->psi) { if ((rc = down(h, v, h->b.psi, npk))) return rc; pk_from_dev(d, v, o->psi); }
-    if (o->Plam) { if ((rc = down(h, v, h->b.Plam, npk))) return rc; pk_from_dev(d, v, o->Plam); }
+    if (o->Plam) {
+        if (h->plam_valid) {
+            if ((rc = down(h, v, h->b.Plam, npk))) return rc;
+        } else {   // Plam = psi o tau' (dc:176) of the last iteration, formed as k_lambda forms it
+            std::vector<double> tau;
+            if ((rc = down(h, v, h->b.psi, npk))) return rc;
+            if ((rc = down(h, tau, h->b.tau + h->cur * (size_t)d.g * KP, (size_t)d.g * KP))) return rc;
+            for (int m = 0; m < d.G; ++m)
+                for (int j = 0; j < d.P; ++j)
+                    for (int k = 0; k < d.K; ++k) {
+                        double &x = v[((size_t)m * d.PP + j) * KP + k];
+                        x = x * tau[(size_t)(d.shard0 + m) * KP + k];
+                    }
+        }
+        pk_from_dev(d, v, o->Plam);
+    }
     if (o->ps) { if ((rc = down(h, v, h->b.ps, (size_t)d.G * d.PP))) return rc; p_from_dev(d, v, o->ps); }
     if (o->omega) { if ((rc = down(h, v, h->b.omega, (size_t)d.G * d.PP))) return rc; p_from_dev(d, v, o->omega); }
     if (o->X) { if ((rc = down(h, v, h->b.X, (size_t)d.NP * KP))) return rc; nk_from_dev(d, v, 1, o->X); }
@@ -480,6 +531,14 @@ int dcfm_set_draws(dcfm_handle *h, const dcfm_draws_view *dv, int64_t first_iter
     const double *srcs[6] = {dv->NZ, dv->NX, dv->NL, dv->Gpsi, dv->Gdelta, dv->Gps};
     const size_t cnt[6] = {nNZ, nNX, nNL, nPsi, nDel, nPs};
     const double **dsts[6] = {&h->dr.NZ, &h->dr.NX, &h->dr.NL, &h->dr.Gpsi, &h->dr.Gdelta, &h->dr.Gps};
+    // Gpsi: MATLAB P x K x g x T -> device [T][g][P][K] (the loading-row kernels read a row's K gammas)
+    std::vector<double> gpsi(nPsi);
+    for (size_t t = 0; t < T; ++t)
+        for (int m = 0; m < d.g; ++m)
+            for (int k = 0; k < d.K; ++k)
+                for (int j = 0; j < d.P; ++j)
+                    gpsi[((t * d.g + m) * d.P + j) * d.K + k] = dv->Gpsi[j + (size_t)d.P * (k + (size_t)d.K * (m + (size_t)d.g * t))];
+    srcs[3] = gpsi.data();
     for (int k = 0; k < 6; ++k) {
         HIPC(h, hipMemcpy(p, srcs[k], cnt[k] * sizeof(double), hipMemcpyHostToDevice));
         *dsts[k] = p;
@@ -541,30 +600,51 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     hipStream_t s = h->stream, ss = h->side;
     const size_t KP = d.kp;
     const size_t nkg = (size_t)d.g * KP;
+    // draws of iteration `it`: the injected buffers, or generated slot it % 3
+    auto ensure_draws = [&](int64_t it) {
+        if (d.inject) return;
+        const int sl = (int)(it % 3);
+        if (h->gen_iter[sl] == it) return;
+        h->gen[sl].first_iter = it;
+        KTimer t(h, DCFM_K_DRAWS, ss);
+        launch_draws(d, h->gen[sl], it, ss);
+        h->gen_iter[sl] = it;
+    };
+    auto draws_of = [&](int64_t it) -> const DrawsDev & { return d.inject ? h->dr : h->gen[it % 3]; };
     HIPC(h, hipEventRecord(h->e_lam, s));      // Lambda/omega of the previous iteration are final
+    HIPC(h, hipStreamWaitEvent(ss, h->e_lam, 0));
+    ensure_draws(first_iter);
     for (int64_t it = first_iter; it < first_iter + n_iter; ++it) {
+        const DrawsDev &dr = draws_of(it);
         // side stream: A_m, R_m, Rx from this iteration's incoming Lambda, omega (dc:98-100,112-118)
         HIPC(h, hipStreamWaitEvent(ss, h->e_lam, 0));
         { KTimer t(h, DCFM_K_PREP, ss); launch_prep(d, b, ss); }
+        HIPC(h, hipEventRecord(h->e_prep, ss));
         { KTimer t(h, DCFM_K_XCHOL, ss); launch_asum(d, b, ss); }
         if (d.nranks > 1) {
             KTimer t(h, DCFM_K_COMM, ss);
             NCCLC(h, ncclAllGather(b.xa, b.xa_all, (size_t)KP * KP, ncclDouble, h->comm_side, ss));
         }
         { KTimer t(h, DCFM_K_XCHOL, ss); launch_xchol(d, b, ss); }
-        HIPC(h, hipEventRecord(h->e_prep, ss));
+        HIPC(h, hipEventRecord(h->e_xchol, ss));
+        ensure_draws(it + 1);                      // next iteration's variates, overlapping this one
         // main stream
         { KTimer t(h, DCFM_K_WPASS, s);  launch_wpass(d, b, s); }
         HIPC(h, hipStreamWaitEvent(s, h->e_prep, 0));
-        { KTimer t(h, DCFM_K_ZDRAW, s);  launch_zdraw(d, b, h->dr, it, s); }
+        { KTimer t(h, DCFM_K_ZDRAW, s);  launch_zdraw(d, b, dr, it, s); }
         { KTimer t(h, DCFM_K_XRED, s);   launch_xred(d, b, s); }
         if (d.nranks > 1) {
             KTimer t(h, DCFM_K_COMM, s);
             NCCLC(h, ncclAllGather(b.xin, b.xall, (size_t)d.NP * KP, ncclDouble, h->comm, s));
         }
-        { KTimer t(h, DCFM_K_XDRAW, s);  launch_xdraw(d, b, h->dr, it, s); }
+        HIPC(h, hipStreamWaitEvent(s, h->e_xchol, 0));
+        { KTimer t(h, DCFM_K_XDRAW, s);  launch_xdraw(d, b, dr, it, s); }
         { KTimer t(h, DCFM_K_CPASS, s);  launch_cpass(d, b, s); }
-        { KTimer t(h, DCFM_K_LAMBDA, s); launch_lambda(d, b, h->dr, it, b.tau + h->cur * nkg, s); }
+        {
+            KTimer t(h, DCFM_K_LAMBDA, s);
+            launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s);
+        }
+        h->plam_valid = false;
         HIPC(h, hipEventRecord(h->e_lam, s));
         { KTimer t(h, DCFM_K_COLSUM, s); launch_colsum(d, b, s); }
         if (d.nranks > 1) {
@@ -573,7 +653,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         }
         {
             KTimer t(h, DCFM_K_DELTA, s);
-            launch_delta(d, b, h->dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+            launch_delta(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
                          b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);
         }
         h->cur ^= 1;
@@ -640,8 +720,15 @@ int dcfm_get_sigma(dcfm_handle *h, double *out) {
 }
 
 int dcfm_set_profiling(dcfm_handle *h, int enable) {
+    return dcfm_set_profiling_mask(h, enable ? 0xFFFFFFFFu : 0u);
+}
+
+int dcfm_set_profiling_mask(dcfm_handle *h, uint32_t mask) {
     if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
-    h->prof = enable != 0;
+    collect_prof(h);
+    h->prof_mask = mask;
+    const bool enable = mask != 0;
+    h->prof = enable;
     if (enable) {
         std::fill(h->kms, h->kms + DCFM_K_COUNT, 0.0);
         std::fill(h->kcnt, h->kcnt + DCFM_K_COUNT, 0);

@@ -6,7 +6,8 @@
 //   yy     [G][PP]       sum_i Y_ij^2 (set_data)                -> residual SS identity
 //   Lam    [G][PP][KW]   loadings, k padded to KW with zeros
 //   omega  [G][PP]       diag(Omega);   ps [G][PP]
-//   psi    [G][PP][KW];  Plam [G][PP][KW]
+//   psi    [G][PP][KW];  Plam [G][PP][KW] (the caller's Plam; valid until the first
+//                        iteration, after which Plam = psi o tau is formed on the fly)
 //   X      [NP][KW]      replicated;    Z [G][NP][KW]
 //   delta, tau [2][g][KW] replicated on every rank, double-buffered per iteration
 //   W      [G][NP][KW]   W_m = Y_m (omega o Lambda_m)                    (k_wpass)
@@ -16,7 +17,7 @@
 //   xin    [NP][KW]      local sum over shards of Sp;  xall [nranks][NP][KW] all-gathered (== xin if 1 rank)
 //   xa, xa_all [nranks][KW][KW]  per-rank sum of A_m (gathered);  XM [2][KW][KW] X-draw operators {Tx, Ux} (k_xchol)
 //   C      [G][PP][KW]   C_m = Y_m' eta_m  (k_cpass);  E [G][KW][KW] = eta_m' eta_m
-//   cpart  [G][PP/8][KW] (KW = 32) or [G][PP][KW] (wide) per-8-row partial column sums of psi o Lambda^2 (k_lambda)
+//   cpart  [G][PP][KW]   psi o Lambda^2 per loading row (k_lambda), summed over rows by k_colsum
 //   sloc   [G][KW], sall [g][KW]  column sums (all-gathered)
 //   Lb     [2][p][LDB]   saved Lambda rows of an assembly batch (double-buffered), sample s at cols s*K..
 //   wsum   [2][p]        sum of saved omega of the batch
@@ -69,7 +70,7 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
-                   const double *tau_cur, hipStream_t s);
+                   const double *tau_cur, const double *plam_src, hipStream_t s);
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                   const double *delta_in, const double *tau_in, double *delta_out,
@@ -79,6 +80,7 @@ void launch_assemble(const Dims &d, const Bufs &b, const double *Lb, const doubl
                      double inv_eff, hipStream_t s);
 void launch_mirror(double *S, int p, hipStream_t s);
 void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s);
+void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,
                      int64_t count, double *out, hipStream_t s);
 
@@ -89,8 +91,7 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *tau_cur,
-                   hipStream_t s);
-void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s);
+                   const double *plam_src, hipStream_t s);
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
                   const double *tau_in, double *delta_out, double *tau_out, hipStream_t s);
 }  // namespace wide

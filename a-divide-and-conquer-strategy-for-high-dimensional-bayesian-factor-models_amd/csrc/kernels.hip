@@ -17,7 +17,9 @@
 //              SS_j via identity, ps_j, omega_j; column sums of psi o L^2  dc:156,169-171
 //   k_colsum   per-shard column sums                                       dc:156
 //   [RCCL all-gather across ranks]
-//   k_delta    MGP chain (quirks Q4/Q5) for all shards, Plam refresh       dc:155-165,175-177
+//   k_delta    MGP chain (quirks Q4/Q5) for all shards                     dc:155-165
+//   (Plam = psi o tau' of dc:175-177 is formed where it is read: in the next
+//    k_lambda, from the psi and tau arrays — the same single product)
 //   saved iterations: k_save; per batch on the assembly stream (overlapping
 //   the following iterations): [RCCL all-gather], k_assemble            dc:180-195
 //
@@ -31,6 +33,18 @@
 #include <algorithm>
 
 namespace dcfm {
+
+#ifdef DCFM_PHASE_TIMING
+__device__ unsigned long long g_phase[32];
+}  // namespace dcfm
+// development build only: read and clear the per-phase shader-clock sums
+extern "C" int dcfm_debug_phases(unsigned long long out[32]) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dcfm::g_phase), 32 * sizeof(unsigned long long)) != hipSuccess) return 1;
+    unsigned long long z[32] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(dcfm::g_phase), z, sizeof z) == hipSuccess ? 0 : 1;
+}
+namespace dcfm {
+#endif
 
 // device helpers (MFMA, lane broadcast, rsqrt, register Cholesky): linalg.h
 
@@ -245,24 +259,14 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
             wv[t] = *reinterpret_cast<const d2 *>(Wi + 8 * t);
             xv[t] = *reinterpret_cast<const d2 *>(Xi + 8 * t);
         }
-        // eps[i][kk], kk = 8t + 2q + e   (dc:104 normrnd, pair index 4t + q)
-        if (d.inject) {
+        // eps[i][kk], kk = 8t + 2q + e   (dc:104 normrnd; draw buffer, k_draws or injected)
+        {
             const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const int kk = 8 * t + 2 * q;
                 ev[t].x = (live && kk < d.K) ? nz[kk] : 0.0;
                 ev[t].y = (live && kk + 1 < d.K) ? nz[kk + 1] : 0.0;
-            }
-        } else {
-            const Rng rng(d.seed);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int kk = 8 * t + 2 * q;
-                double n0 = 0.0, n1 = 0.0;
-                if (live && kk < d.K) rng.normal2(SITE_Z, mg, i, kk >> 1, (uint32_t)iter, n0, n1);
-                ev[t].x = n0;
-                ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
             }
         }
         d4 az[2], as[2];
@@ -402,23 +406,13 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
         for (int rk = 1; rk < d.nranks; ++rk)
             sv[t] += *reinterpret_cast<const d2 *>(xall + rk * stride + (size_t)i * KP + 8 * t + 2 * q);
     }
-    if (d.inject) {
+    {   // eps of dc:126 (draw buffer)
         const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int kk = 8 * t + 2 * q;
             ev[t].x = (live && kk < d.K) ? nx[kk] : 0.0;
             ev[t].y = (live && kk + 1 < d.K) ? nx[kk + 1] : 0.0;
-        }
-    } else {
-        const Rng rng(d.seed);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int kk = 8 * t + 2 * q;
-            double n0 = 0.0, n1 = 0.0;
-            if (live && kk < d.K) rng.normal2(SITE_X, 0, i, kk >> 1, (uint32_t)iter, n0, n1);
-            ev[t].x = n0;
-            ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
         }
     }
     d4 ax[2];
@@ -554,64 +548,77 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
 // ============================================================================
 // k_lambda: loading rows.  A half-wave (32 lanes) owns one row j; lane r holds
 // row r of Q_j = diag(Plam_j) + ps_j E_m in registers.        dc:140-145 (+150,156,169-171)
+//   Plam_j = psi_j o tau' (dc:176, previous iteration's psi and tau) unless plam_src
+//   is given (the first iteration after dcfm_set_state reads the caller's Plam).
 //   L = chol(Q,'lower'), v = L \ (ps_j C_j)   (chol_rows_fwd)
 //   Lambda_j = L' \ (v + z)                    (= ylam + mlam)
 //   psi_j  = Gpsi * 1/(df/2 + 0.5 lambda^2 tau)               (dc:150, tau of the previous it.)
 //   SS_j   = yy_j - 2 lambda.C_j + lambda' E lambda  ->  ps_j = Gps * 1/(bs + 0.5 SS_j), w = 1/ps
-// 8 rows per 256-thread block; per-block column sums of psi o lambda^2 -> cpart.
+// One independent 64-thread block (2 rows) per launch slot: no block barrier, so
+// waves drift apart and one wave's loads overlap another's factorisation; E_m
+// rows come from L2 (no LDS staging).  Every global load of the row is issued up
+// front.  psi o lambda^2 of the row -> cpart[m][j][:] (k_colsum sums the rows).
 // ============================================================================
-__global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict__ C,
+__global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict__ C,
                                                 const double *__restrict__ E,
                                                 const double *__restrict__ yy,
                                                 const double *__restrict__ tau_cur,
                                                 double *__restrict__ Lam, double *__restrict__ psi,
-                                                double *__restrict__ Plam, double *__restrict__ ps,
+                                                const double *__restrict__ plam_src, double *__restrict__ ps,
                                                 double *__restrict__ omega,
                                                 double *__restrict__ cpart, DrawsDev dr,
                                                 int64_t iter) {
-    __shared__ __attribute__((aligned(16))) double LP[8][P2STRIDE];
-    __shared__ double Es[KP][KP + 1];  // E_m, shared by the block's 8 rows (same shard)
-    __shared__ double csum[8][KP];
+    __shared__ __attribute__((aligned(16))) double LP[2][P2STRIDE];
     const int m = blockIdx.y;
     const int mg = d.shard0 + m;
     const int lane = threadIdx.x & 63;
-    const int hw = threadIdx.x >> 5;          // half-wave id 0..7
+    const int hw = threadIdx.x >> 5;          // half-wave id 0..1
     const bool upper = (lane >= 32);
     const int r = lane & 31;                  // matrix row
-    const int j = blockIdx.x * 8 + hw;
+    const int j = blockIdx.x * 2 + hw;
     const bool valid = j < d.P;
     const bool real = r < d.K;
     const size_t rowoff = ((size_t)m * d.PP + (valid ? j : 0)) * KP;
-    {
-        const double *Em = E + (size_t)m * KP * KP;
-        for (int e = threadIdx.x; e < KP * KP; e += 256) Es[e / KP][e % KP] = Em[e];
-    }
-    __syncthreads();
-    // --- build Q row r and rhs
+    // every global load of the row is issued up front (one latency, overlapping the
+    // E staging and the factorisation) — each later dependent load would cost a
+    // full round trip on a latency-bound kernel
+    const bool rv = real && valid;
+    const int64_t ti = iter - dr.first_iter;
+    const int jj = valid ? j : 0;
     const double psj = valid ? ps[(size_t)m * d.PP + j] : 0.0;
+    const double tr = rv ? tau_cur[(size_t)mg * KP + r] : 0.0;
+    const double psi_old = (rv && !plam_src) ? psi[rowoff + r] : 0.0;
+    const double plam_in = (rv && plam_src) ? plam_src[rowoff + r] : 0.0;
+    const double cjr = valid ? C[rowoff + r] : 0.0;
+    const double z = rv ? dr.NL[(((size_t)ti * d.g + mg) * d.P + jj) * d.K + r] : 0.0;         // dc:142
+    const double Gpsi = rv ? dr.Gpsi[(((size_t)ti * d.g + mg) * d.P + jj) * d.K + r] : 0.0;    // dc:150
+    const double Gps = (valid && r == 0) ? dr.Gps[((size_t)ti * d.g + mg) * d.P + jj] : 0.0;    // dc:170
+    const double yyj = (valid && r == 0) ? yy[(size_t)m * d.PP + jj] : 0.0;
+    const double *Er = E + ((size_t)m * KP + r) * KP;     // row r of E_m (L2-resident)
     double q[KP];
 #pragma unroll
-    for (int c = 0; c < KP; ++c) q[c] = psj * Es[r][c];
-    const double plam = (valid && real) ? Plam[rowoff + r] : 1.0;
+    for (int c = 0; c < KP; c += 2) {
+        const d2 e2 = *reinterpret_cast<const d2 *>(Er + c);
+        q[c] = e2.x;
+        q[c + 1] = e2.y;
+    }
+    PHASE_T0();
+    // --- build Q row r and rhs
+#pragma unroll
+    for (int c = 0; c < KP; ++c) q[c] = psj * q[c];
+    const double plam = rv ? (plam_src ? plam_in : psi_old * tr) : 1.0;   // Plam = psi o tau' (dc:176)
 #pragma unroll
     for (int c = 0; c < KP; ++c)
         if (c == r) q[c] = (real && valid) ? plam + q[c] : 1.0;
-    const double cjr = valid ? C[rowoff + r] : 0.0;
 
     double *Lp = LP[hw];
     double vr = 0.0;
+    PHASE(0);
     chol2_rows<true>(q, Lp, r, upper, psj * cjr, vr);
+    PHASE(1);
     // --- + z  (dc:142 normrnd(0,1,K,1))
-    double z = 0.0;
-    if (real && valid) {
-        if (d.inject) {
-            z = dr.NL[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + r];
-        } else {
-            const Rng rng(d.seed);
-            z = rng.normal(SITE_LAMBDA, mg, j, r, (uint32_t)iter);
-        }
-    }
     double wr = vr + z;
+    PHASE(2);
     // --- back solve L' x = w, two rows per step;  L[c][r] = Lp[p2idx(c, r)]
     double xr = 0.0;
     const int br = pb2(r >> 1) - 2 * (r & ~1) + (r & 1);     // L[c][r] at br + 2c
@@ -626,60 +633,71 @@ __global__ __launch_bounds__(256) void k_lambda(Dims d, const double *__restrict
         if (r < c - 1) wr -= Lp[br + 2 * c] * xc + Lp[br + 2 * (c - 1)] * xc1;
     }
     if (!real) xr = 0.0;
+    PHASE(3);
 
     // --- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr; x broadcast through the scratch slots
     Lp[PACK2 + KP + r] = xr;
     double ex = 0.0;
 #pragma unroll
-    for (int c = 0; c < KP; ++c) ex += Es[c][r] * Lp[PACK2 + KP + c];   // (E x)_r, E symmetric
+    for (int c = 0; c < KP; c += 2) {                      // (E x)_r from row r (E symmetric)
+        const d2 e2 = *reinterpret_cast<const d2 *>(Er + c);
+        ex += e2.x * Lp[PACK2 + KP + c];
+        ex += e2.y * Lp[PACK2 + KP + c + 1];
+    }
     double contrib = xr * (ex - 2.0 * cjr);
 #pragma unroll
     for (int o = 16; o >= 1; o >>= 1) contrib += __shfl_xor(contrib, o, 32);
 
+    PHASE(4);
     // --- psi (dc:150), uses tau of the previous iteration (Q11)
     double psir = 0.0;
-    if (real && valid) {
-        const double tr = tau_cur[(size_t)mg * KP + r];
+    if (rv) {
         const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xr * xr * tr));
-        double G;
-        if (d.inject) {
-            G = dr.Gpsi[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + r) * d.P + j];
-        } else {
-            const Rng rng(d.seed);
-            G = rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, mg, j, r, (uint32_t)iter);
-        }
-        psir = scale * G;
+        psir = scale * Gpsi;
     }
-    csum[hw][r] = psir * (xr * xr);       // mat = psijh .* Lambda.^2 (dc:156)
+    PHASE(5);
 
     if (valid) {
         Lam[rowoff + r] = xr;
+        cpart[rowoff + r] = psir * (xr * xr);       // mat = psijh .* Lambda.^2 (dc:156)
         if (real) psi[rowoff + r] = psir;
         if (r == 0) {
-            const double SS = yy[(size_t)m * d.PP + j] + contrib;
-            double G;
-            if (d.inject) {
-                G = dr.Gps[((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j];
-            } else {
-                const Rng rng(d.seed);
-                G = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg, j, 0, (uint32_t)iter);
-            }
-            const double psn = (1.0 / (d.bs + 0.5 * SS)) * G;   // dc:170
+            const double SS = yyj + contrib;
+            const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;   // dc:170
             ps[(size_t)m * d.PP + j] = psn;
             omega[(size_t)m * d.PP + j] = 1.0 / psn;            // dc:171 (Q1)
         }
     }
-    __syncthreads();
-    if (threadIdx.x < KP) {
-        double s = 0.0;
-#pragma unroll
-        for (int h = 0; h < 8; ++h) s += csum[h][threadIdx.x];
-        cpart[((size_t)m * (d.PP >> 3) + blockIdx.x) * KP + threadIdx.x] = s;
-    }
+    PHASE(6);
+    PHASE_END();
 }
 
 // ============================================================================
-// k_colsum: sloc[m][k] = sum_b cpart[m][b][k]                               dc:156 sum(mat)
+// k_colsum: sloc[m][k] = sum_{j<P} cpart[m][j][k], fixed order            dc:156 sum(mat)
+// block = (shard m, 32 columns); 8 row groups x 4 independent accumulators each.
+// ============================================================================
+template <int KW>
+__global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict__ cpart, double *__restrict__ sloc) {
+    __shared__ double part[8][32];
+    const int m = blockIdx.x, k = 32 * blockIdx.y + (threadIdx.x & 31), grp = threadIdx.x >> 5;
+    const double *cp = cpart + (size_t)m * d.PP * KW + k;
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
+    int j = grp;
+    for (; j + 24 < d.P; j += 32) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s4[u] += cp[(size_t)(j + 8 * u) * KW];
+    }
+    for (; j < d.P; j += 8) s4[0] += cp[(size_t)j * KW];
+    part[grp][threadIdx.x & 31] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        double tt = 0.0;
+#pragma unroll
+        for (int g2 = 0; g2 < 8; ++g2) tt += part[g2][threadIdx.x];
+        sloc[(size_t)m * KW + k] = tt;
+    }
+}
+
 // ============================================================================
 __global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict__ cpart,
                                                 double *__restrict__ sloc) {
@@ -708,7 +726,7 @@ __global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict
 // tau, the reference's recomputed cumprod gives dot_h = F_h T_h where
 // F_h = prod_{h'<h} delta_new(h')/delta_old(h')  (exact; rounding-level only).
 // grid = all g shards (delta/tau replicated on every rank); local blocks also
-// refresh Plam = psi o tau'.
+// (formerly) refresh Plam — now formed lazily in k_lambda.
 // ============================================================================
 
 // lane l < K holds delta_old_l, T_l, G_l, 1/delta_old_l and 1/dref_l; returns delta_new_l
@@ -725,15 +743,13 @@ __device__ double delta_chain(const Dims &d, int l, double T, double G, double i
     return dnew;
 }
 
-__global__ __launch_bounds__(256) void k_delta(Dims d, const double *__restrict__ sall,
+__global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__ sall,
                                                const double *__restrict__ delta_in,
                                                const double *__restrict__ tau_in,
                                                double *__restrict__ delta_out,
                                                double *__restrict__ tau_out,
-                                               const double *__restrict__ psi,
-                                               double *__restrict__ Plam, DrawsDev dr,
+                                               DrawsDev dr,
                                                int64_t iter) {
-    __shared__ double tnew[KP];
     const int m = blockIdx.x;   // global shard
     const int t = threadIdx.x;
     if (t < 64) {
@@ -761,7 +777,6 @@ __global__ __launch_bounds__(256) void k_delta(Dims d, const double *__restrict_
             if (l < KP) {
                 delta_out[(size_t)m * KP + l] = act ? dm : delta_in[(size_t)m * KP + l];
                 tau_out[(size_t)m * KP + l] = act ? tm : tau_in[(size_t)m * KP + l];
-                tnew[l] = tm;
             }
         } else {
             if (l == 0) {
@@ -775,21 +790,12 @@ __global__ __launch_bounds__(256) void k_delta(Dims d, const double *__restrict_
                 }
                 delta_out[(size_t)m * KP] = dnew;
                 tau_out[(size_t)m * KP] = prefix;
-                tnew[0] = prefix;
             }
             if (l >= 1 && l < KP) {
                 delta_out[(size_t)m * KP + l] = delta_in[(size_t)m * KP + l];
                 tau_out[(size_t)m * KP + l] = tau_in[(size_t)m * KP + l];
             }
         }
-    }
-    __syncthreads();
-    const int ml = m - d.shard0;
-    if (ml < 0 || ml >= d.G) return;
-    const size_t base = (size_t)ml * d.PP * KP;
-    for (int e = t; e < d.P * KP; e += 256) {
-        const int k = e % KP;
-        if (k < d.K) Plam[base + e] = psi[base + e] * tnew[k];   // dc:176
     }
 }
 
@@ -919,6 +925,103 @@ __global__ __launch_bounds__(256) void k_eta(Dims d, const double *__restrict__ 
     }
 }
 
+// ============================================================================
+// k_draws: every standard variate one iteration consumes, from
+// the counter-based Philox stream, into buffers with the injected-draw layout
+// (T = 1).  ALU-bound; it runs on the side stream one iteration ahead, overlapping
+// the HBM-bound Y passes, so the sweep kernels only load their variates.
+// Segments (wave-aligned): NZ pairs (local shards), NX pairs, NL pairs (local),
+// Gpsi (local), Gps (local), Gdelta (all g shards: every rank runs every chain).
+// Pointers are indexed by GLOBAL shard mg (as the injected full-g arrays are).
+// ============================================================================
+struct DrawSeg { int64_t nz, nx, nl, gpsi, gps, gdel; };
+
+__host__ __device__ inline DrawSeg draw_segments(const Dims &d) {
+    auto al = [](int64_t v) { return (v + 63) / 64 * 64; };
+    const int64_t kp2 = (d.K + 1) / 2;   // normal pairs per row
+    DrawSeg s;
+    s.nz = al((int64_t)d.G * d.n * kp2);
+    s.nx = al((int64_t)d.n * kp2);
+    s.nl = al((int64_t)d.G * d.P * kp2);
+    s.gpsi = al((int64_t)d.G * d.P * d.K);
+    s.gps = al((int64_t)d.G * d.P);
+    s.gdel = al((int64_t)d.g * d.K);
+    return s;
+}
+
+__global__ __launch_bounds__(256) void k_draws(Dims d, DrawsDev dr, int64_t iter) {
+    const DrawSeg sg = draw_segments(d);
+    const int64_t total = sg.nz + sg.nx + sg.nl + sg.gpsi + sg.gps + sg.gdel;
+    const Rng rng(d.seed);
+    const uint32_t it = (uint32_t)iter;
+    const int kp2 = (d.K + 1) / 2;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        int64_t x = e;
+        if (x < sg.nz) {                                   // dc:104, K x n x g
+            const int64_t pr = x % kp2, rest = x / kp2;
+            const int i = rest % d.n, m = rest / d.n;
+            if (m >= d.G) continue;
+            const int mg = d.shard0 + m;
+            double n0, n1;
+            rng.normal2(SITE_Z, mg, i, (uint32_t)pr, it, n0, n1);
+            double *o = const_cast<double *>(dr.NZ) + ((size_t)mg * d.n + i) * d.K + 2 * pr;
+            o[0] = n0;
+            if (2 * pr + 1 < d.K) o[1] = n1;
+            continue;
+        }
+        x -= sg.nz;
+        if (x < sg.nx) {                                   // dc:126, K x n
+            const int64_t pr = x % kp2, i = x / kp2;
+            if (i >= d.n) continue;
+            double n0, n1;
+            rng.normal2(SITE_X, 0, (uint32_t)i, (uint32_t)pr, it, n0, n1);
+            double *o = const_cast<double *>(dr.NX) + (size_t)i * d.K + 2 * pr;
+            o[0] = n0;
+            if (2 * pr + 1 < d.K) o[1] = n1;
+            continue;
+        }
+        x -= sg.nx;
+        if (x < sg.nl) {                                   // dc:142, K x P x g
+            const int64_t pr = x % kp2, rest = x / kp2;
+            const int j = rest % d.P, m = rest / d.P;
+            if (m >= d.G) continue;
+            const int mg = d.shard0 + m;
+            double n0, n1;
+            rng.normal2(SITE_LAMBDA, mg, j, (uint32_t)pr, it, n0, n1);
+            double *o = const_cast<double *>(dr.NL) + ((size_t)mg * d.P + j) * d.K + 2 * pr;
+            o[0] = n0;
+            if (2 * pr + 1 < d.K) o[1] = n1;
+            continue;
+        }
+        x -= sg.nl;
+        if (x < sg.gpsi) {                                 // dc:150, device layout [g][P][K], shape df/2 + 1/2
+            const int k = x % d.K;
+            const int64_t rest = x / d.K;
+            const int j = rest % d.P, m = rest / d.P;
+            if (m >= d.G) continue;
+            const int mg = d.shard0 + m;
+            const_cast<double *>(dr.Gpsi)[((size_t)mg * d.P + j) * d.K + k] =
+                rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, mg, j, k, it);
+            continue;
+        }
+        x -= sg.gpsi;
+        if (x < sg.gps) {                                  // dc:170, P x g, shape as + n/2
+            const int j = x % d.P, m = x / d.P;
+            if (m >= d.G) continue;
+            const int mg = d.shard0 + m;
+            const_cast<double *>(dr.Gps)[(size_t)mg * d.P + j] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg, j, 0, it);
+            continue;
+        }
+        x -= sg.gps;
+        if (x < (int64_t)d.g * d.K) {                      // dc:158,163, K x g, all shards
+            const int h = x % d.K, mg = x / d.K;
+            const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - h);
+            const_cast<double *>(dr.Gdelta)[(size_t)mg * d.K + h] = rng.gamma(shape, SITE_DELTA, mg, 0, h, it);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_rng_fill(uint64_t seed, int kind, double shape, int site,
                                                   int shard, int64_t iter, int64_t count,
                                                   double *__restrict__ out) {
@@ -979,21 +1082,25 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     }
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
-                   const double *tau_cur, hipStream_t s) {
-    if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, s);
-    hipLaunchKernelGGL(k_lambda, dim3(cdiv(d.P, 8), d.G), dim3(256), 0, s, d, b.C, b.E, b.yy, tau_cur,
-                       b.Lam, b.psi, b.Plam, b.ps, b.omega, b.cpart, dr, iter);
+                   const double *tau_cur, const double *plam_src, hipStream_t s) {
+    if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, plam_src, s);
+    hipLaunchKernelGGL(k_lambda, dim3(cdiv(d.P, 2), d.G), dim3(64), 0, s, d, b.C, b.E, b.yy, tau_cur,
+                       b.Lam, b.psi, plam_src, b.ps, b.omega, b.cpart, dr, iter);
 }
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s) {
-    if (d.kp != KP) return wide::launch_colsum(d, b, s);
-    hipLaunchKernelGGL(k_colsum, dim3(d.G), dim3(256), 0, s, d, b.cpart, b.sloc);
+    const dim3 grid(d.G, d.kp / 32);
+    switch (d.kp) {
+    case 32: hipLaunchKernelGGL(k_colsum<32>, grid, dim3(256), 0, s, d, b.cpart, b.sloc); break;
+    case 64: hipLaunchKernelGGL(k_colsum<64>, grid, dim3(256), 0, s, d, b.cpart, b.sloc); break;
+    default: hipLaunchKernelGGL(k_colsum<128>, grid, dim3(256), 0, s, d, b.cpart, b.sloc); break;
+    }
 }
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                   const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
                   hipStream_t s) {
     if (d.kp != KP) return wide::launch_delta(d, b, dr, iter, delta_in, tau_in, delta_out, tau_out, s);
-    hipLaunchKernelGGL(k_delta, dim3(d.g), dim3(256), 0, s, d, b.sall, delta_in, tau_in, delta_out,
-                       tau_out, b.psi, b.Plam, dr, iter);
+    hipLaunchKernelGGL(k_delta, dim3(d.g), dim3(64), 0, s, d, b.sall, delta_in, tau_in, delta_out,
+                       tau_out, dr, iter);
 }
 void launch_save(const Dims &d, const Bufs &b, double *Lb, double *wsum, int slot, hipStream_t s) {
     const size_t total = (size_t)d.G * d.P * d.K;
@@ -1014,6 +1121,12 @@ void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s) {
     const size_t total = (size_t)d.G * d.NP * d.kp;
     const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
     hipLaunchKernelGGL(k_eta, dim3(grid), dim3(256), 0, s, d, b.X, b.Z, eta_out);
+}
+void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+    const DrawSeg sg = draw_segments(d);
+    const int64_t total = sg.nz + sg.nx + sg.nl + sg.gpsi + sg.gps + sg.gdel;
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_draws, dim3(grid), dim3(256), 0, s, d, dr, iter);
 }
 void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,
                      int64_t count, double *out, hipStream_t s) {

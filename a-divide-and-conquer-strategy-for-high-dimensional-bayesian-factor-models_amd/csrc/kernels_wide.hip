@@ -7,15 +7,15 @@
 // Kernel map (same dataflow as the narrow path)                reference lines
 //   k_gram     A_m = Lambda' diag(w) Lambda, 32x32 tiles, fp64 MFMA    dc:98-99,114-115
 //   k_prep     Zprec chol (LDS, packed), U = L^-1, T = U U',           dc:100-107
-//              Z-draw operators {M1, M2, U, NA} of shard m
+//              Z-draw operators {M1 = s1r T, U} of shard m
 //   k_xchol    Xprec = g I + rho sum A, chol, {Tx, Ux}                  dc:117-118
-//   k_zdraw    Z' = M1 W' + M2 X' + U eps'; S' = W' + NA Z'  fp64 MFMA  dc:101-107,121-123
+//   k_zdraw    V' = W' - sr A X'; Z' = M1 V' + U eps';                  dc:101-107,121-123
+//              S' = W' - s1r A Z'                             fp64 MFMA
 //   k_xdraw    X' = Tx S' + Ux eps'                           fp64 MFMA  dc:119-128
 //   k_lambda   one workgroup per loading row j: register-blocked        dc:140-145,150,
 //              Cholesky of Q_j (8x8 blocks per thread), fused forward   dc:156,169-171
 //              solve, blocked back solve; psi, SS identity, ps, omega
-//   k_colsum   column sums of psi o Lambda^2                            dc:156
-//   k_delta    MGP chain over up to 128 factors (2 per lane), Plam      dc:155-165,175-177
+//   k_delta    MGP chain over up to 128 factors (2 per lane)            dc:155-165
 #include "dcfm_internal.h"
 #include "philox.h"
 #include "linalg.h"
@@ -141,8 +141,9 @@ __global__ __launch_bounds__(256) void k_gram(Dims d, const double *__restrict__
 // k_prep: Z-draw operators of shard m (one block per local shard).        dc:100-107
 //   R = cholcov(Zprec), Zprec = I + (1-rho) A_m; cholcov reads the upper triangle,
 //   so the lower factor L = R' is the Cholesky of S[r][c] = Zprec[c][r] (c <= r).
-//   U = L^{-1}, T = U U';  ZM = {M1 = s1r T, M2 = -s1r sr T A, U, NA = -s1r A}
-//   (the reference's R'\(R\bz) + R'\z is T bz + U z, quirk Q2).  Padding (>= K) is 0.
+//   U = L^{-1}, T = U U';  ZM[m] = {M1 = s1r T, -, U, -}: the reference's
+//   R'\(R\bz) + R'\z is T bz + U z (quirk Q2), with bz = s1r (W - sr A X) formed in
+//   k_zdraw from A directly.  Padding (>= K) is 0.
 // ============================================================================
 template <int KW>
 __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__ A, double *__restrict__ ZM) {
@@ -157,22 +158,11 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
     wg_lower_inverse_packed(S1, dinv, S2, N);   // U -> S2
     wg_uut_packed(S2, S1, N);                   // T -> S1 (L no longer needed)
     double *Zm = ZM + (size_t)m * 4 * KW * KW;
-    const double s2 = -d.s1r * d.sr;
     for (int e = t; e < KW * KW; e += 256) {
         const int a = e / KW, c = e % KW;
-        double m1 = 0.0, m2 = 0.0, u = 0.0, na = 0.0;
-        if (a < N && c < N) {
-            m1 = d.s1r * packed_sym(S1, N, a, c);
-            u = packed_low(S2, N, a, c);
-            na = -d.s1r * Am[e];
-            double acc = 0.0;
-            for (int b = 0; b < N; ++b) acc += packed_sym(S1, N, a, b) * Am[(size_t)b * KW + c];
-            m2 = s2 * acc;
-        }
-        Zm[e] = m1;
-        Zm[(size_t)KW * KW + e] = m2;
-        Zm[(size_t)2 * KW * KW + e] = u;
-        Zm[(size_t)3 * KW * KW + e] = na;
+        const bool in = a < N && c < N;
+        Zm[e] = in ? d.s1r * packed_sym(S1, N, a, c) : 0.0;
+        Zm[(size_t)2 * KW * KW + e] = in ? packed_low(S2, N, a, c) : 0.0;
     }
 }
 
@@ -209,28 +199,25 @@ __device__ __forceinline__ d2 row_normals(const Dims &d, const double *inj, bool
                                           int kk, int64_t iter) {
     d2 ev = {0.0, 0.0};
     if (!live || kk >= d.K) return ev;
-    if (d.inject) {
-        ev.x = inj[kk];
-        ev.y = (kk + 1 < d.K) ? inj[kk + 1] : 0.0;
-    } else {
-        const Rng rng(d.seed);
-        double n0, n1;
-        rng.normal2(site, mg, i, kk >> 1, (uint32_t)iter, n0, n1);
-        ev.x = n0;
-        ev.y = (kk + 1 < d.K) ? n1 : 0.0;
-    }
+    ev.x = inj[kk];
+    ev.y = (kk + 1 < d.K) ? inj[kk + 1] : 0.0;
     return ev;
 }
 
 // ============================================================================
 // k_zdraw: per (shard m, 64 rows), one wave per 16 rows i.                  dc:101-107,121-123
-//   Z' = M1 W' + M2 X' + U eps'   (KW x 16, MT = KW/16 MFMA tiles, operators from L2)
-//   S' = W' + NA Z'               the C/D layout of Z' (row = q + 4g) is the B operand
+//   V' = W' - sr A X'        (= bz / s1r: Zmsg'(Y_i - sr L X_i) by the identity W = Y (w o L))
+//   Z' = M1 V' + U eps'      (M1 = s1r T, U from k_prep; KW x 16 as MT = KW/16 MFMA tiles)
+//   S' = W' - s1r A Z'       (the shard's X message, dc:121-123)
+// The f64 C/D layout of each product (row = q + 4g of tile mt) is directly the B
+// operand of the next one (k-step 4 mt + g), so nothing crosses LDS; the A
+// operands (A_m, M1, U) stream from L2.
 // ============================================================================
 template <int KW>
-__global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W, const double *__restrict__ ZM,
-                                               const double *__restrict__ X, double *__restrict__ Z,
-                                               double *__restrict__ Sp, DrawsDev dr, int64_t iter) {
+__global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W, const double *__restrict__ A,
+                                               const double *__restrict__ ZM, const double *__restrict__ X,
+                                               double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
+                                               int64_t iter) {
     constexpr int MT = KW / 16;
     const int nrb = d.NP >> 6;
     const int w = xcd_remap(blockIdx.x, gridDim.x);
@@ -240,39 +227,53 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
     const int mg = d.shard0 + m;
     const int i = rb * 64 + wave * 16 + c;
     const bool live = i < d.n;
-    const double *M1 = ZM + (size_t)m * 4 * KW * KW, *M2 = M1 + KW * KW, *U = M2 + KW * KW, *NA = U + KW * KW;
+    const double *Am = A + (size_t)m * KW * KW;
+    const double *M1 = ZM + (size_t)m * 4 * KW * KW, *U = M1 + 2 * KW * KW;
     const double *Wi = W + ((size_t)m * d.NP + i) * KW;
     const double *Xi = X + (size_t)i * KW;
-    const double *nz = d.inject ? dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K
-                                : nullptr;
-    d4 az[MT];
+    // --- A X'
+    d4 av[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) az[mt] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int mt = 0; mt < MT; ++mt) av[mt] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 2
     for (int t = 0; t < KW / 8; ++t) {
         const int kk = 8 * t + 2 * q;
-        const d2 wv = *reinterpret_cast<const d2 *>(Wi + kk);
         const d2 xv = *reinterpret_cast<const d2 *>(Xi + kk);
-        const d2 ev = row_normals(d, nz, live, SITE_Z, mg, i, kk, iter);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-            const size_t o = (size_t)(16 * mt + c) * KW + kk;
-            const d2 a1 = *reinterpret_cast<const d2 *>(M1 + o);
-            const d2 a2 = *reinterpret_cast<const d2 *>(M2 + o);
-            const d2 a3 = *reinterpret_cast<const d2 *>(U + o);
-            az[mt] = mfma16x16x4(a1.x, wv.x, az[mt]);
-            az[mt] = mfma16x16x4(a2.x, xv.x, az[mt]);
-            az[mt] = mfma16x16x4(a3.x, ev.x, az[mt]);
-            az[mt] = mfma16x16x4(a1.y, wv.y, az[mt]);
-            az[mt] = mfma16x16x4(a2.y, xv.y, az[mt]);
-            az[mt] = mfma16x16x4(a3.y, ev.y, az[mt]);
+            const d2 a2 = *reinterpret_cast<const d2 *>(Am + (size_t)(16 * mt + c) * KW + kk);
+            av[mt] = mfma16x16x4(a2.x, xv.x, av[mt]);
+            av[mt] = mfma16x16x4(a2.y, xv.y, av[mt]);
         }
     }
-    d4 as[MT];
+    // --- V' = W' - sr (A X')
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) as[mt][g] = Wi[16 * mt + q + 4 * g];
+        for (int g = 0; g < 4; ++g) av[mt][g] = Wi[16 * mt + q + 4 * g] - d.sr * av[mt][g];
+    // --- Z' = M1 V' + U eps'      eps[i][kk] of dc:104, kk = 16 mt2 + 4 g + q
+    const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K;
+    d4 az[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) az[mt] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int mt2 = 0; mt2 < MT; ++mt2)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int kk = 16 * mt2 + 4 * g + q;
+            double e = 0.0;
+            if (live && kk < d.K) e = nz[kk];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                const size_t o = (size_t)(16 * mt + c) * KW + kk;
+                az[mt] = mfma16x16x4(M1[o], av[mt2][g], az[mt]);
+                az[mt] = mfma16x16x4(U[o], e, az[mt]);
+            }
+        }
+    // --- S' = W' - s1r (A Z')
+    d4 as[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) as[mt] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int mt2 = 0; mt2 < MT; ++mt2)
 #pragma unroll
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
             const int kk = 16 * mt2 + 4 * g + q;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt)
-                as[mt] = mfma16x16x4(NA[(size_t)(16 * mt + c) * KW + kk], az[mt2][g], as[mt]);
+                as[mt] = mfma16x16x4(Am[(size_t)(16 * mt + c) * KW + kk], az[mt2][g], as[mt]);
         }
     double *Zr = Z + ((size_t)m * d.NP + i) * KW;
     double *Sr = Sp + ((size_t)m * d.NP + i) * KW;
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
         for (int g = 0; g < 4; ++g) {
             const int k = 16 * mt + q + 4 * g;
             if (live) Zr[k] = (k < d.K) ? az[mt][g] : 0.0;
-            Sr[k] = live ? as[mt][g] : 0.0;
+            Sr[k] = live ? Wi[k] - d.s1r * as[mt][g] : 0.0;
         }
 }
 
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
     const bool live = i < d.n;
     const size_t stride = (size_t)d.NP * KW;
     const double *Tx = XM, *Ux = XM + KW * KW;
-    const double *nx = d.inject ? dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K : nullptr;
+    const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K;
     d4 ax[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) ax[mt] = d4{0.0, 0.0, 0.0, 0.0};
@@ -350,6 +351,8 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
 //     waves 1.., threads 64..      off-diagonal blocks (I, J), I > J
 //   Right-looking: per pivot k the owners of block column k/8 scale column k into
 //   LDS, everyone with columns > k applies the rank-1 update from registers.
+//   Plam_j = psi_j o tau' (dc:176) is formed here from the previous iteration's psi
+//   and tau unless plam_src is given (first iteration after dcfm_set_state).
 //   Then Lambda_j = L' \ (v + z) (blocked back solve, z = normrnd dc:142),
 //   psi_j (dc:150), SS_j = yy_j - 2 x.C_j + x'E x, ps_j, omega_j (dc:169-171).
 //   Rows r >= K inside the last block are an identity pad.
@@ -359,7 +362,7 @@ constexpr int lambda_threads(int KW) { return 64 + ((KW / 8) * (KW / 8 - 1) / 2 
 template <int KW>
 __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
     Dims d, const double *__restrict__ C, const double *__restrict__ E, const double *__restrict__ yy,
-    const double *__restrict__ tau_cur, const double *__restrict__ Plam, double *__restrict__ Lam,
+    const double *__restrict__ tau_cur, const double *__restrict__ plam_src, double *__restrict__ Lam,
     double *__restrict__ psi, double *__restrict__ ps, double *__restrict__ omega, double *__restrict__ cpart,
     DrawsDev dr, int64_t iter) {
     constexpr int NB = KW / 8;
@@ -402,7 +405,11 @@ __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
                 double val;
                 if (r < K && c < K) {
                     val = psj * Em[(size_t)r * KW + c];                  // ps_j * eta2 (dc:141)
-                    if (r == c) val = Plam[rowoff + r] + val;            // diag(Plam_j) + ...
+                    if (r == c) {                                         // diag(Plam_j) + ...
+                        const double pl = plam_src ? plam_src[rowoff + r]
+                                                   : psi[rowoff + r] * tau_cur[(size_t)mg * KW + r];   // dc:176
+                        val = pl + val;
+                    }
                 } else {
                     val = (r == c) ? 1.0 : 0.0;
                 }
@@ -418,7 +425,11 @@ __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
     }
     __syncthreads();
     // ---- factorisation with fused forward solve (dc:142 chol, dc:143 Llam \ blam)
+#ifdef DCFM_VARIANT_NOFACTOR
+    for (int Jk = 0; Jk < 0; ++Jk) {
+#else
     for (int Jk = 0; Jk < nb; ++Jk) {
+#endif
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
             const int k = 8 * Jk + kk;
@@ -443,7 +454,11 @@ __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
                 }
             }
             __syncthreads();
+#ifndef DCFM_VARIANT_NOUPDATE
             if (role != 3 && J >= Jk) {
+#else
+            if (role != 3 && J >= Jk && d.n < 0) {
+#endif
                 const bool same = (J == Jk);
                 double lc[8];
 #pragma unroll
@@ -495,15 +510,7 @@ __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
             const int c = 8 * J + v;
-            double z = 0.0;
-            if (c < K) {
-                if (d.inject) {
-                    z = dr.NL[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + c];
-                } else {
-                    const Rng rng(d.seed);
-                    z = rng.normal(SITE_LAMBDA, mg, j, c, (uint32_t)iter);
-                }
-            }
+            const double z = (c < K) ? dr.NL[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + c] : 0.0;
             sw[c] = a[0][v] + z;
         }
     }
@@ -543,20 +550,23 @@ __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
         const int r = t;
         const double xr = (r < K) ? sx[r] : 0.0;
         const double cjr = C[rowoff + r];
-        double ex = 0.0;
-        for (int c = 0; c < K; ++c) ex += Em[(size_t)c * KW + r] * sx[c];   // (E x)_r
+        double ex = 0.0;                                                 // (E x)_r
+        {
+            double e8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+            int c = 0;
+            for (; c + 8 <= K; c += 8) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) e8[u] += Em[(size_t)(c + u) * KW + r] * sx[c + u];
+            }
+            for (; c < K; ++c) e8[0] += Em[(size_t)c * KW + r] * sx[c];
+            ex = ((e8[0] + e8[1]) + (e8[2] + e8[3])) + ((e8[4] + e8[5]) + (e8[6] + e8[7]));
+        }
         contrib = xr * (ex - 2.0 * cjr);
         double psir = 0.0;
         if (r < K) {
             const double tr = tau_cur[(size_t)mg * KW + r];
             const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xr * xr * tr));
-            double G;
-            if (d.inject) {
-                G = dr.Gpsi[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + r) * d.P + j];
-            } else {
-                const Rng rng(d.seed);
-                G = rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, mg, j, r, (uint32_t)iter);
-            }
+            const double G = dr.Gpsi[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + r];
             psir = scale * G;
             psi[rowoff + r] = psir;
         }
@@ -571,13 +581,7 @@ __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
         double s = 0.0;
         for (int w = 0; w < (KW + 63) / 64; ++w) s += red[w];
         const double SS = yy[(size_t)m * d.PP + j] + s;
-        double G;
-        if (d.inject) {
-            G = dr.Gps[((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j];
-        } else {
-            const Rng rng(d.seed);
-            G = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg, j, 0, (uint32_t)iter);
-        }
+        const double G = dr.Gps[((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j];
         const double psn = (1.0 / (d.bs + 0.5 * SS)) * G;     // dc:170
         ps[(size_t)m * d.PP + j] = psn;
         omega[(size_t)m * d.PP + j] = 1.0 / psn;              // dc:171 (Q1)
@@ -585,22 +589,26 @@ __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
 }
 
 // ============================================================================
-// k_colsum: sloc[m][k] = sum_{j<P} cpart[m][j][k], fixed order          dc:156 sum(mat)
-// ============================================================================
+// block = (shard m, 32 columns); 8 row groups x 4 independent accumulators each.
 template <int KW>
 __global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict__ cpart, double *__restrict__ sloc) {
-    constexpr int NG = 256 / KW;
-    __shared__ double part[NG][KW];
-    const int m = blockIdx.x, k = threadIdx.x % KW, grp = threadIdx.x / KW;
-    double s = 0.0;
-    for (int j = grp; j < d.P; j += NG) s += cpart[((size_t)m * d.PP + j) * KW + k];
-    part[grp][k] = s;
+    __shared__ double part[8][32];
+    const int m = blockIdx.x, k = 32 * blockIdx.y + (threadIdx.x & 31), grp = threadIdx.x >> 5;
+    const double *cp = cpart + (size_t)m * d.PP * KW + k;
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
+    int j = grp;
+    for (; j + 24 < d.P; j += 32) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s4[u] += cp[(size_t)(j + 8 * u) * KW];
+    }
+    for (; j < d.P; j += 8) s4[0] += cp[(size_t)j * KW];
+    part[grp][threadIdx.x & 31] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     __syncthreads();
-    if (threadIdx.x < KW) {
+    if (threadIdx.x < 32) {
         double tt = 0.0;
 #pragma unroll
-        for (int g2 = 0; g2 < NG; ++g2) tt += part[g2][threadIdx.x];
-        sloc[(size_t)m * KW + threadIdx.x] = tt;
+        for (int g2 = 0; g2 < 8; ++g2) tt += part[g2][threadIdx.x];
+        sloc[(size_t)m * KW + k] = tt;
     }
 }
 
@@ -608,8 +616,8 @@ __global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict
 // k_delta: multiplicative-gamma-process chain for K in 33..128 (NV = KW/64
 // factors per lane: index l + 64 s).  Same algebra as the narrow kernel: every
 // shard's h >= 2 step reads shard 1's already-updated delta_h (quirk Q4), the
-// recomputed cumprod is the scalar factor F_h (dc:155-165); then Plam = psi o tau'
-// (dc:175-177) for local shards.  (K == 1, quirk Q5, is narrow-only.)
+// recomputed cumprod is the scalar factor F_h (dc:155-165).  (K == 1, quirk Q5,
+// is narrow-only.)
 // ============================================================================
 template <int NV>
 __device__ __forceinline__ void suffix_sum_nv(double (&v)[NV], int l) {
@@ -643,13 +651,11 @@ __device__ void delta_chain_nv(const Dims &d, int l, const double (&T)[NV], cons
 }
 
 template <int KW>
-__global__ __launch_bounds__(256) void k_delta(Dims d, const double *__restrict__ sall,
+__global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__ sall,
                                                const double *__restrict__ delta_in, const double *__restrict__ tau_in,
                                                double *__restrict__ delta_out, double *__restrict__ tau_out,
-                                               const double *__restrict__ psi, double *__restrict__ Plam, DrawsDev dr,
-                                               int64_t iter) {
+                                               DrawsDev dr, int64_t iter) {
     constexpr int NV = KW / 64;
-    __shared__ double tnew[KW];
     const int m = blockIdx.x;   // global shard
     const int t = threadIdx.x;
     if (t < 64) {
@@ -696,16 +702,7 @@ __global__ __launch_bounds__(256) void k_delta(Dims d, const double *__restrict_
             const size_t o = (size_t)m * KW + idx;
             delta_out[o] = act ? dm[s] : delta_in[o];
             tau_out[o] = act ? tm[s] : tau_in[o];
-            tnew[idx] = tm[s];
         }
-    }
-    __syncthreads();
-    const int ml = m - d.shard0;
-    if (ml < 0 || ml >= d.G) return;
-    const size_t base = (size_t)ml * d.PP * KW;
-    for (int e = t; e < d.P * KW; e += 256) {
-        const int k = e % KW;
-        if (k < d.K) Plam[base + e] = psi[base + e] * tnew[k];   // dc:176
     }
 }
 
@@ -734,26 +731,23 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
                                            d.nranks > 1 ? b.xa_all : b.xa, b.XM));
 }
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
-    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_zdraw<KW>, dim3((d.NP / 64) * d.G), dim3(256), 0, s, d, b.W, b.ZM,
-                                           b.X, b.Z, b.Sp, dr, iter));
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_zdraw<KW>, dim3((d.NP / 64) * d.G), dim3(256), 0, s, d, b.W, b.A,
+                                           b.ZM, b.X, b.Z, b.Sp, dr, iter));
 }
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_xdraw<KW>, dim3(cdiv(d.n, 16)), dim3(64), 0, s, d, b.xall, b.XM, b.X,
                                            dr, iter));
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *tau_cur,
-                   hipStream_t s) {
+                   const double *plam_src, hipStream_t s) {
     WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_lambda<KW>, dim3(d.P, d.G), dim3(lambda_threads(KW)), 0, s, d, b.C,
-                                           b.E, b.yy, tau_cur, b.Plam, b.Lam, b.psi, b.ps, b.omega, b.cpart, dr,
+                                           b.E, b.yy, tau_cur, plam_src, b.Lam, b.psi, b.ps, b.omega, b.cpart, dr,
                                            iter));
-}
-void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s) {
-    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_colsum<KW>, dim3(d.G), dim3(256), 0, s, d, b.cpart, b.sloc));
 }
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
                   const double *tau_in, double *delta_out, double *tau_out, hipStream_t s) {
-    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_delta<KW>, dim3(d.g), dim3(256), 0, s, d, b.sall, delta_in, tau_in,
-                                           delta_out, tau_out, b.psi, b.Plam, dr, iter));
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_delta<KW>, dim3(d.g), dim3(64), 0, s, d, b.sall, delta_in, tau_in,
+                                           delta_out, tau_out, dr, iter));
 }
 #undef WIDE_DISPATCH
 

@@ -68,13 +68,33 @@ __device__ __forceinline__ double wave_suffix_sum(double v, int l) {
     return v;
 }
 
-// standard gamma of the delta site, h = 0-based factor index (dc:158,163)
+// standard gamma of the delta site, h = 0-based factor index (dc:158,163), from the draw buffer
 __device__ inline double delta_G(const Dims &d, const DrawsDev &dr, int64_t iter, int mg, int h) {
-    if (d.inject) return dr.Gdelta[((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + h];
-    const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - h);
-    const Rng rng(d.seed);
-    return rng.gamma(shape, SITE_DELTA, mg, 0, h, (uint32_t)iter);
+    return dr.Gdelta[((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + h];
 }
+
+// Development-only phase timer (build with -DDCFM_PHASE_TIMING): lane 0 of every
+// wave adds shader-clock deltas per phase into g_phase (read by dcfm_debug_phases).
+#ifdef DCFM_PHASE_TIMING
+extern __device__ unsigned long long g_phase[32];
+#define PHASE_T0()                                                                          \
+    unsigned long long ph_t_ = __builtin_amdgcn_s_memtime(), ph_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define PHASE(k)                                                                            \
+    do {                                                                                    \
+        const unsigned long long ph_n_ = __builtin_amdgcn_s_memtime();                      \
+        ph_acc_[(k)] += ph_n_ - ph_t_;                                                      \
+        ph_t_ = ph_n_;                                                                      \
+    } while (0)
+#define PHASE_END()                                                                         \
+    do {                                                                                    \
+        if ((threadIdx.x & 63) == 0)                                                        \
+            for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_phase[k_], ph_acc_[k_]);            \
+    } while (0)
+#else
+#define PHASE_T0() (void)0
+#define PHASE(k) (void)0
+#define PHASE_END() (void)0
+#endif
 
 // eta = sqrt(rho) X + sqrt(1-rho) Z    (dc:81,133) — one definition for every use
 __device__ __forceinline__ double eta_of(double sr, double s1r, double x, double z) {

@@ -158,6 +158,13 @@ class Sampler:
     def set_profiling(self, on: bool):
         self._check(self.lib.dcfm_set_profiling(self.h, 1 if on else 0))
 
+    def set_profiling_kernels(self, names):
+        """Time only these kernels (names of _abi.KERNEL_IDS); empty = off."""
+        mask = 0
+        for nm in names:
+            mask |= 1 << _abi.KERNEL_IDS[nm]
+        self._check(self.lib.dcfm_set_profiling_mask(self.h, mask))
+
     def kernel_stats(self) -> dict:
         ms = (C.c_double * _abi.K_COUNT)()
         cnt = (C.c_int64 * _abi.K_COUNT)()

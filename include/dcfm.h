@@ -148,8 +148,12 @@ int64_t dcfm_saved_samples(const dcfm_handle *h);
 #define DCFM_K_ASSEMBLE 10
 #define DCFM_K_COMM     11
 #define DCFM_K_XCHOL    12
-#define DCFM_K_COUNT    13
+#define DCFM_K_DRAWS    13   /* on-device Philox variates of the next iteration (side stream) */
+#define DCFM_K_COUNT    14
 int  dcfm_set_profiling(dcfm_handle *h, int enable);
+/* Time only the kernels whose bit (1u << DCFM_K_*) is set: two events per timed
+ * launch cost host time, so a throughput run times just the kernel it reports. */
+int  dcfm_set_profiling_mask(dcfm_handle *h, uint32_t mask);
 int  dcfm_get_kernel_stats(dcfm_handle *h, double ms[DCFM_K_COUNT], int64_t launches[DCFM_K_COUNT]);
 const char *dcfm_kernel_name(int id);
 
