@@ -567,7 +567,7 @@ static int flush_batch(dcfm_handle *h) {
                                h->sasm));
         NCCLC(h, ncclGroupEnd());
     }
-    const int kext = round_up(h->batch * d.K, 8);
+    const int kext = round_up(h->batch * d.K, 16);   // k_assemble chunk
     const double effsamp = (double)h->cfg.mcmc / (double)h->cfg.thin;   // dc:45 (Q8)
     {
         KTimer t(h, DCFM_K_ASSEMBLE, h->sasm);

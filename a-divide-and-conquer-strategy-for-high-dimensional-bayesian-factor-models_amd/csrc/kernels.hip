@@ -546,130 +546,211 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
 }
 
 // ============================================================================
-// k_lambda: loading rows.  A half-wave (32 lanes) owns one row j; lane r holds
-// row r of Q_j = diag(Plam_j) + ps_j E_m in registers.        dc:140-145 (+150,156,169-171)
-//   Plam_j = psi_j o tau' (dc:176, previous iteration's psi and tau) unless plam_src
-//   is given (the first iteration after dcfm_set_state reads the caller's Plam).
-//   L = chol(Q,'lower'), v = L \ (ps_j C_j)   (chol_rows_fwd)
-//   Lambda_j = L' \ (v + z)                    (= ylam + mlam)
-//   psi_j  = Gpsi * 1/(df/2 + 0.5 lambda^2 tau)               (dc:150, tau of the previous it.)
-//   SS_j   = yy_j - 2 lambda.C_j + lambda' E lambda  ->  ps_j = Gps * 1/(bs + 0.5 SS_j), w = 1/ps
-// One independent 64-thread block (2 rows) per launch slot: no block barrier, so
-// waves drift apart and one wave's loads overlap another's factorisation; E_m
-// rows come from L2 (no LDS staging).  Every global load of the row is issued up
-// front.  psi o lambda^2 of the row -> cpart[m][j][:] (k_colsum sums the rows).
+// k_lambda: loading rows.                                   dc:140-145 (+150,156,169-171)
+// One wave = 4 loading rows j; a 16-lane DPP row (quarter wave) owns one row:
+// lane l holds rows l and l+16 of Q_j = diag(Plam_j) + ps_j E_m in registers
+// (qa, qb).  Per pair of pivots (k, k+1):
+//   * the 2x2 pivot block and the rhs entries are broadcast inside the quarter
+//     with v_mov_dpp row_newbcast (compile-time lanes, no SGPR round trip),
+//   * each lane forms its rows' L entries, writes them to the pair-packed LDS
+//     image, and applies the rank-2 trailing update from LDS,
+//   * the forward solve L v = ps_j C_j rides along (dc:143 vlam = Llam \ blam).
+// Rows < 16 finish after pivot 15, so the second half of the factorisation
+// touches only qb (compile-time pruning; ~3x fewer VALU ops per row than a
+// 32-lane row).  Then Lambda_j = L' \ (v + z) (dc:143-144) right-looking from
+// the bottom, psi_j (dc:150), SS_j = yy_j - 2 x.C_j + x'E x and ps_j, omega_j
+// (dc:169-171).  Plam_j = psi_j o tau' (dc:176) is formed from the previous
+// iteration's psi and tau unless plam_src is given (first iteration after
+// dcfm_set_state).  Every global load of the row is issued up front.
+// psi o lambda^2 of the row -> cpart[m][j][:] (k_colsum sums the rows).
 // ============================================================================
 __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict__ C,
-                                                const double *__restrict__ E,
-                                                const double *__restrict__ yy,
-                                                const double *__restrict__ tau_cur,
-                                                double *__restrict__ Lam, double *__restrict__ psi,
-                                                const double *__restrict__ plam_src, double *__restrict__ ps,
-                                                double *__restrict__ omega,
-                                                double *__restrict__ cpart, DrawsDev dr,
-                                                int64_t iter) {
-    __shared__ __attribute__((aligned(16))) double LP[2][P2STRIDE];
+                                               const double *__restrict__ E,
+                                               const double *__restrict__ yy,
+                                               const double *__restrict__ tau_cur,
+                                               double *__restrict__ Lam, double *__restrict__ psi,
+                                               const double *__restrict__ plam_src, double *__restrict__ ps,
+                                               double *__restrict__ omega,
+                                               double *__restrict__ cpart, DrawsDev dr,
+                                               int64_t iter) {
+    __shared__ __attribute__((aligned(16))) double LP[4][P2STRIDE];
     const int m = blockIdx.y;
     const int mg = d.shard0 + m;
-    const int lane = threadIdx.x & 63;
-    const int hw = threadIdx.x >> 5;          // half-wave id 0..1
-    const bool upper = (lane >= 32);
-    const int r = lane & 31;                  // matrix row
-    const int j = blockIdx.x * 2 + hw;
+    const int lane = threadIdx.x, qw = lane >> 4, l = lane & 15;
+    const int j = blockIdx.x * 4 + qw;
     const bool valid = j < d.P;
-    const bool real = r < d.K;
-    const size_t rowoff = ((size_t)m * d.PP + (valid ? j : 0)) * KP;
-    // every global load of the row is issued up front (one latency, overlapping the
-    // E staging and the factorisation) — each later dependent load would cost a
-    // full round trip on a latency-bound kernel
-    const bool rv = real && valid;
-    const int64_t ti = iter - dr.first_iter;
     const int jj = valid ? j : 0;
-    const double psj = valid ? ps[(size_t)m * d.PP + j] : 0.0;
-    const double tr = rv ? tau_cur[(size_t)mg * KP + r] : 0.0;
-    const double psi_old = (rv && !plam_src) ? psi[rowoff + r] : 0.0;
-    const double plam_in = (rv && plam_src) ? plam_src[rowoff + r] : 0.0;
-    const double cjr = valid ? C[rowoff + r] : 0.0;
-    const double z = rv ? dr.NL[(((size_t)ti * d.g + mg) * d.P + jj) * d.K + r] : 0.0;         // dc:142
-    const double Gpsi = rv ? dr.Gpsi[(((size_t)ti * d.g + mg) * d.P + jj) * d.K + r] : 0.0;    // dc:150
-    const double Gps = (valid && r == 0) ? dr.Gps[((size_t)ti * d.g + mg) * d.P + jj] : 0.0;    // dc:170
-    const double yyj = (valid && r == 0) ? yy[(size_t)m * d.PP + jj] : 0.0;
-    const double *Er = E + ((size_t)m * KP + r) * KP;     // row r of E_m (L2-resident)
-    double q[KP];
+    const int r0 = l, r1 = l + 16;
+    const bool rv0 = valid && r0 < d.K, rv1 = valid && r1 < d.K;
+    const size_t rowoff = ((size_t)m * d.PP + jj) * KP;
+    const int64_t ti = iter - dr.first_iter;
+    const size_t drow = ((size_t)ti * d.g + mg) * d.P + jj;
+    // ---- every global load up front
+    const double psj = valid ? ps[(size_t)m * d.PP + jj] : 0.0;
+    const double tr0 = rv0 ? tau_cur[(size_t)mg * KP + r0] : 0.0, tr1 = rv1 ? tau_cur[(size_t)mg * KP + r1] : 0.0;
+    const double *pin = plam_src ? plam_src : psi;
+    const double pin0 = rv0 ? pin[rowoff + r0] : 0.0, pin1 = rv1 ? pin[rowoff + r1] : 0.0;
+    const double c0 = valid ? C[rowoff + r0] : 0.0, c1 = valid ? C[rowoff + r1] : 0.0;
+    const double z0 = rv0 ? dr.NL[drow * d.K + r0] : 0.0, z1 = rv1 ? dr.NL[drow * d.K + r1] : 0.0;       // dc:142
+    const double G0 = rv0 ? dr.Gpsi[drow * d.K + r0] : 0.0, G1 = rv1 ? dr.Gpsi[drow * d.K + r1] : 0.0;   // dc:150
+    const double Gps = (valid && l == 0) ? dr.Gps[((size_t)ti * d.g + mg) * d.P + jj] : 0.0;           // dc:170
+    const double yyj = (valid && l == 0) ? yy[(size_t)m * d.PP + jj] : 0.0;
+    const double *Ea = E + ((size_t)m * KP + r0) * KP, *Eb = E + ((size_t)m * KP + r1) * KP;
+    constexpr int KH = KP / 2;       // rows < 16 only ever touch columns < 16 (lower triangle)
+    double qa[KH], qb[KP];
 #pragma unroll
     for (int c = 0; c < KP; c += 2) {
-        const d2 e2 = *reinterpret_cast<const d2 *>(Er + c);
-        q[c] = e2.x;
-        q[c + 1] = e2.y;
+        const d2 eb = *reinterpret_cast<const d2 *>(Eb + c);
+        qb[c] = eb.x; qb[c + 1] = eb.y;
+        if (c < KH) {
+            const d2 ea = *reinterpret_cast<const d2 *>(Ea + c);
+            qa[c] = ea.x; qa[c + 1] = ea.y;
+        }
     }
-    PHASE_T0();
-    // --- build Q row r and rhs
+    // ---- Q_j rows r0, r1: ps_j * eta2 + diag(Plam_j) (dc:141), identity padding
+    const double plam0 = plam_src ? pin0 : pin0 * tr0, plam1 = plam_src ? pin1 : pin1 * tr1;   // dc:176
 #pragma unroll
-    for (int c = 0; c < KP; ++c) q[c] = psj * q[c];
-    const double plam = rv ? (plam_src ? plam_in : psi_old * tr) : 1.0;   // Plam = psi o tau' (dc:176)
-#pragma unroll
-    for (int c = 0; c < KP; ++c)
-        if (c == r) q[c] = (real && valid) ? plam + q[c] : 1.0;
-
-    double *Lp = LP[hw];
-    double vr = 0.0;
-    PHASE(0);
-    chol2_rows<true>(q, Lp, r, upper, psj * cjr, vr);
-    PHASE(1);
-    // --- + z  (dc:142 normrnd(0,1,K,1))
-    double wr = vr + z;
-    PHASE(2);
-    // --- back solve L' x = w, two rows per step;  L[c][r] = Lp[p2idx(c, r)]
-    double xr = 0.0;
-    const int br = pb2(r >> 1) - 2 * (r & ~1) + (r & 1);     // L[c][r] at br + 2c
-#pragma unroll 2
-    for (int c = KP - 1; c >= 1; c -= 2) {
-        // x_c = w_c / L_cc ; x_{c-1} = (w_{c-1} - L[c][c-1] x_c) / L_{c-1,c-1}
-        const double xc = readsel(wr, c, upper) * Lp[PACK2 + c];
-        const double lcc1 = Lp[p2idx(c, c - 1)];
-        const double xc1 = (readsel(wr, c - 1, upper) - lcc1 * xc) * Lp[PACK2 + c - 1];
-        if (r == c) xr = xc;
-        if (r == c - 1) xr = xc1;
-        if (r < c - 1) wr -= Lp[br + 2 * c] * xc + Lp[br + 2 * (c - 1)] * xc1;
+    for (int c = 0; c < KP; ++c) {
+        qb[c] = psj * qb[c];
+        if (c == r1) qb[c] = rv1 ? plam1 + qb[c] : 1.0;
+        if (c < KH) {
+            qa[c] = psj * qa[c];
+            if (c == r0) qa[c] = rv0 ? plam0 + qa[c] : 1.0;
+        }
     }
-    if (!real) xr = 0.0;
-    PHASE(3);
-
-    // --- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr; x broadcast through the scratch slots
-    Lp[PACK2 + KP + r] = xr;
-    double ex = 0.0;
+    double bva = psj * c0, bvb = psj * c1;        // blam = ps_j eta' Y_j (dc:141)
+    double va = 0.0, vb = 0.0;
+    double *Lp = LP[qw];
+    // ---- factorisation, two pivots per step, forward solve fused
+    static_for<KP / 2>([&](auto JC) {
+        constexpr int jp = decltype(JC)::value, k = 2 * jp;
+        double a, b, c2, bk, bk1;
+        if constexpr (k < 16) {
+            a = bcast16<k>(qa[k]);
+            b = bcast16<k + 1>(qa[k]);
+            c2 = bcast16<k + 1>(qa[k + 1]);
+            bk = bcast16<k>(bva);
+            bk1 = bcast16<k + 1>(bva);
+        } else {
+            a = bcast16<k - 16>(qb[k]);
+            b = bcast16<k - 15>(qb[k]);
+            c2 = bcast16<k - 15>(qb[k + 1]);
+            bk = bcast16<k - 16>(bvb);
+            bk1 = bcast16<k - 15>(bvb);
+        }
+        const double i00 = rsqrt_f64(a);
+        const double l00 = a * i00, l10 = b * i00;
+        const double d11 = c2 - l10 * l10;
+        const double i11 = rsqrt_f64(d11);
+        const double l11 = d11 * i11;
+        const double v0 = bk * i00, v1 = (bk1 - l10 * v0) * i11;
+        auto rowpiv = [&](auto &q, int r, double &bv, double &vr, double &lr0, double &lr1) {
+            if (r > k + 1) {
+                lr0 = q[k] * i00;
+                lr1 = (q[k + 1] - lr0 * l10) * i11;
+            } else if (r == k + 1) {
+                lr0 = l10;
+                lr1 = l11;
+            } else if (r == k) {
+                lr0 = l00;
+                lr1 = 0.0;
+            } else {
+                lr0 = 0.0;
+                lr1 = 0.0;
+            }
+            q[k] = lr0;
+            q[k + 1] = lr1;
+            if (r >= k) {
+                d2 v;
+                v.x = lr0;
+                v.y = lr1;
+                *reinterpret_cast<d2 *>(Lp + pb2(jp) + 2 * (r - k)) = v;
+            }
+            if (r == k) {
+                d2 v;
+                v.x = i00;
+                v.y = i11;
+                *reinterpret_cast<d2 *>(Lp + PACK2 + k) = v;
+                vr = v0;
+            }
+            if (r == k + 1) vr = v1;
+            if (r > k + 1) bv = fma(-lr1, v1, fma(-lr0, v0, bv));
+        };
+        double la0 = 0.0, la1 = 0.0, lb0, lb1;
+        if constexpr (k < 16) rowpiv(qa, r0, bva, va, la0, la1);
+        rowpiv(qb, r1, bvb, vb, lb0, lb1);
 #pragma unroll
-    for (int c = 0; c < KP; c += 2) {                      // (E x)_r from row r (E symmetric)
-        const d2 e2 = *reinterpret_cast<const d2 *>(Er + c);
-        ex += e2.x * Lp[PACK2 + KP + c];
-        ex += e2.y * Lp[PACK2 + KP + c + 1];
-    }
-    double contrib = xr * (ex - 2.0 * cjr);
+        for (int c = k + 2; c < KP; ++c) {
+            const d2 lc = *reinterpret_cast<const d2 *>(Lp + pb2(jp) + 2 * (c - k));
+            if constexpr (k < 16) {
+                if (c < KH) qa[c < KH ? c : 0] = fma(-la1, lc.y, fma(-la0, lc.x, qa[c < KH ? c : 0]));
+            }
+            qb[c] = fma(-lb1, lc.y, fma(-lb0, lc.x, qb[c]));
+        }
 #pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) contrib += __shfl_xor(contrib, o, 32);
-
-    PHASE(4);
-    // --- psi (dc:150), uses tau of the previous iteration (Q11)
-    double psir = 0.0;
-    if (rv) {
-        const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xr * xr * tr));
-        psir = scale * Gpsi;
+        for (int c = k + 2; c < KP; ++c) {
+            if (k < 16 && c < KH) asm volatile("" : "+v"(qa[c < KH ? c : 0]));
+            asm volatile("" : "+v"(qb[c]));
+        }
+    });
+    // ---- back solve L' x = w, w = v + z (dc:142-144), two rows per step from the bottom
+    double wa = va + z0, wb = vb + z1;
+    double xa = 0.0, xb = 0.0;
+    const int bra = pb2(r0 >> 1) - 2 * (r0 & ~1) + (r0 & 1);   // L[c][r0] at bra + 2c
+    const int brb = pb2(r1 >> 1) - 2 * (r1 & ~1) + (r1 & 1);
+    static_for<KP / 2>([&](auto JC) {
+        constexpr int c = KP - 1 - 2 * decltype(JC)::value;     // pivots c, c-1
+        const double wc = (c >= 16) ? bcast16<(c >= 16 ? c - 16 : 0)>(wb) : bcast16<(c < 16 ? c : 0)>(wa);
+        const double wc1 = (c - 1 >= 16) ? bcast16<(c - 1 >= 16 ? c - 17 : 0)>(wb) : bcast16<(c - 1 < 16 ? c - 1 : 0)>(wa);
+        const d2 dd = *reinterpret_cast<const d2 *>(Lp + PACK2 + c - 1);   // {1/L[c-1][c-1], 1/L[c][c]}
+        const double xc = wc * dd.y;
+        const double lcc1 = Lp[pb2((c - 1) >> 1) + 2 * (c - ((c - 1) & ~1)) + ((c - 1) & 1)];
+        const double xc1 = (wc1 - lcc1 * xc) * dd.x;
+        if constexpr (c >= 16) {
+            if (r1 == c) xb = xc;
+            if (r1 == c - 1) xb = xc1;
+            if (r1 < c - 1) wb = fma(-Lp[brb + 2 * (c - 1)], xc1, fma(-Lp[brb + 2 * c], xc, wb));
+        }
+        if (r0 == c) xa = xc;
+        if (r0 == c - 1) xa = xc1;
+        if (r0 < c - 1) wa = fma(-Lp[bra + 2 * (c - 1)], xc1, fma(-Lp[bra + 2 * c], xc, wa));
+    });
+    if (!rv0) xa = 0.0;
+    if (!rv1) xb = 0.0;
+    // ---- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr  (x through the LDS scratch slots)
+    Lp[PACK2 + KP + r0] = xa;
+    Lp[PACK2 + KP + r1] = xb;
+    double exa = 0.0, exb = 0.0;
+#pragma unroll
+    for (int c = 0; c < KP; c += 2) {
+        const d2 ea = *reinterpret_cast<const d2 *>(Ea + c), eb = *reinterpret_cast<const d2 *>(Eb + c);
+        const d2 xv = *reinterpret_cast<const d2 *>(Lp + PACK2 + KP + c);
+        exa += ea.x * xv.x;
+        exa += ea.y * xv.y;
+        exb += eb.x * xv.x;
+        exb += eb.y * xv.y;
     }
-    PHASE(5);
-
+    double contrib = xa * (exa - 2.0 * c0) + xb * (exb - 2.0 * c1);
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) contrib += __shfl_xor(contrib, o, 16);
+    // ---- psi (dc:150, tau of the previous iteration, Q11) and the outputs
+    double psa = 0.0, psb = 0.0;
+    if (rv0) psa = (1.0 / (d.df * 0.5 + 0.5 * (xa * xa * tr0))) * G0;
+    if (rv1) psb = (1.0 / (d.df * 0.5 + 0.5 * (xb * xb * tr1))) * G1;
     if (valid) {
-        Lam[rowoff + r] = xr;
-        cpart[rowoff + r] = psir * (xr * xr);       // mat = psijh .* Lambda.^2 (dc:156)
-        if (real) psi[rowoff + r] = psir;
-        if (r == 0) {
+        Lam[rowoff + r0] = xa;
+        Lam[rowoff + r1] = xb;
+        cpart[rowoff + r0] = psa * (xa * xa);       // mat = psijh .* Lambda.^2 (dc:156)
+        cpart[rowoff + r1] = psb * (xb * xb);
+        if (rv0) psi[rowoff + r0] = psa;
+        if (rv1) psi[rowoff + r1] = psb;
+        if (l == 0) {
             const double SS = yyj + contrib;
             const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;   // dc:170
             ps[(size_t)m * d.PP + j] = psn;
             omega[(size_t)m * d.PP + j] = 1.0 / psn;            // dc:171 (Q1)
         }
     }
-    PHASE(6);
-    PHASE_END();
 }
 
 // ============================================================================
@@ -822,62 +903,78 @@ __global__ __launch_bounds__(256) void k_save(Dims d, const double *__restrict__
 // k_assemble: Sigma[a][b] += (coef(a,b)/effsamp) sum_kk Lb[a][kk] Lb[b][kk]
 //                            + [a==b] wsum[a]/effsamp                       dc:184-195
 // coef = 1 inside a diagonal shard block (Lambda_r Lambda_r' + Omega_r), rho
-// across blocks (rho Lambda_r Lambda_c').  Lower-triangle 128x128 tiles only;
-// 4 waves in 2x2, each 64x64 = 4x4 tiles of v_mfma_f64_16x16x4; operands
-// streamed from L2 with one chunk (8 k) of register prefetch.
+// across blocks (rho Lambda_r Lambda_c').  Lower-triangle 128x128 tiles only,
+// XCD-contiguous tile order (a block's row panel stays in its XCD's L2).
+// 4 waves in 2x2, each 64x64 = 4x4 tiles of v_mfma_f64_16x16x4.  The k extent
+// (batch x K) runs in chunks of 16 through double-buffered LDS, stored k-major
+// with a 144-double pitch: an MFMA operand read (16 consecutive rows x 4 k) is a
+// conflict-free ds_read_b64, and the next chunk's global loads are in flight
+// during the current chunk's 64 MFMAs per wave.  One barrier per chunk.
 // ============================================================================
-__global__ __launch_bounds__(256) void k_assemble(Dims d, const double *__restrict__ Lb, int LDB,
-                                                  int kext, const double *__restrict__ wsum,
-                                                  double inv_eff, const int2 *__restrict__ tiles,
-                                                  double *__restrict__ Sig) {
-    const int2 T = tiles[blockIdx.x];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+constexpr int AKC = 16, ALD = ASM_TILE + 16;
+
+__global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__restrict__ Lb, int LDB,
+                                                     int kext, const double *__restrict__ wsum,
+                                                     double inv_eff, const int2 *__restrict__ tiles,
+                                                     double *__restrict__ Sig) {
+    __shared__ double As[2][AKC][ALD], Bs[2][AKC][ALD];
+    const int2 T = tiles[xcd_remap(blockIdx.x, gridDim.x)];
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const int r = lane & 15, q = lane >> 4;
-    const int a0 = T.x * ASM_TILE + (wave >> 1) * 64;
-    const int b0 = T.y * ASM_TILE + (wave & 1) * 64;
     const int p = d.p;
-    const double *pa[4], *pb[4];
-    bool va[4], vb[4];
+    const int wa = (wave >> 1) * 64, wb = (wave & 1) * 64;
+    // global -> LDS: thread t stages row (t >> 1) of both panels, k = 8 (t & 1) .. +7
+    const int srow = t >> 1, shalf = t & 1;
+    const int ga = T.x * ASM_TILE + srow, gb = T.y * ASM_TILE + srow;
+    const bool va = ga < p, vb = gb < p;
+    const double *pa = Lb + (size_t)(va ? ga : 0) * LDB + 8 * shalf;
+    const double *pb = Lb + (size_t)(vb ? gb : 0) * LDB + 8 * shalf;
+    const d2 zero2 = {0.0, 0.0};
+    d2 ra[4], rb[4];
+    auto gload = [&](int kc) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int ar = a0 + 16 * u + r, br = b0 + 16 * u + r;
-        va[u] = ar < p;
-        vb[u] = br < p;
-        pa[u] = Lb + (size_t)(va[u] ? ar : 0) * LDB + 2 * q;
-        pb[u] = Lb + (size_t)(vb[u] ? br : 0) * LDB + 2 * q;
-    }
+        for (int i = 0; i < 4; ++i) {
+            ra[i] = va ? *reinterpret_cast<const d2 *>(pa + kc + 2 * i) : zero2;
+            rb[i] = vb ? *reinterpret_cast<const d2 *>(pb + kc + 2 * i) : zero2;
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = 8 * shalf + 2 * i;
+            As[buf][k][srow] = ra[i].x;
+            As[buf][k + 1][srow] = ra[i].y;
+            Bs[buf][k][srow] = rb[i].x;
+            Bs[buf][k + 1][srow] = rb[i].y;
+        }
+    };
     d4 acc[4][4];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int v = 0; v < 4; ++v) acc[u][v] = d4{0.0, 0.0, 0.0, 0.0};
-    const d2 zero2 = {0.0, 0.0};
-    d2 an[4], bn[4];
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int kc = 0, buf = 0; kc < kext; kc += AKC, buf ^= 1) {
+        const bool more = kc + AKC < kext;
+        if (more) gload(kc + AKC);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        an[u] = va[u] ? *reinterpret_cast<const d2 *>(pa[u]) : zero2;
-        bn[u] = vb[u] ? *reinterpret_cast<const d2 *>(pb[u]) : zero2;
-    }
-    for (int kc = 0; kc < kext; kc += 8) {
-        d2 ac[4], bc[4];
+        for (int s4 = 0; s4 < AKC / 4; ++s4) {
+            double a[4], b[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) { ac[u] = an[u]; bc[u] = bn[u]; }
-        if (kc + 8 < kext) {
+            for (int u = 0; u < 4; ++u) a[u] = As[buf][4 * s4 + q][wa + 16 * u + r];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                an[u] = va[u] ? *reinterpret_cast<const d2 *>(pa[u] + kc + 8) : zero2;
-                bn[u] = vb[u] ? *reinterpret_cast<const d2 *>(pb[u] + kc + 8) : zero2;
-            }
+            for (int v = 0; v < 4; ++v) b[v] = Bs[buf][4 * s4 + q][wb + 16 * v + r];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) acc[u][v] = mfma16x16x4(a[u], b[v], acc[u][v]);
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) acc[u][v] = mfma16x16x4(ac[u].x, bc[v].x, acc[u][v]);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) acc[u][v] = mfma16x16x4(ac[u].y, bc[v].y, acc[u][v]);
+        if (more) lstore(buf ^ 1);
+        __syncthreads();
     }
+    const int a0 = T.x * ASM_TILE + wa, b0 = T.y * ASM_TILE + wb;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
 #pragma unroll
@@ -950,74 +1047,74 @@ __host__ __device__ inline DrawSeg draw_segments(const Dims &d) {
 }
 
 __global__ __launch_bounds__(256) void k_draws(Dims d, DrawsDev dr, int64_t iter) {
+    // 32-bit index arithmetic throughout (64-bit division is a long software sequence)
     const DrawSeg sg = draw_segments(d);
-    const int64_t total = sg.nz + sg.nx + sg.nl + sg.gpsi + sg.gps + sg.gdel;
+    const uint32_t snz = (uint32_t)sg.nz, snx = (uint32_t)sg.nx, snl = (uint32_t)sg.nl, sgpsi = (uint32_t)sg.gpsi,
+                   sgps = (uint32_t)sg.gps;
+    const uint32_t total = snz + snx + snl + sgpsi + sgps + (uint32_t)sg.gdel;
     const Rng rng(d.seed);
     const uint32_t it = (uint32_t)iter;
-    const int kp2 = (d.K + 1) / 2;
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        int64_t x = e;
-        if (x < sg.nz) {                                   // dc:104, K x n x g
-            const int64_t pr = x % kp2, rest = x / kp2;
-            const int i = rest % d.n, m = rest / d.n;
-            if (m >= d.G) continue;
-            const int mg = d.shard0 + m;
+    const uint32_t kp2 = (d.K + 1) / 2, n = d.n, P = d.P, K = d.K, G = d.G;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        uint32_t x = e;
+        if (x < snz) {                                     // dc:104, K x n x g
+            const uint32_t pr = x % kp2, rest = x / kp2;
+            const uint32_t i = rest % n, m = rest / n;
+            if (m >= G) continue;
+            const uint32_t mg = d.shard0 + m;
             double n0, n1;
-            rng.normal2(SITE_Z, mg, i, (uint32_t)pr, it, n0, n1);
-            double *o = const_cast<double *>(dr.NZ) + ((size_t)mg * d.n + i) * d.K + 2 * pr;
+            rng.normal2(SITE_Z, mg, i, pr, it, n0, n1);
+            double *o = const_cast<double *>(dr.NZ) + ((size_t)mg * n + i) * K + 2 * pr;
             o[0] = n0;
-            if (2 * pr + 1 < d.K) o[1] = n1;
+            if (2 * pr + 1 < K) o[1] = n1;
             continue;
         }
-        x -= sg.nz;
-        if (x < sg.nx) {                                   // dc:126, K x n
-            const int64_t pr = x % kp2, i = x / kp2;
-            if (i >= d.n) continue;
+        x -= snz;
+        if (x < snx) {                                     // dc:126, K x n
+            const uint32_t pr = x % kp2, i = x / kp2;
+            if (i >= n) continue;
             double n0, n1;
-            rng.normal2(SITE_X, 0, (uint32_t)i, (uint32_t)pr, it, n0, n1);
-            double *o = const_cast<double *>(dr.NX) + (size_t)i * d.K + 2 * pr;
+            rng.normal2(SITE_X, 0, i, pr, it, n0, n1);
+            double *o = const_cast<double *>(dr.NX) + (size_t)i * K + 2 * pr;
             o[0] = n0;
-            if (2 * pr + 1 < d.K) o[1] = n1;
+            if (2 * pr + 1 < K) o[1] = n1;
             continue;
         }
-        x -= sg.nx;
-        if (x < sg.nl) {                                   // dc:142, K x P x g
-            const int64_t pr = x % kp2, rest = x / kp2;
-            const int j = rest % d.P, m = rest / d.P;
-            if (m >= d.G) continue;
-            const int mg = d.shard0 + m;
+        x -= snx;
+        if (x < snl) {                                     // dc:142, K x P x g
+            const uint32_t pr = x % kp2, rest = x / kp2;
+            const uint32_t j = rest % P, m = rest / P;
+            if (m >= G) continue;
+            const uint32_t mg = d.shard0 + m;
             double n0, n1;
-            rng.normal2(SITE_LAMBDA, mg, j, (uint32_t)pr, it, n0, n1);
-            double *o = const_cast<double *>(dr.NL) + ((size_t)mg * d.P + j) * d.K + 2 * pr;
+            rng.normal2(SITE_LAMBDA, mg, j, pr, it, n0, n1);
+            double *o = const_cast<double *>(dr.NL) + ((size_t)mg * P + j) * K + 2 * pr;
             o[0] = n0;
-            if (2 * pr + 1 < d.K) o[1] = n1;
+            if (2 * pr + 1 < K) o[1] = n1;
             continue;
         }
-        x -= sg.nl;
-        if (x < sg.gpsi) {                                 // dc:150, device layout [g][P][K], shape df/2 + 1/2
-            const int k = x % d.K;
-            const int64_t rest = x / d.K;
-            const int j = rest % d.P, m = rest / d.P;
-            if (m >= d.G) continue;
-            const int mg = d.shard0 + m;
-            const_cast<double *>(dr.Gpsi)[((size_t)mg * d.P + j) * d.K + k] =
-                rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, mg, j, k, it);
+        x -= snl;
+        if (x < sgpsi) {                                   // dc:150, device layout [g][P][K], shape df/2 + 1/2
+            const uint32_t k = x % K, rest = x / K;
+            const uint32_t j = rest % P, m = rest / P;
+            if (m >= G) continue;
+            const uint32_t mg = d.shard0 + m;
+            const_cast<double *>(dr.Gpsi)[((size_t)mg * P + j) * K + k] = rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, mg, j, k, it);
             continue;
         }
-        x -= sg.gpsi;
-        if (x < sg.gps) {                                  // dc:170, P x g, shape as + n/2
-            const int j = x % d.P, m = x / d.P;
-            if (m >= d.G) continue;
-            const int mg = d.shard0 + m;
-            const_cast<double *>(dr.Gps)[(size_t)mg * d.P + j] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg, j, 0, it);
+        x -= sgpsi;
+        if (x < sgps) {                                    // dc:170, P x g, shape as + n/2
+            const uint32_t j = x % P, m = x / P;
+            if (m >= G) continue;
+            const uint32_t mg = d.shard0 + m;
+            const_cast<double *>(dr.Gps)[(size_t)mg * P + j] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg, j, 0, it);
             continue;
         }
-        x -= sg.gps;
-        if (x < (int64_t)d.g * d.K) {                      // dc:158,163, K x g, all shards
-            const int h = x % d.K, mg = x / d.K;
-            const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - h);
-            const_cast<double *>(dr.Gdelta)[(size_t)mg * d.K + h] = rng.gamma(shape, SITE_DELTA, mg, 0, h, it);
+        x -= sgps;
+        if (x < (uint32_t)d.g * K) {                       // dc:158,163, K x g, all shards
+            const uint32_t h = x % K, mg = x / K;
+            const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - (int)h);
+            const_cast<double *>(dr.Gdelta)[(size_t)mg * K + h] = rng.gamma(shape, SITE_DELTA, mg, 0, h, it);
         }
     }
 }
@@ -1084,7 +1181,7 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, const double *plam_src, hipStream_t s) {
     if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, plam_src, s);
-    hipLaunchKernelGGL(k_lambda, dim3(cdiv(d.P, 2), d.G), dim3(64), 0, s, d, b.C, b.E, b.yy, tau_cur,
+    hipLaunchKernelGGL(k_lambda, dim3(cdiv(d.P, 4), d.G), dim3(64), 0, s, d, b.C, b.E, b.yy, tau_cur,
                        b.Lam, b.psi, plam_src, b.ps, b.omega, b.cpart, dr, iter);
 }
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s) {

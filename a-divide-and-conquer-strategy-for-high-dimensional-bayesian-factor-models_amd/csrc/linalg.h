@@ -6,6 +6,9 @@
 #include "dcfm_internal.h"
 #include "philox.h"
 
+#include <type_traits>
+#include <utility>
+
 namespace dcfm {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -28,6 +31,26 @@ __device__ __forceinline__ double readsel(double x, int c, bool upper) {
     const double lo = readlane_d(x, c);
     const double hi = readlane_d(x, 32 + c);
     return upper ? hi : lo;
+}
+
+// compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1 (DPP lane
+// selectors and per-step register choices must be constants)
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// value of lane LANE of this lane's 16-lane DPP row (v_mov_b32_dpp row_newbcast)
+template <int LANE>
+__device__ __forceinline__ double bcast16(double v) {
+    static_assert(LANE >= 0 && LANE < 16, "row_newbcast lane");
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x150 + LANE, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x150 + LANE, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
 }
 
 // 1/sqrt(x) to full fp64 precision: hardware estimate + 2 Newton steps
