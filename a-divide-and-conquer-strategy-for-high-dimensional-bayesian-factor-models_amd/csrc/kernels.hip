@@ -811,7 +811,7 @@ __global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict
 // ============================================================================
 
 // lane l < K holds delta_old_l, T_l, G_l, 1/delta_old_l and 1/dref_l; returns delta_new_l
-__device__ double delta_chain(const Dims &d, int l, double T, double G, double idold, double idref) {
+__device__ __forceinline__ double delta_chain(const Dims &d, int l, double T, double G, double idold, double idref) {
     double F = 1.0, dnew = 1.0;
     for (int h = 0; h < d.K; ++h) {
         const double Th = readlane_d(T, h), ih = readlane_d(idref, h);

@@ -19,76 +19,12 @@
 #include "dcfm_internal.h"
 #include "philox.h"
 #include "linalg.h"
+#include "tile_linalg.h"
 
 namespace dcfm {
 namespace wide {
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
-
-// packed lower column-major storage of an N x N matrix: (r, c), r >= c, at cbp(N, c) + r - c
-__device__ __forceinline__ int cbp(int N, int c) { return c * N - (c * (c - 1)) / 2; }
-
-// ----------------------------------------------------------------------------
-// Workgroup (256 threads) Cholesky of a packed SPD matrix in LDS, right-looking,
-// column by column (the K x K systems of dc:100,118 — g+1 per iteration, off the
-// critical path).  On return A holds L (packed) and dinv[k] = 1/L_kk.
-// ----------------------------------------------------------------------------
-__device__ void wg_chol_packed(double *A, double *dinv, int N) {
-    const int t = threadIdx.x, tr = t & 15, tc = t >> 4;
-    for (int k = 0; k < N; ++k) {
-        const int ck = cbp(N, k);
-        const double piv = A[ck];
-        const double ikk = rsqrt_f64(piv);
-        __syncthreads();
-        if (t == 0) {
-            A[ck] = piv * ikk;
-            dinv[k] = ikk;
-        }
-        for (int r = k + 1 + t; r < N; r += 256) A[ck + r - k] *= ikk;
-        __syncthreads();
-        for (int c = k + 1 + tc; c < N; c += 16) {
-            const double lc = A[ck + c - k];
-            const int cc = cbp(N, c);
-            for (int r = c + tr; r < N; r += 16) A[cc + r - c] -= A[ck + r - k] * lc;
-        }
-        __syncthreads();
-    }
-}
-
-// U = L^{-1} (packed, same layout): thread j forward-substitutes column j.
-__device__ void wg_lower_inverse_packed(const double *L, const double *dinv, double *U, int N) {
-    for (int j = threadIdx.x; j < N; j += blockDim.x) {
-        const int cj = cbp(N, j);
-        for (int a = j; a < N; ++a) {
-            double acc = (a == j) ? 1.0 : 0.0;
-            for (int b = j; b < a; ++b) acc -= L[cbp(N, b) + a - b] * U[cj + b - j];
-            U[cj + a - j] = acc * dinv[a];
-        }
-    }
-    __syncthreads();
-}
-
-// T = U U' (symmetric) into packed Tpk, from packed lower U
-__device__ void wg_uut_packed(const double *U, double *Tpk, int N) {
-    const int tot = N * (N + 1) / 2;
-    for (int e = threadIdx.x; e < tot; e += blockDim.x) {
-        // e -> (a, c), a >= c, column-major packed
-        int c = 0;
-        while (cbp(N, c + 1) <= e) ++c;
-        const int a = c + (e - cbp(N, c));
-        double acc = 0.0;
-        for (int b = 0; b <= c; ++b) acc += U[cbp(N, b) + a - b] * U[cbp(N, b) + c - b];
-        Tpk[e] = acc;
-    }
-    __syncthreads();
-}
-
-__device__ __forceinline__ double packed_sym(const double *S, int N, int a, int c) {
-    return a >= c ? S[cbp(N, c) + a - c] : S[cbp(N, a) + c - a];
-}
-__device__ __forceinline__ double packed_low(const double *L, int N, int a, int c) {
-    return a >= c ? L[cbp(N, c) + a - c] : 0.0;
-}
 
 // ============================================================================
 // k_gram: A_m = (w o Lambda_m)' Lambda_m, 32x32 tile (ta, tb) per block; the 4
@@ -143,27 +79,27 @@ __global__ __launch_bounds__(256) void k_gram(Dims d, const double *__restrict__
 //   so the lower factor L = R' is the Cholesky of S[r][c] = Zprec[c][r] (c <= r).
 //   U = L^{-1}, T = U U';  ZM[m] = {M1 = s1r T, -, U, -}: the reference's
 //   R'\(R\bz) + R'\z is T bz + U z (quirk Q2), with bz = s1r (W - sr A X) formed in
-//   k_zdraw from A directly.  Padding (>= K) is 0.
+//   k_zdraw from A directly.  Tiled LDS Cholesky / inverse / U U' (tile_linalg.h).
 // ============================================================================
 template <int KW>
 __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__ A, double *__restrict__ ZM) {
-    constexpr int PK = KW * (KW + 1) / 2;
-    __shared__ double S1[PK], S2[PK], dinv[KW];
-    const int m = blockIdx.x, N = d.K, t = threadIdx.x;
+    constexpr int NB = KW / tile::TS, NT = tile::ntiles(NB);
+    __shared__ double Ts[NT * tile::TSZ], Us[NT * tile::TSZ], dinv[KW];
+    const int m = blockIdx.x, N = d.K, nb = (N + tile::TS - 1) / tile::TS, t = threadIdx.x;
     const double *Am = A + (size_t)m * KW * KW;
-    for (int c = 0; c < N; ++c)
-        for (int r = c + t; r < N; r += 256) S1[cbp(N, c) + r - c] = (r == c ? 1.0 : 0.0) + (1.0 - d.rho) * Am[(size_t)c * KW + r];
-    __syncthreads();
-    wg_chol_packed(S1, dinv, N);
-    wg_lower_inverse_packed(S1, dinv, S2, N);   // U -> S2
-    wg_uut_packed(S2, S1, N);                   // T -> S1 (L no longer needed)
-    double *Zm = ZM + (size_t)m * 4 * KW * KW;
-    for (int e = t; e < KW * KW; e += 256) {
-        const int a = e / KW, c = e % KW;
-        const bool in = a < N && c < N;
-        Zm[e] = in ? d.s1r * packed_sym(S1, N, a, c) : 0.0;
-        Zm[(size_t)2 * KW * KW + e] = in ? packed_low(S2, N, a, c) : 0.0;
+    for (int e = t; e < tile::ntiles(nb) * tile::TS * tile::TS; e += 256) {
+        int I, J;
+        tile::tri_pair(e >> 8, I, J);
+        const int r = (e >> 4) & 15, c = e & 15, R = 16 * I + r, Cc = 16 * J + c;
+        const double v = (R < N && Cc < N) ? (R == Cc ? 1.0 : 0.0) + (1.0 - d.rho) * Am[(size_t)Cc * KW + R]
+                                           : (R == Cc ? 1.0 : 0.0);
+        Ts[tile::tix(I, J) * tile::TSZ + c * tile::TLD + r] = v;
     }
+    __syncthreads();
+    tile::potrf(Ts, dinv, nb);
+    tile::trtri(Ts, dinv, Us, nb);
+    double *Zm = ZM + (size_t)m * 4 * KW * KW;
+    tile::uut_store(Us, nb, N, d.s1r, Zm, KW, Zm + (size_t)2 * KW * KW);
 }
 
 // ============================================================================
@@ -172,26 +108,26 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 // ============================================================================
 template <int KW>
 __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict__ xa_all, double *__restrict__ XM) {
-    constexpr int PK = KW * (KW + 1) / 2;
-    __shared__ double S1[PK], S2[PK], dinv[KW];
-    const int N = d.K, t = threadIdx.x;
-    for (int c = 0; c < N; ++c)
-        for (int r = c + t; r < N; r += 256) {
-            const size_t e = (size_t)c * KW + r;   // upper triangle: Xprec[c][r]
-            double v = xa_all[e];
-            for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * KW * KW + e];
-            S1[cbp(N, c) + r - c] = (r == c ? (double)d.g : 0.0) + d.rho * v;
+    constexpr int NB = KW / tile::TS, NT = tile::ntiles(NB);
+    __shared__ double Ts[NT * tile::TSZ], Us[NT * tile::TSZ], dinv[KW];
+    const int N = d.K, nb = (N + tile::TS - 1) / tile::TS, t = threadIdx.x;
+    for (int e = t; e < tile::ntiles(nb) * tile::TS * tile::TS; e += 256) {
+        int I, J;
+        tile::tri_pair(e >> 8, I, J);
+        const int r = (e >> 4) & 15, c = e & 15, R = 16 * I + r, Cc = 16 * J + c;
+        double v = (R == Cc) ? 1.0 : 0.0;
+        if (R < N && Cc < N) {
+            const size_t o = (size_t)Cc * KW + R;   // upper triangle: Xprec[c][r]
+            double sa = xa_all[o];
+            for (int rk = 1; rk < d.nranks; ++rk) sa += xa_all[(size_t)rk * KW * KW + o];
+            v = (R == Cc ? (double)d.g : 0.0) + d.rho * sa;
         }
-    __syncthreads();
-    wg_chol_packed(S1, dinv, N);
-    wg_lower_inverse_packed(S1, dinv, S2, N);
-    wg_uut_packed(S2, S1, N);
-    for (int e = t; e < KW * KW; e += 256) {
-        const int a = e / KW, c = e % KW;
-        const bool in = a < N && c < N;
-        XM[e] = in ? d.sr * packed_sym(S1, N, a, c) : 0.0;
-        XM[(size_t)KW * KW + e] = in ? packed_low(S2, N, a, c) : 0.0;
+        Ts[tile::tix(I, J) * tile::TSZ + c * tile::TLD + r] = v;
     }
+    __syncthreads();
+    tile::potrf(Ts, dinv, nb);
+    tile::trtri(Ts, dinv, Us, nb);
+    tile::uut_store(Us, nb, N, d.sr, XM, KW, XM + (size_t)KW * KW);
 }
 
 // standard normals eps[i][kk], eps[i][kk+1] of a Z / X row (kk even)       dc:104,126
@@ -630,7 +566,7 @@ __device__ __forceinline__ void scan_prod_nv(double (&v)[NV], int l) {
     if (NV == 2) v[NV - 1] = wave_scan_prod(v[NV - 1], l) * readlane_d(v[0], 63);
 }
 template <int NV>
-__device__ void delta_chain_nv(const Dims &d, int l, const double (&T)[NV], const double (&G)[NV],
+__device__ __forceinline__ void delta_chain_nv(const Dims &d, int l, const double (&T)[NV], const double (&G)[NV],
                                const double (&idold)[NV], const double (&idref)[NV], double (&dnew)[NV]) {
     double F = 1.0;
 #pragma unroll

@@ -186,17 +186,21 @@ def main():
     d = {"n": n, "P": P, "K": K, "G": gl, "p": p, "nranks": world}
     kern = {}
     roof = None
-    def work_of(name, cnt, saved):
+    def work_of(name, cnt, saved, iters):
+        """Algorithmic (flops, bytes, bound) per launch: per-iteration work spread over the
+        launches of one iteration (the Y-pass / row kernels run as two shard groups)."""
         if name == "k_assemble":
             return algorithmic_work(name, d, saved / max(cnt, 1))
-        return algorithmic_work(name, d, 0)
+        fl, by, bound = algorithmic_work(name, d, 0)
+        per_iter = max(cnt, 1) / max(iters, 1)
+        return fl / per_iter, by / per_iter, bound
 
     if stats:
         for name, (ms, cnt) in stats.items():
             if cnt == 0:
                 continue
             avg_s = ms / cnt / 1e3
-            fl, by, bound = work_of(name, cnt, saved_prof)
+            fl, by, bound = work_of(name, cnt, saved_prof, n_prof)
             kern[name] = {"ms_total": round(ms, 4), "launches": int(cnt), "avg_us": round(avg_s * 1e6, 2),
                           "gflops_per_launch": round(fl / 1e9, 4), "mb_per_launch": round(by / 1e6, 3),
                           "tflops": round(fl / avg_s / 1e12, 3) if avg_s > 0 else None,
@@ -204,7 +208,7 @@ def main():
     if live and live[1]:
         ms, cnt = live
         avg_s = ms / cnt / 1e3
-        fl, by, bound = work_of(dominant, cnt, saved_in_region)
+        fl, by, bound = work_of(dominant, cnt, saved_in_region, args.steps)
         if bound == "mfma":
             ach, peak, unit = fl / avg_s / 1e12, FP64_MFMA_PEAK_TFLOPS, "TFLOP/s"
         else:
