@@ -51,11 +51,23 @@ def algorithmic_work(kname, d, n_launch_samples):
         return 2.0 * G * n * (P + K) * K, 8.0 * (G * n * P + n * K + G * n * K + G * P * K), "hbm"
     if kname == "k_assemble":  # lower triangle of sum_s coef.(L_s L_s') over the batch
         return float(p) * (p + 1) * n_launch_samples * K / nr, 16.0 * p * (p + 1) / 2 / nr, "mfma"
-    if kname == "k_lambda":
-        return G * P * (K ** 3 / 3.0 + 6.0 * K * K), 8.0 * G * P * (4 * K + 4), "mfma"
+    if kname == "k_lambda":   # per row: read C, psi, NL, Gpsi (K each), ps, yy, Gps; write Lam, psi, cpart, ps, omega
+        return G * P * (K ** 3 / 3.0 + 6.0 * K * K), 8.0 * G * P * (7 * K + 5), "mfma"
     if kname == "k_zdraw":
         return G * n * (4.0 * K * K + 2.0 * K * K), 8.0 * G * n * 4 * K, "hbm"
     return 0.0, 0.0, "hbm"
+
+
+def pmc_traffic(kernel, workload_tag):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the
+    same workload (profiles/r01_<tag>_pmc.json, written by tools/pmc_summary.py from
+    separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 note of
+    the MI355X microarchitecture guide).  None when no summary matches."""
+    f = ROOT / "profiles" / f"r01_{workload_tag}_pmc.json"
+    if not f.exists():
+        return None, None
+    k = json.load(open(f))["kernels"].get(kernel, {})
+    return k.get("hbm_bytes_per_dispatch"), str(f.relative_to(ROOT))
 
 
 def cpu_baseline_run(n, p, g, K, rho, steps=5, thin=5):
@@ -213,8 +225,13 @@ def main():
             ach, peak, unit = fl / avg_s / 1e12, FP64_MFMA_PEAK_TFLOPS, "TFLOP/s"
         else:
             ach, peak, unit = by / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+        tag = {(64, 312, 1000, 30): "c3", (8, 1250, 2000, 100): "c4"}.get((g, P, n, K))
+        traffic, tsrc = pmc_traffic(dominant, tag) if tag else (None, None)
         roof = {"kernel": dominant, "bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": unit,
-                "frac": round(ach / peak, 4), "traffic": None, "avg_us": round(avg_s * 1e6, 2),
+                "frac": round(ach / peak, 4),
+                "traffic": round(traffic) if traffic is not None else None,
+                "traffic_unit": "bytes/launch", "traffic_source": tsrc,
+                "algorithmic_bytes": round(by), "avg_us": round(avg_s * 1e6, 2),
                 "launches": int(cnt),
                 "note": "achieved = algorithmic work per launch / mean HIP-event duration of this kernel, "
                         "events recorded around it alone inside the timed region"}

@@ -1,0 +1,65 @@
+"""Summarise rocprofv3 PMC passes per kernel (tools/profile_round.sh output).
+
+HBM bytes per dispatch: FETCH_SIZE (KiB) x 1024 x 2 — the gfx950 correction of
+/opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts exactly
+half of the bytes of a wide (16 B/lane) coalesced read — and WRITE_SIZE (KiB) x
+1024 as is.  Both include Infinity-Cache hits (memory-side requests), so on a
+working set that stays MALL-resident they are an upper bound on HBM traffic.
+fp64 MFMA flops: SQ_INSTS_VALU_MFMA_MOPS_F64 x 512.
+Usage: python tools/pmc_summary.py gpurun_out/prof_TAG > profiles/..._pmc.json
+"""
+import csv
+import glob
+import json
+import re
+import sys
+from collections import defaultdict
+
+
+def load(dirpat):
+    rows = []
+    for f in glob.glob(f"{dirpat}/**/*counter_collection.csv", recursive=True):
+        rows += list(csv.DictReader(open(f)))
+    return rows
+
+
+def short(name):
+    m = re.search(r"(k_\w+)", name)
+    return m.group(1) if m else name[:40]
+
+
+def per_kernel(rows, counter):
+    acc = defaultdict(lambda: defaultdict(float))
+    for r in rows:
+        if r.get("Counter_Name") != counter:
+            continue
+        k = short(r["Kernel_Name"])
+        acc[k][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: (sum(v.values()) / len(v), len(v)) for k, v in acc.items()}
+
+
+base = sys.argv[1]
+fetch = per_kernel(load(base + "_fetch"), "FETCH_SIZE")
+write = per_kernel(load(base + "_write"), "WRITE_SIZE")
+mrows = load(base + "_mfma")
+mops = per_kernel(mrows, "SQ_INSTS_VALU_MFMA_MOPS_F64")
+busy = per_kernel(mrows, "SQ_VALU_MFMA_BUSY_CYCLES")
+gui = per_kernel(mrows, "GRBM_GUI_ACTIVE")
+out = {}
+for k in sorted(set(fetch) | set(write) | set(mops)):
+    e = {}
+    if k in fetch:
+        e["fetch_bytes_per_dispatch"] = fetch[k][0] * 1024 * 2
+        e["dispatches"] = fetch[k][1]
+    if k in write:
+        e["write_bytes_per_dispatch"] = write[k][0] * 1024
+    if "fetch_bytes_per_dispatch" in e and "write_bytes_per_dispatch" in e:
+        e["hbm_bytes_per_dispatch"] = e["fetch_bytes_per_dispatch"] + e["write_bytes_per_dispatch"]
+    if k in mops:
+        e["mfma_f64_flops_per_dispatch"] = mops[k][0] * 512
+    if k in busy and k in gui and gui[k][0] > 0:
+        # MfmaUtil (rocprofv3 derived): busy cycles summed over SIMDs / (GUI_ACTIVE x SIMDs)
+        e["mfma_busy_frac"] = busy[k][0] / (gui[k][0] * 1024)
+    out[k] = e
+json.dump({"source": base, "kernels": out}, sys.stdout, indent=1)
+print()
