@@ -690,33 +690,45 @@ int dcfm_synchronize(dcfm_handle *h) {
 
 int64_t dcfm_saved_samples(const dcfm_handle *h) { return h ? h->saved : -1; }
 
-int dcfm_get_sigma(dcfm_handle *h, double *out) {
+int dcfm_get_sigma_cols(dcfm_handle *h, int64_t col0, int64_t ncols, double *out) {
     if (!h || !out) return fail(h, DCFM_ERR_INVALID, "null argument");
     Dims &d = h->d;
+    if (col0 < 0 || ncols < 0 || col0 + ncols > d.p)
+        return fail(h, DCFM_ERR_INVALID, "columns [%lld, %lld) outside 0..p = %d", (long long)col0,
+                    (long long)(col0 + ncols), d.p);
+    if (ncols == 0) return DCFM_OK;
     HIPC(h, hipSetDevice(h->cfg.device));
-    const size_t pp = (size_t)d.p * d.p;
-    double *tmp = nullptr;
-    void *q = nullptr;
     sync_all(h);
-    HIPC(h, hipMalloc(&q, pp * sizeof(double)));
-    tmp = static_cast<double *>(q);
+    const size_t n = (size_t)ncols * d.p;
+    void *q = nullptr;
+    HIPC(h, hipMalloc(&q, n * sizeof(double)));
+    double *tmp = static_cast<double *>(q);
     int rc = DCFM_OK;
-    if (d.nranks > 1) {
-        ncclResult_t r = ncclAllReduce(h->b.Sigma, tmp, pp, ncclDouble, ncclSum, h->comm_asm, h->stream);
+    launch_sigma_cols(h->b.Sigma, d.p, (int)col0, (int)ncols, tmp, h->stream);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "sigma_cols: %s", hipGetErrorString(e));
+    if (rc == DCFM_OK && d.nranks > 1) {   // each element is owned by exactly one rank: the sum is exact
+        ncclResult_t r = ncclAllReduce(tmp, tmp, n, ncclDouble, ncclSum, h->comm_asm, h->stream);
         if (r != ncclSuccess) rc = fail(h, DCFM_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
-    } else {
-        hipError_t e = hipMemcpyAsync(tmp, h->b.Sigma, pp * sizeof(double), hipMemcpyDeviceToDevice, h->stream);
-        if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "hipMemcpyAsync: %s", hipGetErrorString(e));
     }
     if (rc == DCFM_OK) {
-        launch_mirror(tmp, d.p, h->stream);
-        hipError_t e = hipGetLastError();
-        if (e == hipSuccess) e = hipMemcpyAsync(out, tmp, pp * sizeof(double), hipMemcpyDeviceToHost, h->stream);
+        e = hipMemcpyAsync(out, tmp, n * sizeof(double), hipMemcpyDeviceToHost, h->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-        if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "get_sigma: %s", hipGetErrorString(e));
+        if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "get_sigma_cols: %s", hipGetErrorString(e));
     }
     (void)hipFree(tmp);
     return rc;
+}
+
+int dcfm_get_sigma(dcfm_handle *h, double *out) {
+    if (!h || !out) return fail(h, DCFM_ERR_INVALID, "null argument");
+    const int64_t p = h->d.p;
+    const int64_t chunk = std::max<int64_t>(32, std::min<int64_t>(p, ((int64_t)1 << 29) / p));   // <= 4 GiB stripes
+    for (int64_t c = 0; c < p; c += chunk) {
+        const int rc = dcfm_get_sigma_cols(h, c, std::min(chunk, p - c), out + (size_t)c * p);
+        if (rc) return rc;
+    }
+    return DCFM_OK;
 }
 
 int dcfm_set_profiling(dcfm_handle *h, int enable) {

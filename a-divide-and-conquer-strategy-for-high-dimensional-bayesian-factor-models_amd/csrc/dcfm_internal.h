@@ -78,7 +78,7 @@ void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
 void launch_save(const Dims &d, const Bufs &b, double *Lb, double *wsum, int slot, hipStream_t s);
 void launch_assemble(const Dims &d, const Bufs &b, const double *Lb, const double *wsum, int kext,
                      double inv_eff, hipStream_t s);
-void launch_mirror(double *S, int p, hipStream_t s);
+void launch_sigma_cols(const double *S, int p, int c0, int nc, double *out, hipStream_t s);
 void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s);
 void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,

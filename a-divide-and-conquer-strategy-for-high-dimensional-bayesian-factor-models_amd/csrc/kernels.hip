@@ -995,20 +995,30 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
     }
 }
 
-// Sigma[a][b] = Sigma[b][a] for a < b (lower -> upper), 32x32 LDS tiles
-__global__ __launch_bounds__(256) void k_mirror(double *__restrict__ S, int p) {
-    __shared__ double tile[32][33];
-    const int tr = blockIdx.y, tc = blockIdx.x;   // destination tile (upper: tr <= tc)
-    if (tr > tc) return;
+// Column stripe of the symmetric Sigmaout from the lower-triangle accumulator:
+// out[(c - c0) * p + r] = Sigma(r, c) for c in [c0, c0 + nc) — i.e. columns c0.. of
+// the MATLAB column-major p x p array, contiguous (dc:194-195 output, Q9: the
+// symmetrisation is this mirror).  32x32 tiles: Sigma(r, c) = S[r][c] for r >= c
+// (read along c, transposed through LDS), S[c][r] for r < c (read along r).
+__global__ __launch_bounds__(256) void k_sigma_cols(const double *__restrict__ S, int p, int c0, int nc,
+                                                    double *__restrict__ out) {
+    __shared__ double lo[32][33];
+    const int r0 = blockIdx.x * 32, cb = c0 + blockIdx.y * 32;
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-    for (int yy = ty; yy < 32; yy += 8) {
-        const int sr = tc * 32 + yy, sc = tr * 32 + tx;   // source lower tile (tc, tr)
-        tile[yy][tx] = (sr < p && sc < p) ? S[(size_t)sr * p + sc] : 0.0;
+    const bool need_lo = r0 + 31 >= cb;            // some r >= c in the tile
+    const bool need_up = r0 < cb + 31;             // some r < c
+    if (need_lo) {
+        for (int yy = ty; yy < 32; yy += 8) {      // rows r = r0 + yy, columns c = cb + tx
+            const int r = r0 + yy, c = cb + tx;
+            lo[yy][tx] = (r < p && c < c0 + nc && r >= c) ? S[(size_t)r * p + c] : 0.0;
+        }
     }
     __syncthreads();
-    for (int yy = ty; yy < 32; yy += 8) {
-        const int dr = tr * 32 + yy, dc = tc * 32 + tx;
-        if (dr < p && dc < p && dr < dc) S[(size_t)dr * p + dc] = tile[tx][yy];
+    for (int yy = ty; yy < 32; yy += 8) {          // output column c = cb + yy, rows r = r0 + tx
+        const int c = cb + yy, r = r0 + tx;
+        if (c >= c0 + nc || r >= p) continue;
+        const double v = (r >= c) ? lo[tx][yy] : (need_up ? S[(size_t)c * p + r] : 0.0);
+        out[(size_t)(c - c0) * p + r] = v;
     }
 }
 
@@ -1210,9 +1220,9 @@ void launch_assemble(const Dims &d, const Bufs &b, const double *Lb, const doubl
     hipLaunchKernelGGL(k_assemble, dim3(b.ntiles), dim3(256), 0, s, d, Lb, b.LDB, kext, wsum, inv_eff,
                        b.tiles, b.Sigma);
 }
-void launch_mirror(double *S, int p, hipStream_t s) {
-    const int nt = cdiv(p, 32);
-    hipLaunchKernelGGL(k_mirror, dim3(nt, nt), dim3(256), 0, s, S, p);
+void launch_sigma_cols(const double *S, int p, int c0, int nc, double *out, hipStream_t s) {
+    if (nc <= 0) return;
+    hipLaunchKernelGGL(k_sigma_cols, dim3(cdiv(p, 32), cdiv(nc, 32)), dim3(256), 0, s, S, p, c0, nc, out);
 }
 void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s) {
     const size_t total = (size_t)d.G * d.NP * d.kp;

@@ -151,6 +151,13 @@ class Sampler:
         self._check(self.lib.dcfm_get_sigma(self.h, _ptr(S)))
         return S
 
+    def get_sigma_cols(self, col0: int, ncols: int) -> np.ndarray:
+        """Sigmaout(:, col0 : col0+ncols) as a p x ncols Fortran array (collective if nranks > 1)."""
+        p = self.P * self.g
+        S = np.zeros((p, int(ncols)), dtype=np.float64, order="F")
+        self._check(self.lib.dcfm_get_sigma_cols(self.h, int(col0), int(ncols), _ptr(S)))
+        return S
+
     def saved_samples(self) -> int:
         return int(self.lib.dcfm_saved_samples(self.h))
 

@@ -130,6 +130,11 @@ int  dcfm_get_state(dcfm_handle *h, dcfm_state_view *out);
  * standardised coordinates (dc:186-195, quirk Q7).  Collective when
  * nranks > 1: every rank must call it; every rank receives the full matrix. */
 int  dcfm_get_sigma(dcfm_handle *h, double *out);
+/* Columns col0 .. col0+ncols-1 of Sigmaout: p x ncols column-major, i.e. exactly
+ * out = Sigmaout(:, col0+1 : col0+ncols) — a contiguous chunk of the MATLAB array,
+ * so a caller can fill a p x p result stripe by stripe (config c5: 80 GB) with
+ * device scratch of only p x ncols.  Collective when nranks > 1. */
+int  dcfm_get_sigma_cols(dcfm_handle *h, int64_t col0, int64_t ncols, double *out);
 int64_t dcfm_saved_samples(const dcfm_handle *h);
 
 /* ---- measurement --------------------------------------------------------- */
