@@ -598,8 +598,8 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     }
     HIPC(h, hipSetDevice(h->cfg.device));
     hipStream_t s = h->stream, ss = h->side;
-    const size_t KP = d.kp;
-    const size_t nkg = (size_t)d.g * KP;
+    const size_t KW = d.kp;
+    const size_t nkg = (size_t)d.g * KW;
     // draws of iteration `it`: the injected buffers, or generated slot it % 3
     auto ensure_draws = [&](int64_t it) {
         if (d.inject) return;
@@ -623,7 +623,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         { KTimer t(h, DCFM_K_XCHOL, ss); launch_asum(d, b, ss); }
         if (d.nranks > 1) {
             KTimer t(h, DCFM_K_COMM, ss);
-            NCCLC(h, ncclAllGather(b.xa, b.xa_all, (size_t)KP * KP, ncclDouble, h->comm_side, ss));
+            NCCLC(h, ncclAllGather(b.xa, b.xa_all, KW * KW, ncclDouble, h->comm_side, ss));
         }
         { KTimer t(h, DCFM_K_XCHOL, ss); launch_xchol(d, b, ss); }
         HIPC(h, hipEventRecord(h->e_xchol, ss));
@@ -635,7 +635,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         { KTimer t(h, DCFM_K_XRED, s);   launch_xred(d, b, s); }
         if (d.nranks > 1) {
             KTimer t(h, DCFM_K_COMM, s);
-            NCCLC(h, ncclAllGather(b.xin, b.xall, (size_t)d.NP * KP, ncclDouble, h->comm, s));
+            NCCLC(h, ncclAllGather(b.xin, b.xall, (size_t)d.NP * KW, ncclDouble, h->comm, s));
         }
         HIPC(h, hipStreamWaitEvent(s, h->e_xchol, 0));
         { KTimer t(h, DCFM_K_XDRAW, s);  launch_xdraw(d, b, dr, it, s); }
@@ -649,7 +649,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         { KTimer t(h, DCFM_K_COLSUM, s); launch_colsum(d, b, s); }
         if (d.nranks > 1) {
             KTimer t(h, DCFM_K_COMM, s);
-            NCCLC(h, ncclAllGather(b.sloc, b.sall, (size_t)d.G * KP, ncclDouble, h->comm, s));
+            NCCLC(h, ncclAllGather(b.sloc, b.sall, (size_t)d.G * KW, ncclDouble, h->comm, s));
         }
         {
             KTimer t(h, DCFM_K_DELTA, s);

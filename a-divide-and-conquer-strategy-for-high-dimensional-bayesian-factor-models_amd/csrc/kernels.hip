@@ -119,25 +119,24 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
     __syncthreads();
     lower_inverse2(Lp, part[1], t);                                 // U -> part[1]
     __syncthreads();
+    {   // T = U U' (fp64 MFMA, one 16x16 tile per wave) -> part[2]; M1 = s1r T; U
+        const int ti = wave >> 1, tj = wave & 1, j = lane & 15, q = lane >> 4;
+        const d4 T = mfma_tile32<true>(part[1], part[1], ti, tj, lane);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {                                   // T = U U' -> part[2]
-        const int e = t + 256 * u, a = e / KP, c = e % KP;
-        double acc = 0.0;
-#pragma unroll
-        for (int b = 0; b < KP; ++b) acc += part[1][a][b] * part[1][c][b];
-        part[2][a][c] = acc;
-        Zm[e] = d.s1r * acc;                                        // M1
-        Zm[2 * KP * KP + e] = part[1][a][c];                        // U
+        for (int g = 0; g < 4; ++g) {
+            const int a = 16 * ti + q + 4 * g, c = 16 * tj + j;
+            part[2][a][c] = T[g];
+            Zm[a * KP + c] = d.s1r * T[g];                          // M1
+            Zm[2 * KP * KP + a * KP + c] = part[1][a][c];           // U
+        }
     }
     __syncthreads();
-    const double s2 = -d.s1r * d.sr;
+    {   // M2 = -s1r sr T A (fp64 MFMA)
+        const int ti = wave >> 1, tj = wave & 1, j = lane & 15, q = lane >> 4;
+        const d4 M = mfma_tile32<false>(part[2], part[0], ti, tj, lane);
+        const double s2 = -d.s1r * d.sr;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {                                   // M2 = -s1r sr T A
-        const int e = t + 256 * u, a = e / KP, c = e % KP;
-        double acc = 0.0;
-#pragma unroll
-        for (int b = 0; b < KP; ++b) acc += part[2][a][b] * part[0][b][c];
-        Zm[KP * KP + e] = s2 * acc;
+        for (int g = 0; g < 4; ++g) Zm[KP * KP + (16 * ti + q + 4 * g) * KP + 16 * tj + j] = s2 * M[g];
     }
 }
 
@@ -345,21 +344,21 @@ __global__ __launch_bounds__(256) void k_asum(Dims d, const double *__restrict__
 
 // ============================================================================
 // k_xchol: Xprec = g*I + rho*sum A (dc:117) and Rx = cholcov(Xprec) (dc:118), on the
-// side stream.  Sums the per-rank sums xa_all in rank order (nranks == 1: xa itself)
-// and writes the X-draw operators XM = {Tx = sqrt(rho) Ux Ux', Ux = Rx^{-T}}.
+// side stream.  Sums the per-rank sums xa_all (k_asum, all-gathered) in rank order
+// and writes the X-draw operators XM = {Tx = sqrt(rho) Ux Ux', Ux = Rx^{-T}} (Tx by MFMA).
 // ============================================================================
-__global__ __launch_bounds__(64) void k_xchol(Dims d, const double *__restrict__ xa_all,
-                                              double *__restrict__ XM) {
+__global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict__ xa_all,
+                                               double *__restrict__ XM) {
     __shared__ __attribute__((aligned(16))) double Lp[P2STRIDE];
     __shared__ double As[KP][KP + 1], Us[KP][KP + 1];
-    const int lane = threadIdx.x;
-    for (int e = lane; e < KP * KP; e += 64) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    for (int e = t; e < KP * KP; e += 256) {
         double v = xa_all[e];
         for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * KP * KP + e];
         As[e / KP][e % KP] = v;
     }
     __syncthreads();
-    {
+    if (wave == 0) {
         const int rr = lane & 31;
         double qq[KP];
 #pragma unroll
@@ -369,16 +368,16 @@ __global__ __launch_bounds__(64) void k_xchol(Dims d, const double *__restrict__
         chol2_rows<false>(qq, Lp, rr, lane >= 32, 0.0, vr);
     }
     __syncthreads();
-    lower_inverse2(Lp, Us, lane);          // Ux = Lx^{-1} = Rx^{-T}
+    lower_inverse2(Lp, Us, t);             // Ux = Lx^{-1} = Rx^{-T}
     __syncthreads();
     // X = Rx^{-T}(Rx^{-1} sqrt(rho) S + eps) = Tx S + Ux eps,  Tx = sqrt(rho) Ux Ux'
-    for (int e = lane; e < KP * KP; e += 64) {
-        const int a = e / KP, c = e % KP;
-        double acc = 0.0;
+    const int ti = wave >> 1, tj = wave & 1, j = lane & 15, q = lane >> 4;
+    const d4 T = mfma_tile32<true>(Us, Us, ti, tj, lane);
 #pragma unroll
-        for (int b = 0; b < KP; ++b) acc += Us[a][b] * Us[c][b];
-        XM[e] = d.sr * acc;
-        XM[KP * KP + e] = Us[a][c];
+    for (int g = 0; g < 4; ++g) {
+        const int a = 16 * ti + q + 4 * g, c = 16 * tj + j;
+        XM[a * KP + c] = d.sr * T[g];
+        XM[KP * KP + a * KP + c] = Us[a][c];
     }
 }
 
@@ -1174,7 +1173,7 @@ void launch_asum(const Dims &d, const Bufs &b, hipStream_t s) {
 }
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
     if (d.kp != KP) return wide::launch_xchol(d, b, s);
-    hipLaunchKernelGGL(k_xchol, dim3(1), dim3(64), 0, s, d, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
+    hipLaunchKernelGGL(k_xchol, dim3(1), dim3(256), 0, s, d, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
 }
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return wide::launch_xdraw(d, b, dr, iter, s);

@@ -260,6 +260,24 @@ __device__ __forceinline__ void chol2_rows(double (&q)[KP], double *P, int r, bo
     }
 }
 
+// One 16x16 tile of a 32x32 product in LDS, fp64 MFMA (whole wave, 8 k-steps):
+//   NT: C = A B'  (C[a][c] = sum_b A[a][b] B[c][b]);   NN: C = A B (B[b][c]).
+// Tile (ti, tj); returns the C/D fragment: lane (j = lane&15, q = lane>>4) holds
+// C[16 ti + q + 4 g][16 tj + j], g = 0..3.
+template <bool NT>
+__device__ __forceinline__ d4 mfma_tile32(const double (*A)[KP + 1], const double (*B)[KP + 1], int ti, int tj,
+                                          int lane) {
+    const int i = lane & 15, k = lane >> 4;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < KP / 4; ++s) {
+        const double a = A[16 * ti + i][4 * s + k];
+        const double b = NT ? B[16 * tj + i][4 * s + k] : B[4 * s + k][16 * tj + i];
+        acc = mfma16x16x4(a, b, acc);
+    }
+    return acc;
+}
+
 // U = L^{-1} from the pair-packed image P of chol2_rows: lane j (threads 0..31)
 // forward-substitutes column j; result in Us[a][j].
 __device__ __forceinline__ void lower_inverse2(const double *P, double (*Us)[KP + 1], int t) {
