@@ -30,12 +30,13 @@ struct dcfm_handle {
     Bufs b{};
     DrawsDev dr{};
     hipStream_t stream = nullptr;     // main: the sweep chain
-    hipStream_t side = nullptr;       // k_prep + k_xchol, overlapping k_wpass
+    hipStream_t side = nullptr;       // k_prep + k_xchol, overlapping k_wpass (unfused paths)
+    hipStream_t sdraw = nullptr;      // on-device Philox variates, a batch ahead of the sweep
     hipStream_t sasm = nullptr;       // covariance assembly, overlapping later iterations
     ncclComm_t comm = nullptr, comm_side = nullptr, comm_asm = nullptr;
     bool comm_ok = false;
     hipEvent_t e_lam = nullptr, e_prep = nullptr, e_xchol = nullptr, e_batch = nullptr,
-               e_free[2] = {nullptr, nullptr};
+               e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
     bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
@@ -47,11 +48,15 @@ struct dcfm_handle {
     std::string err;
     std::vector<void *> allocs;
     double *draws_mem = nullptr;
-    // on-device Philox draws (no INJECT): three iteration slots, generated one
-    // iteration ahead on the side stream; a slot is valid for the iteration it was
-    // generated for whatever the state (the stream is counter-based)
-    DrawsDev gen[3] = {};
-    int64_t gen_iter[3] = {-1, -1, -1};
+    // on-device Philox draws (no INJECT): two slots of DB iterations, the next batch
+    // generated on sdraw while the sweep consumes the current one, so the main stream
+    // waits on an event once per batch.  A slot is valid for the iterations it was
+    // generated for whatever the state (the stream is counter-based).
+    DrawsDev gen[2] = {};
+    int64_t gen_first[2] = {-1, -1}, gen_n[2] = {0, 0};
+    bool used_pending[2] = {false, false};   // e_used[slot] recorded after the slot's last consumer
+    int DB = 1;                              // iterations per draws batch
+    size_t draw_iter_sz[6] = {};             // per-iteration doubles of NZ, NX, NL, Gpsi, Gdelta, Gps
     bool prof = false;
     uint32_t prof_mask = 0;       // kernel ids (bit DCFM_K_*) timed with events
     std::vector<ProfRec> recs;
@@ -141,6 +146,7 @@ struct KTimer {
 static void sync_all(dcfm_handle *h) {
     (void)hipStreamSynchronize(h->stream);
     if (h->side) (void)hipStreamSynchronize(h->side);
+    if (h->sdraw) (void)hipStreamSynchronize(h->sdraw);
     if (h->sasm) (void)hipStreamSynchronize(h->sasm);
 }
 
@@ -203,9 +209,10 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     {   // DCFM_SERIALIZE=1: one stream for everything (isolated per-kernel timings)
         const char *ser = std::getenv("DCFM_SERIALIZE");
         if (ser && ser[0] == '1') {
-            h->side = h->sasm = h->stream;
+            h->side = h->sasm = h->sdraw = h->stream;
         } else {
             HIPC(h, hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+            HIPC(h, hipStreamCreateWithFlags(&h->sdraw, hipStreamNonBlocking));
             HIPC(h, hipStreamCreateWithFlags(&h->sasm, hipStreamNonBlocking));
         }
     }
@@ -215,6 +222,10 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     HIPC(h, hipEventCreateWithFlags(&h->e_batch, hipEventDisableTiming));
     HIPC(h, hipEventCreateWithFlags(&h->e_free[0], hipEventDisableTiming));
     HIPC(h, hipEventCreateWithFlags(&h->e_free[1], hipEventDisableTiming));
+    for (int sl = 0; sl < 2; ++sl) {
+        HIPC(h, hipEventCreateWithFlags(&h->e_drawn[sl], hipEventDisableTiming));
+        HIPC(h, hipEventCreateWithFlags(&h->e_used[sl], hipEventDisableTiming));
+    }
 
     Dims &d = h->d;
     d.n = c.n; d.P = c.P; d.g = c.g; d.K = c.K;
@@ -256,6 +267,12 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     ALLOC(b.xa, KP * KP);
     ALLOC(b.xa_all, (size_t)nranks * KP * KP);
     ALLOC(b.XM, 2 * KP * KP);
+    ALLOC(b.xpart, (G + 7) / 8 * KP * KP);
+    {
+        double *tk = nullptr;
+        ALLOC(tk, (G + 7) / 8 + 1);
+        b.ticket = reinterpret_cast<unsigned *>(tk);
+    }
     ALLOC(b.C, G * PP * KP);
     ALLOC(b.E, G * KP * KP);
     ALLOC(b.cpart, G * PP * KP);
@@ -269,18 +286,23 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     if (!d.inject) {
         const size_t K = c.K, n = c.n, P = c.P;
         const size_t nz = K * n * g, nx = K * n, nl = K * P * g, gpsi = P * K * g, gdel = K * g, gps = P * g;
+        const size_t per_it = nz + nx + nl + gpsi + gdel + gps;
+        // batches of up to 8 iterations, two slots within ~2 GiB
+        h->DB = (int)std::max<size_t>(1, std::min<size_t>(8, (size_t(2) << 30) / (2 * per_it * sizeof(double))));
+        const size_t sz[6] = {nz, nx, nl, gpsi, gdel, gps};
+        for (int i = 0; i < 6; ++i) h->draw_iter_sz[i] = sz[i];
         double *gm = nullptr;
-        ALLOC(gm, 3 * (nz + nx + nl + gpsi + gdel + gps));
-        for (int sl = 0; sl < 3; ++sl) {
+        ALLOC(gm, 2 * (size_t)h->DB * per_it);
+        for (int sl = 0; sl < 2; ++sl) {
             DrawsDev &G = h->gen[sl];
-            G.NZ = gm; gm += nz;
-            G.NX = gm; gm += nx;
-            G.NL = gm; gm += nl;
-            G.Gpsi = gm; gm += gpsi;
-            G.Gdelta = gm; gm += gdel;
-            G.Gps = gm; gm += gps;
+            G.NZ = gm; gm += nz * h->DB;
+            G.NX = gm; gm += nx * h->DB;
+            G.NL = gm; gm += nl * h->DB;
+            G.Gpsi = gm; gm += gpsi * h->DB;
+            G.Gdelta = gm; gm += gdel * h->DB;
+            G.Gps = gm; gm += gps * h->DB;
             G.first_iter = -1;
-            G.n_iter = 1;
+            G.n_iter = h->DB;
         }
     }
 #undef ALLOC
@@ -315,7 +337,8 @@ void dcfm_destroy(dcfm_handle *h) {
     if (h->stream) sync_all(h);
     for (auto &r : h->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : h->evpool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {h->e_lam, h->e_prep, h->e_xchol, h->e_batch, h->e_free[0], h->e_free[1]})
+    for (hipEvent_t e : {h->e_lam, h->e_prep, h->e_xchol, h->e_batch, h->e_free[0], h->e_free[1], h->e_drawn[0],
+                         h->e_drawn[1], h->e_used[0], h->e_used[1]})
         if (e) (void)hipEventDestroy(e);
     if (h->comm_asm) ncclCommDestroy(h->comm_asm);
     if (h->comm_side) ncclCommDestroy(h->comm_side);
@@ -324,6 +347,7 @@ void dcfm_destroy(dcfm_handle *h) {
     if (h->draws_mem) (void)hipFree(h->draws_mem);
     if (h->sasm && h->sasm != h->stream) (void)hipStreamDestroy(h->sasm);
     if (h->side && h->side != h->stream) (void)hipStreamDestroy(h->side);
+    if (h->sdraw && h->sdraw != h->stream) (void)hipStreamDestroy(h->sdraw);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -597,47 +621,92 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
                         (long long)first_iter, (long long)(first_iter + n_iter));
     }
     HIPC(h, hipSetDevice(h->cfg.device));
-    hipStream_t s = h->stream, ss = h->side;
+    hipStream_t s = h->stream, ss = h->side, sd = h->sdraw;
     const size_t KW = d.kp;
     const size_t nkg = (size_t)d.g * KW;
-    // draws of iteration `it`: the injected buffers, or generated slot it % 3
-    auto ensure_draws = [&](int64_t it) {
-        if (d.inject) return;
-        const int sl = (int)(it % 3);
-        if (h->gen_iter[sl] == it) return;
-        h->gen[sl].first_iter = it;
-        KTimer t(h, DCFM_K_DRAWS, ss);
-        launch_draws(d, h->gen[sl], it, ss);
-        h->gen_iter[sl] = it;
+    const int64_t end_iter = first_iter + n_iter;
+    // one rank, K <= 32: prep and the X operators ride inside k_wprep / k_zxchol on the
+    // main stream; otherwise they run on the side stream (with the xa all-gather)
+    const bool fused = d.nranks == 1 && d.kp == KP;
+    // generated draws: batches [b0, b0 + DB) aligned to this call's first iteration,
+    // queued on sdraw into a slot whose previous batch the sweep has finished with
+    int rc_gen = DCFM_OK;
+    auto gen_batch = [&](int64_t b0, int busy) -> int {
+        const int64_t nb = std::min<int64_t>(h->DB, end_iter - b0);
+        for (int sl = 0; sl < 2; ++sl)
+            if (h->gen_first[sl] == b0 && h->gen_n[sl] >= nb) return sl;
+        int sl = busy >= 0 ? 1 - busy : (h->gen_first[0] <= h->gen_first[1] ? 0 : 1);
+        hipError_t e = hipSuccess;
+        if (h->used_pending[sl]) {
+            e = hipStreamWaitEvent(sd, h->e_used[sl], 0);
+            h->used_pending[sl] = false;
+        }
+        for (int64_t it = b0; e == hipSuccess && it < b0 + nb; ++it) {
+            const size_t o = (size_t)(it - b0);
+            DrawsDev v = h->gen[sl];
+            v.NZ += o * h->draw_iter_sz[0];
+            v.NX += o * h->draw_iter_sz[1];
+            v.NL += o * h->draw_iter_sz[2];
+            v.Gpsi += o * h->draw_iter_sz[3];
+            v.Gdelta += o * h->draw_iter_sz[4];
+            v.Gps += o * h->draw_iter_sz[5];
+            v.first_iter = it;
+            v.n_iter = 1;
+            KTimer t(h, DCFM_K_DRAWS, sd);
+            launch_draws(d, v, it, sd);
+        }
+        if (e == hipSuccess) e = hipEventRecord(h->e_drawn[sl], sd);
+        if (e != hipSuccess) {
+            rc_gen = fail(h, DCFM_ERR_HIP, "draws batch at iteration %lld: %s", (long long)b0, hipGetErrorString(e));
+            return -1;
+        }
+        h->gen[sl].first_iter = b0;
+        h->gen_first[sl] = b0;
+        h->gen_n[sl] = nb;
+        return sl;
     };
-    auto draws_of = [&](int64_t it) -> const DrawsDev & { return d.inject ? h->dr : h->gen[it % 3]; };
-    HIPC(h, hipEventRecord(h->e_lam, s));      // Lambda/omega of the previous iteration are final
-    HIPC(h, hipStreamWaitEvent(ss, h->e_lam, 0));
-    ensure_draws(first_iter);
-    for (int64_t it = first_iter; it < first_iter + n_iter; ++it) {
-        const DrawsDev &dr = draws_of(it);
-        // side stream: A_m, R_m, Rx from this iteration's incoming Lambda, omega (dc:98-100,112-118)
-        HIPC(h, hipStreamWaitEvent(ss, h->e_lam, 0));
-        { KTimer t(h, DCFM_K_PREP, ss); launch_prep(d, b, ss); }
-        HIPC(h, hipEventRecord(h->e_prep, ss));
-        { KTimer t(h, DCFM_K_XCHOL, ss); launch_asum(d, b, ss); }
-        if (d.nranks > 1) {
-            KTimer t(h, DCFM_K_COMM, ss);
-            NCCLC(h, ncclAllGather(b.xa, b.xa_all, KW * KW, ncclDouble, h->comm_side, ss));
+    int slot = -1;
+    int64_t batch0 = first_iter, batch_n = 0;
+    if (!fused) {
+        HIPC(h, hipEventRecord(h->e_lam, s));      // Lambda/omega of the previous iteration are final
+    }
+    for (int64_t it = first_iter; it < end_iter; ++it) {
+        if (!d.inject && (it == first_iter || it == batch0 + batch_n)) {
+            batch0 = it;
+            batch_n = std::min<int64_t>(h->DB, end_iter - it);
+            slot = gen_batch(it, -1);
+            if (slot < 0) return rc_gen;
+            HIPC(h, hipStreamWaitEvent(s, h->e_drawn[slot], 0));
+            if (it + batch_n < end_iter && gen_batch(it + batch_n, slot) < 0) return rc_gen;   // next batch
         }
-        { KTimer t(h, DCFM_K_XCHOL, ss); launch_xchol(d, b, ss); }
-        HIPC(h, hipEventRecord(h->e_xchol, ss));
-        ensure_draws(it + 1);                      // next iteration's variates, overlapping this one
-        // main stream
-        { KTimer t(h, DCFM_K_WPASS, s);  launch_wpass(d, b, s); }
-        HIPC(h, hipStreamWaitEvent(s, h->e_prep, 0));
-        { KTimer t(h, DCFM_K_ZDRAW, s);  launch_zdraw(d, b, dr, it, s); }
-        { KTimer t(h, DCFM_K_XRED, s);   launch_xred(d, b, s); }
-        if (d.nranks > 1) {
-            KTimer t(h, DCFM_K_COMM, s);
-            NCCLC(h, ncclAllGather(b.xin, b.xall, (size_t)d.NP * KW, ncclDouble, h->comm, s));
+        const DrawsDev &dr = d.inject ? h->dr : h->gen[slot];
+        if (fused) {
+            { KTimer t(h, DCFM_K_WPASS, s); launch_wprep(d, b, s); }
+            { KTimer t(h, DCFM_K_ZDRAW, s); launch_zxchol(d, b, dr, it, s); }
+            { KTimer t(h, DCFM_K_XRED, s);  launch_xred(d, b, s); }
+        } else {
+            // side stream: A_m, R_m, Rx from this iteration's incoming Lambda, omega (dc:98-100,112-118)
+            HIPC(h, hipStreamWaitEvent(ss, h->e_lam, 0));
+            { KTimer t(h, DCFM_K_PREP, ss); launch_prep(d, b, ss); }
+            HIPC(h, hipEventRecord(h->e_prep, ss));
+            { KTimer t(h, DCFM_K_XCHOL, ss); launch_asum(d, b, ss); }
+            if (d.nranks > 1) {
+                KTimer t(h, DCFM_K_COMM, ss);
+                NCCLC(h, ncclAllGather(b.xa, b.xa_all, KW * KW, ncclDouble, h->comm_side, ss));
+            }
+            { KTimer t(h, DCFM_K_XCHOL, ss); launch_xchol(d, b, ss); }
+            HIPC(h, hipEventRecord(h->e_xchol, ss));
+            // main stream
+            { KTimer t(h, DCFM_K_WPASS, s);  launch_wpass(d, b, s); }
+            HIPC(h, hipStreamWaitEvent(s, h->e_prep, 0));
+            { KTimer t(h, DCFM_K_ZDRAW, s);  launch_zdraw(d, b, dr, it, s); }
+            { KTimer t(h, DCFM_K_XRED, s);   launch_xred(d, b, s); }
+            if (d.nranks > 1) {
+                KTimer t(h, DCFM_K_COMM, s);
+                NCCLC(h, ncclAllGather(b.xin, b.xall, (size_t)d.NP * KW, ncclDouble, h->comm, s));
+            }
+            HIPC(h, hipStreamWaitEvent(s, h->e_xchol, 0));
         }
-        HIPC(h, hipStreamWaitEvent(s, h->e_xchol, 0));
         { KTimer t(h, DCFM_K_XDRAW, s);  launch_xdraw(d, b, dr, it, s); }
         { KTimer t(h, DCFM_K_CPASS, s);  launch_cpass(d, b, s); }
         {
@@ -645,7 +714,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s);
         }
         h->plam_valid = false;
-        HIPC(h, hipEventRecord(h->e_lam, s));
+        if (!fused) HIPC(h, hipEventRecord(h->e_lam, s));
         { KTimer t(h, DCFM_K_COLSUM, s); launch_colsum(d, b, s); }
         if (d.nranks > 1) {
             KTimer t(h, DCFM_K_COMM, s);
@@ -655,6 +724,10 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             KTimer t(h, DCFM_K_DELTA, s);
             launch_delta(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
                          b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);
+        }
+        if (!d.inject && it == batch0 + batch_n - 1) {      // the batch's last consumer is queued
+            HIPC(h, hipEventRecord(h->e_used[slot], s));
+            h->used_pending[slot] = true;
         }
         h->cur ^= 1;
         HIPC(h, hipGetLastError());
@@ -684,6 +757,7 @@ int dcfm_synchronize(dcfm_handle *h) {
     HIPC(h, hipSetDevice(h->cfg.device));
     HIPC(h, hipStreamSynchronize(h->stream));
     HIPC(h, hipStreamSynchronize(h->side));
+    HIPC(h, hipStreamSynchronize(h->sdraw));
     HIPC(h, hipStreamSynchronize(h->sasm));
     return DCFM_OK;
 }

@@ -57,12 +57,14 @@ namespace dcfm {
 //     S = W + NA Z,              NA = -sqrt(1-rho) A
 // ZM[m] = {M1, M2, U, NA}.  4 waves split the j reduction of A (fp64 MFMA 2x2 tiles).
 // ============================================================================
-__global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__ Lam,
-                                              const double *__restrict__ omega,
-                                              double *__restrict__ A, double *__restrict__ ZM) {
-    __shared__ double part[4][KP][KP + 1];     // partial A per wave; later A, U, T
-    __shared__ __attribute__((aligned(16))) double Lp[P2STRIDE];
-    const int m = blockIdx.x;
+constexpr int PREP_SMEM = 4 * KP * (KP + 1) + 3 * TS16;
+__device__ __forceinline__ void prep_shard(const Dims &d, const double *__restrict__ Lam,
+                                           const double *__restrict__ omega, double *__restrict__ A,
+                                           double *__restrict__ ZM, int m, double *smem) {
+    // partial A per wave; later A, U, Zprec/T, scratch
+    double (*part)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);
+    double *lds_l = smem + 4 * KP * (KP + 1), *lds_u = lds_l + 2 * TS16;
+    PHASE_T0();
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const int r = lane & 15, q = lane >> 4;
     const double *L = Lam + (size_t)m * d.PP * KP;
@@ -88,7 +90,9 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
         part[wave][16 + a][r] = a10[g];
         part[wave][16 + a][16 + r] = a11[g];
     }
+    PHASE(0);
     __syncthreads();
+    PHASE(1);
     double *Am = A + (size_t)m * KP * KP;
     double *Zm = ZM + (size_t)m * 4 * KP * KP;
     double av[4];
@@ -96,29 +100,26 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
     for (int u = 0; u < 4; ++u) {
         const int e = t + 256 * u, a = e / KP, b = e % KP;
         av[u] = (part[0][a][b] + part[1][a][b]) + (part[2][a][b] + part[3][a][b]);
-        Am[e] = av[u];
+        __hip_atomic_store(Am + e, av[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // read by shard_sum_tree
         Zm[3 * KP * KP + e] = -d.s1r * av[u];                       // NA
     }
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int e = t + 256 * u;
-        part[0][e / KP][e % KP] = av[u];                            // A
+        const int a = e / KP, b = e % KP;
+        part[0][a][b] = av[u];                                      // A
+        // cholcov reads the upper triangle: lower of Sm = (Zprec upper)'
+        if (a <= b) part[2][b][a] = (a == b ? 1.0 : 0.0) + (1.0 - d.rho) * av[u];
     }
     __syncthreads();
-    if (wave == 0) {
-        // cholcov reads the upper triangle: S[rr][c] = Zprec[c][rr] for c <= rr
-        const int rr = lane & 31;
-        double qq[KP];
-#pragma unroll
-        for (int c = 0; c < KP; ++c)
-            qq[c] = (c <= rr) ? ((c == rr ? 1.0 : 0.0) + (1.0 - d.rho) * part[0][c][rr]) : 0.0;
-        double vr = 0.0;
-        chol2_rows<false>(qq, Lp, rr, lane >= 32, 0.0, vr);
+    if (wave == 0) {                                                // U = L^{-1} -> part[1]
+        PHASE(2);
+        chol_inv32(part[2], part[1], part[3], lds_l, lds_u, lane);
+        PHASE(3);
     }
     __syncthreads();
-    lower_inverse2(Lp, part[1], t);                                 // U -> part[1]
-    __syncthreads();
+    PHASE(4);
     {   // T = U U' (fp64 MFMA, one 16x16 tile per wave) -> part[2]; M1 = s1r T; U
         const int ti = wave >> 1, tj = wave & 1, j = lane & 15, q = lane >> 4;
         const d4 T = mfma_tile32<true>(part[1], part[1], ti, tj, lane);
@@ -138,6 +139,15 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 #pragma unroll
         for (int g = 0; g < 4; ++g) Zm[KP * KP + (16 * ti + q + 4 * g) * KP + 16 * tj + j] = s2 * M[g];
     }
+    PHASE(5);
+    PHASE_END_AT(8);
+}
+
+__global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__ Lam,
+                                              const double *__restrict__ omega,
+                                              double *__restrict__ A, double *__restrict__ ZM) {
+    __shared__ double smem[PREP_SMEM];
+    prep_shard(d, Lam, omega, A, ZM, blockIdx.x, smem);
 }
 
 // ============================================================================
@@ -149,19 +159,16 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 // uses the same j <-> (q, e) map.  Register double-buffered prefetch of 2 chunks.
 // ============================================================================
 template <int KW>
-__global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict__ Y,
-                                               const double *__restrict__ Lam,
-                                               const double *__restrict__ omega,
-                                               double *__restrict__ W) {
+__device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restrict__ Y,
+                                           const double *__restrict__ Lam, const double *__restrict__ omega,
+                                           double *__restrict__ W, int w, int kt) {
     const int nrb = d.NP >> 7;                       // 128-row blocks per shard
-    const int w = xcd_remap(blockIdx.x, gridDim.x);
     const int m = w / nrb, rb = w % nrb;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int i0 = rb * 128 + wave * 32;
     const int r = lane & 15, q = lane >> 4;
     const double *Y0 = Y + ((size_t)m * d.NP + i0 + r) * d.PP + 2 * q;
     const double *Y1 = Y0 + (size_t)16 * d.PP;
-    const int kt = blockIdx.y;
     const double *L = Lam + (size_t)m * d.PP * KW + 32 * kt + 2 * r;
     const double *wp = omega + (size_t)m * d.PP + 2 * q;
     d4 acc[2][2];
@@ -216,6 +223,14 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
     }
 }
 
+template <int KW>
+__global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict__ Y,
+                                               const double *__restrict__ Lam,
+                                               const double *__restrict__ omega,
+                                               double *__restrict__ W) {
+    wpass_tile<KW>(d, Y, Lam, omega, W, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y);
+}
+
 // ============================================================================
 // k_zdraw: Z draw and per-shard X message as fp64 MFMA chains.   dc:101-107,121-123
 //   Z' = M1 W' + M2 X' + U eps'      (k_prep operators; columns = rows i)
@@ -225,14 +240,13 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
 // the f64 C/D layout of Z' (row = q + 4r) is directly the B operand of the
 // NA Z' product (k-step r), so nothing crosses LDS.
 // ============================================================================
-__global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W,
-                                               const double *__restrict__ ZM,
-                                               const double *__restrict__ X,
-                                               double *__restrict__ Z, double *__restrict__ Sp,
-                                               DrawsDev dr, int64_t iter) {
-    __shared__ double Ms[4][KP][KP + 1];     // M1, M2, U, NA
+constexpr int ZDRAW_SMEM = 4 * KP * (KP + 1);
+__device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restrict__ W,
+                                           const double *__restrict__ ZM, const double *__restrict__ X,
+                                           double *__restrict__ Z, double *__restrict__ Sp, const DrawsDev &dr,
+                                           int64_t iter, int w, double *smem) {
+    double (*Ms)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);   // M1, M2, U, NA
     const int nrb = d.NP >> 7;
-    const int w = xcd_remap(blockIdx.x, gridDim.x);
     const int m = w / nrb, rb = w % nrb;
     {
         const double *Zm = ZM + (size_t)m * 4 * KP * KP;
@@ -314,6 +328,15 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
     }
 }
 
+__global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W,
+                                               const double *__restrict__ ZM,
+                                               const double *__restrict__ X,
+                                               double *__restrict__ Z, double *__restrict__ Sp,
+                                               DrawsDev dr, int64_t iter) {
+    __shared__ double smem[ZDRAW_SMEM];
+    zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blockIdx.x, gridDim.x), smem);
+}
+
 // ============================================================================
 // k_xred: xin[i][k] = sum_m Sp[m][i][k]  (local shards, fixed order)     dc:120-124
 // ============================================================================
@@ -347,29 +370,22 @@ __global__ __launch_bounds__(256) void k_asum(Dims d, const double *__restrict__
 // side stream.  Sums the per-rank sums xa_all (k_asum, all-gathered) in rank order
 // and writes the X-draw operators XM = {Tx = sqrt(rho) Ux Ux', Ux = Rx^{-T}} (Tx by MFMA).
 // ============================================================================
-__global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict__ xa_all,
-                                               double *__restrict__ XM) {
-    __shared__ __attribute__((aligned(16))) double Lp[P2STRIDE];
-    __shared__ double As[KP][KP + 1], Us[KP][KP + 1];
+constexpr int XCHOL_SMEM = 2 * KP * (KP + 1) + TS16 * (KP + 1) + 3 * TS16 + 2;
+// smem = {Sm, Us, Wk, lds_l, lds_u, flag}; Sm (lower) holds Xprec's upper triangle on entry
+__device__ __forceinline__ void xchol_factor(const Dims &d, double *__restrict__ XM, double *smem) {
+    double (*Sm)[KP + 1] = reinterpret_cast<double (*)[KP + 1]>(smem);
+    double (*Us)[KP + 1] = Sm + KP;
+    double (*Wk)[KP + 1] = Us + KP;
+    double *lds_l = smem + 2 * KP * (KP + 1) + TS16 * (KP + 1), *lds_u = lds_l + 2 * TS16;
+    PHASE_T0();
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    for (int e = t; e < KP * KP; e += 256) {
-        double v = xa_all[e];
-        for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * KP * KP + e];
-        As[e / KP][e % KP] = v;
+    if (wave == 0) {                       // Ux = Lx^{-1} = Rx^{-T}
+        PHASE(1);
+        chol_inv32(Sm, Us, Wk, lds_l, lds_u, lane);
+        PHASE(2);
     }
     __syncthreads();
-    if (wave == 0) {
-        const int rr = lane & 31;
-        double qq[KP];
-#pragma unroll
-        for (int c = 0; c < KP; ++c)   // cholcov reads the upper triangle: S[rr][c] = Xprec[c][rr]
-            qq[c] = (c <= rr) ? ((c == rr ? (double)d.g : 0.0) + d.rho * As[c][rr]) : 0.0;
-        double vr = 0.0;
-        chol2_rows<false>(qq, Lp, rr, lane >= 32, 0.0, vr);
-    }
-    __syncthreads();
-    lower_inverse2(Lp, Us, t);             // Ux = Lx^{-1} = Rx^{-T}
-    __syncthreads();
+    PHASE(3);
     // X = Rx^{-T}(Rx^{-1} sqrt(rho) S + eps) = Tx S + Ux eps,  Tx = sqrt(rho) Ux Ux'
     const int ti = wave >> 1, tj = wave & 1, j = lane & 15, q = lane >> 4;
     const d4 T = mfma_tile32<true>(Us, Us, ti, tj, lane);
@@ -379,6 +395,122 @@ __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict_
         XM[a * KP + c] = d.sr * T[g];
         XM[KP * KP + a * KP + c] = Us[a][c];
     }
+    PHASE(4);
+    PHASE_END_AT(16);
+}
+
+// Xprec's upper triangle, transposed into the lower triangle of Sm: g I + rho sum A   dc:117
+__device__ __forceinline__ void xprec_store(const Dims &d, double *smem, int e, double v) {
+    double (*Sm)[KP + 1] = reinterpret_cast<double (*)[KP + 1]>(smem);
+    const int a = e / KP, b = e % KP;
+    if (a <= b) Sm[b][a] = (a == b ? (double)d.g : 0.0) + d.rho * v;
+}
+
+__global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict__ xa_all,
+                                               double *__restrict__ XM) {
+    __shared__ double smem[XCHOL_SMEM];
+    for (int e = threadIdx.x; e < KP * KP; e += 256) {
+        double v = xa_all[e];
+        for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * KP * KP + e];
+        xprec_store(d, smem, e, v);
+    }
+    __syncthreads();
+    xchol_factor(d, XM, smem);
+}
+
+// ============================================================================
+// Fused single-stream launches (one rank, K <= 32): the side-stream hops they
+// replace cost ~6 us of event latency each on the critical path.
+// k_wprep:  blocks [0, G) = k_prep shards (dispatched first) + the shard sum xa of A
+//           (shard_sum_tree), the rest k_wpass tiles.
+// k_zxchol: block 0 forms the X-draw operators from xa (k_xchol); the rest are k_zdraw tiles.
+// ============================================================================
+// xa = sum_m A_m over the local shards as a fixed two-level tree (groups of 8 shards in
+// shard order, then the groups in order), run by whichever prep blocks finish last:
+// after its A_m is out (device-scope release), a block takes a ticket for its group;
+// the last of the group sums the group into gpart, takes a ticket for the root, and the
+// last group-summer adds the group sums into xa.  No block waits on another.
+// The exchanged values (A_m, group sums) are written and read with agent-scope relaxed
+// atomics (sc1: coherent across the XCDs' L2s without write-back / invalidate), so the
+// hand-off needs only the stores' completion before the ticket — not __threadfence,
+// whose buffer_wbl2 / buffer_inv would flush and drop the wpass tiles' L2 contents.
+constexpr int SUM_GROUP = 8;
+__device__ __forceinline__ void st_agent(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double *p) {
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool last_arrival(unsigned *ticket, unsigned count, double *smem) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this thread's agent-scope stores are done
+    __syncthreads();
+    unsigned *flag = reinterpret_cast<unsigned *>(smem);
+    if (threadIdx.x == 0) {
+        const bool last =
+            __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == count - 1;
+        if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+        *flag = last ? 1u : 0u;
+    }
+    __syncthreads();
+    const bool last = *flag != 0u;
+    __syncthreads();
+    return last;
+}
+__device__ __forceinline__ void shard_sum_tree(const Dims &d, const double *__restrict__ A,
+                                               double *__restrict__ gpart, unsigned *__restrict__ tickets,
+                                               double *__restrict__ xa, int m, double *smem) {
+    const int ng = (d.G + SUM_GROUP - 1) / SUM_GROUP, grp = m / SUM_GROUP;
+    const int g0 = grp * SUM_GROUP, g1 = min(d.G, g0 + SUM_GROUP);
+    if (!last_arrival(tickets + grp, (unsigned)(g1 - g0), smem)) return;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < KP * KP / 256; ++u) {
+        const int e = t + 256 * u;
+        double v = 0.0;
+#pragma unroll 8
+        for (int mm = g0; mm < g1; ++mm) v += ld_agent(A + (size_t)mm * KP * KP + e);
+        st_agent(gpart + (size_t)grp * KP * KP + e, v);
+    }
+    if (!last_arrival(tickets + ng, (unsigned)ng, smem)) return;
+#pragma unroll
+    for (int u = 0; u < KP * KP / 256; ++u) {
+        const int e = t + 256 * u;
+        double v = 0.0;
+        for (int gg = 0; gg < ng; ++gg) v += ld_agent(gpart + (size_t)gg * KP * KP + e);
+        xa[e] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_wprep(Dims d, const double *__restrict__ Y,
+                                               const double *__restrict__ Lam,
+                                               const double *__restrict__ omega, double *__restrict__ W,
+                                               double *__restrict__ A, double *__restrict__ ZM,
+                                               double *__restrict__ gpart, unsigned *__restrict__ tickets,
+                                               double *__restrict__ xa) {
+    __shared__ double smem[PREP_SMEM];
+    if ((int)blockIdx.x < d.G) {
+        prep_shard(d, Lam, omega, A, ZM, blockIdx.x, smem);
+        shard_sum_tree(d, A, gpart, tickets, xa, blockIdx.x, smem);
+        return;
+    }
+    const int vb = blockIdx.x - d.G;
+    wpass_tile<KP>(d, Y, Lam, omega, W, xcd_remap(vb, gridDim.x - d.G), 0);
+}
+
+constexpr int ZX_SMEM = ZDRAW_SMEM > XCHOL_SMEM ? ZDRAW_SMEM : XCHOL_SMEM;
+__global__ __launch_bounds__(256) void k_zxchol(Dims d, const double *__restrict__ W,
+                                                const double *__restrict__ ZM, const double *__restrict__ X,
+                                                double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
+                                                int64_t iter, const double *__restrict__ xa,
+                                                double *__restrict__ XM) {
+    __shared__ double smem[ZX_SMEM];
+    if (blockIdx.x > 0) {
+        zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blockIdx.x - 1, gridDim.x - 1), smem);
+        return;
+    }
+    for (int e = threadIdx.x; e < KP * KP; e += 256) xprec_store(d, smem, e, xa[e]);
+    __syncthreads();
+    xchol_factor(d, XM, smem);
 }
 
 // ============================================================================
@@ -1163,6 +1295,16 @@ void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
     if (d.kp != KP) return wide::launch_zdraw(d, b, dr, iter, s);
     hipLaunchKernelGGL(k_zdraw, dim3((d.NP / 128) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
                        dr, iter);
+}
+void launch_wprep(const Dims &d, const Bufs &b, hipStream_t s) {
+    if (d.kp != KP) return;
+    hipLaunchKernelGGL(k_wprep, dim3(d.G + (d.NP / 128) * d.G), dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W, b.A,
+                       b.ZM, b.xpart, b.ticket, b.xa);
+}
+void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+    if (d.kp != KP) return;
+    hipLaunchKernelGGL(k_zxchol, dim3(1 + (d.NP / 128) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp, dr,
+                       iter, b.xa, b.XM);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
     const int total = d.NP * d.kp;

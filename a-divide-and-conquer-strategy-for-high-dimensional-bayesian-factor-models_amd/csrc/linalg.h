@@ -108,12 +108,14 @@ extern __device__ unsigned long long g_phase[32];
         ph_acc_[(k)] += ph_n_ - ph_t_;                                                      \
         ph_t_ = ph_n_;                                                                      \
     } while (0)
-#define PHASE_END()                                                                         \
+#define PHASE_END_AT(b)                                                                     \
     do {                                                                                    \
         if ((threadIdx.x & 63) == 0)                                                        \
-            for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_phase[k_], ph_acc_[k_]);            \
+            for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_phase[(b) + k_], ph_acc_[k_]);      \
     } while (0)
+#define PHASE_END() PHASE_END_AT(0)
 #else
+#define PHASE_END_AT(b) (void)0
 #define PHASE_T0() (void)0
 #define PHASE(k) (void)0
 #define PHASE_END() (void)0
@@ -258,6 +260,116 @@ __device__ __forceinline__ void chol2_rows(double (&q)[KP], double *P, int r, bo
 #pragma unroll
         for (int c = k + 2; c < KP; ++c) asm volatile("" : "+v"(q[c]));
     }
+}
+
+constexpr int TS16 = 16;
+
+// value of x held by lane 4*(lane/4) + J (DPP quad_perm [J,J,J,J])
+template <int J>
+__device__ __forceinline__ double quad_bcast(double x) {
+    constexpr int ctrl = J | (J << 2) | (J << 4) | (J << 6);
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), ctrl, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// one step k = 4 kk + J of chol_inv16 (below); explicit scalars keep it in registers
+template <int J>
+__device__ __forceinline__ void chol16_step(double &a0, double &a1, double &a2, double &a3, double &R0, double &R1,
+                                            double &R2, double &R3, int kk, int r, int cg, double *lds_l,
+                                            double *lds_u) {
+    const int k = 4 * kk + J;
+    const double piv = readlane_d(a0, 4 * k + J);
+    const double ik = rsqrt_f64(piv);
+    const double v = quad_bcast<J>(a0);
+    const double l = (r > k) ? v * ik : (r == k ? piv * ik : 0.0);
+    if (cg == 0) lds_l[r] = l;
+    if (r == k) {
+        R0 *= ik; R1 *= ik; R2 *= ik; R3 *= ik;
+        lds_u[cg] = R0; lds_u[4 + cg] = R1; lds_u[8 + cg] = R2; lds_u[12 + cg] = R3;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const double *pl = lds_l + 4 * kk + cg;
+    const double l0 = pl[0], l1 = pl[4], l2 = pl[8], l3 = pl[12];
+    const double u0 = lds_u[cg], u1 = lds_u[4 + cg], u2 = lds_u[8 + cg], u3 = lds_u[12 + cg];
+    a0 = fma(-l, l0, a0); a1 = fma(-l, l1, a1); a2 = fma(-l, l2, a2); a3 = fma(-l, l3, a3);
+    const double lr = (r > k) ? l : 0.0;
+    R0 = fma(-lr, u0, R0); R1 = fma(-lr, u1, R1); R2 = fma(-lr, u2, R2); R3 = fma(-lr, u3, R3);
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Cholesky factor and inverse of the 16x16 diagonal block at (o, o) of Sm (lower
+// triangle read) on one wave: writes Ub(o.., o..) = L^{-1} (zeros above the diagonal).
+// The one-block kernels (k_prep, k_xchol) run this cold every iteration, so the code
+// is a rolled loop and the per-step latency chain is short: lane = 4 r + cg holds
+// row r, columns 4 i + cg (i = 0..3) of the working matrix in a0..a3 (shifted one
+// column group per outer step, so the pivot column is always a0) and of the
+// right-hand side of L U = I in R0..R3.  Step k: pivot by readlane, l_r by a DPP
+// quad broadcast, then one LDS round trip hands out column k of L (lds_l, 32 slots,
+// the upper 16 zero) and row k of U (lds_u, 16 slots).
+__device__ __forceinline__ void chol_inv16(const double (*Sm)[KP + 1], int o, double (*Ub)[KP + 1],
+                                           double *lds_l, double *lds_u, int lane) {
+    const int r = lane >> 2, cg = lane & 3;
+    const double *srow = &Sm[o + r][o + cg];   // entries above the diagonal are never consumed
+    double a0 = srow[0], a1 = srow[4], a2 = srow[8], a3 = srow[12];
+    double R0 = (cg == r) ? 1.0 : 0.0, R1 = (4 + cg == r) ? 1.0 : 0.0;
+    double R2 = (8 + cg == r) ? 1.0 : 0.0, R3 = (12 + cg == r) ? 1.0 : 0.0;
+    if (lane < 16) lds_l[16 + lane] = 0.0;
+#pragma unroll 1
+    for (int kk = 0; kk < 4; ++kk) {
+        chol16_step<0>(a0, a1, a2, a3, R0, R1, R2, R3, kk, r, cg, lds_l, lds_u);
+        chol16_step<1>(a0, a1, a2, a3, R0, R1, R2, R3, kk, r, cg, lds_l, lds_u);
+        chol16_step<2>(a0, a1, a2, a3, R0, R1, R2, R3, kk, r, cg, lds_l, lds_u);
+        chol16_step<3>(a0, a1, a2, a3, R0, R1, R2, R3, kk, r, cg, lds_l, lds_u);
+        a0 = a1; a1 = a2; a2 = a3; a3 = 0.0;
+    }
+    double *urow = &Ub[o + r][o + cg];
+    urow[0] = R0; urow[4] = R1; urow[8] = R2; urow[12] = R3;
+}
+
+// U = L^{-1}, L = chol of the KP x KP (= 32) SPD matrix whose lower triangle is in
+// Sm, on one wave: two chol_inv16 diagonal blocks plus fp64 MFMA for the rest:
+//   L21 = A21 U11',  S22 <- S22 - L21 L21'  (in place in Sm),  U21 = -U22 L21 U11.
+// Wk: 16 x (KP+1) scratch (L21).  Upper triangle of Us is written 0.
+__device__ __forceinline__ void chol_inv32(double (*Sm)[KP + 1], double (*Us)[KP + 1], double (*Wk)[KP + 1],
+                                           double *lds_l, double *lds_u, int lane) {
+    static_assert(KP == 32, "narrow operator path");
+    const int i = lane & 15, q = lane >> 4;
+    chol_inv16(Sm, 0, Us, lds_l, lds_u, lane);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    d4 l21 = {0.0, 0.0, 0.0, 0.0};                       // L21[q+4g][i] = sum_k A21[.][k] U11[i][k]
+#pragma unroll
+    for (int s = 0; s < 4; ++s) l21 = mfma16x16x4(Sm[16 + i][4 * s + q], Us[i][4 * s + q], l21);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        Wk[q + 4 * g][i] = l21[g];
+        Us[q + 4 * g][16 + i] = 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    d4 s22;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) s22[g] = Sm[16 + q + 4 * g][16 + i];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) s22 = mfma16x16x4(-Wk[i][4 * s + q], Wk[i][4 * s + q], s22);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) Sm[16 + q + 4 * g][16 + i] = s22[g];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    chol_inv16(Sm, 16, Us, lds_l, lds_u, lane);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    d4 x = {0.0, 0.0, 0.0, 0.0};                         // X = L21 U11  (NN)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) x = mfma16x16x4(Wk[i][4 * s + q], Us[4 * s + q][i], x);
+    d4 u21 = {0.0, 0.0, 0.0, 0.0};                       // U21 = -U22 X, X in C/D layout = B operand
+#pragma unroll
+    for (int g = 0; g < 4; ++g) u21 = mfma16x16x4(-Us[16 + i][16 + q + 4 * g], x[g], u21);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) Us[16 + q + 4 * g][i] = u21[g];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
 }
 
 // One 16x16 tile of a 32x32 product in LDS, fp64 MFMA (whole wave, 8 k-steps):

@@ -1,0 +1,26 @@
+"""Per-phase shader-clock cycles of k_prep (slots 8..) and k_xchol (slots 16..) at c3
+(dev aid; needs build/libdcfm_phase.so from tools/build_variant.sh phase -DDCFM_PHASE_TIMING)."""
+import ctypes as C, os, sys
+os.environ["DCFM_LIB"] = os.path.abspath("build/libdcfm_phase.so")
+sys.path.insert(0, ".")
+import __graft_entry__ as ge
+import bench
+dcfm = ge.load_package()
+g, P, n, K = 64, 312, 1000, 30
+Y = bench.synth_data(n, g * P)
+hyper = dcfm.Hyper()
+Yk, n, pk, P, K_, keep = dcfm.preprocess(Y, g, K * g)
+init = dcfm.driver._HostInitDraws(1, n, pk, g, K, hyper)
+Yd = dcfm.partition_standardize(Yk, g, init.varind)
+state = dcfm.initial_state(n, P, K, g, 0.5, hyper, init)
+smp = dcfm.Sampler(n, P, g, K, 0.5, 0, 100, 1000, seed=1)
+smp.set_data(Yd); smp.set_state(dcfm.local_state(state, 0, g))
+lib = smp.lib
+lib.dcfm_debug_phases.argtypes = [C.POINTER(C.c_ulonglong)]
+buf = (C.c_ulonglong * 32)()
+smp.run(1, 10); smp.synchronize(); lib.dcfm_debug_phases(buf)
+T = 20
+smp.run(11, T); smp.synchronize(); lib.dcfm_debug_phases(buf)
+for name, base, waves in (("k_prep", 8, 4 * g), ("k_xchol", 16, 4)):
+    print(name, "cycles per wave per launch:",
+          " ".join(f"p{k}={buf[base + k] / waves / T:.0f}" for k in range(8) if buf[base + k]))

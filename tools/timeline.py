@@ -5,13 +5,15 @@ from collections import defaultdict
 rows = []
 for f in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
     rows += list(csv.DictReader(open(f)))
-anchor = sys.argv[2] if len(sys.argv) > 2 else "k_wpass"
+anchor = sys.argv[2] if len(sys.argv) > 2 else None
 ev = []
 for r in rows:
     m = re.search(r"(k_\w+)", r["Kernel_Name"])
     k = m.group(1) if m else r["Kernel_Name"][:20]
     ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k, r["Queue_Id"]))
 ev.sort()
+if anchor is None:
+    anchor = "k_wprep" if any(e[2] == "k_wprep" for e in ev) else "k_wpass"
 w = [e[0] for e in ev if e[2] == anchor]
 t0, t1 = w[-20], w[-10]
 win = [e for e in ev if t0 <= e[0] < t1]
