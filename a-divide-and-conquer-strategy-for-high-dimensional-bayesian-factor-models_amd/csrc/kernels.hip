@@ -1172,91 +1172,106 @@ __global__ __launch_bounds__(256) void k_eta(Dims d, const double *__restrict__ 
 // Gpsi (local), Gps (local), Gdelta (all g shards: every rank runs every chain).
 // Pointers are indexed by GLOBAL shard mg (as the injected full-g arrays are).
 // ============================================================================
-struct DrawSeg { int64_t nz, nx, nl, gpsi, gps, gdel; };
-
-__host__ __device__ inline DrawSeg draw_segments(const Dims &d) {
-    auto al = [](int64_t v) { return (v + 63) / 64 * 64; };
-    const int64_t kp2 = (d.K + 1) / 2;   // normal pairs per row
-    DrawSeg s;
-    s.nz = al((int64_t)d.G * d.n * kp2);
-    s.nx = al((int64_t)d.n * kp2);
-    s.nl = al((int64_t)d.G * d.P * kp2);
-    s.gpsi = al((int64_t)d.G * d.P * d.K);
-    s.gps = al((int64_t)d.G * d.P);
-    s.gdel = al((int64_t)d.g * d.K);
-    return s;
+// Block plan of k_draws: every segment gets whole blocks, and a block covers
+// 256 / LR rows of one shard with LR in {16, 32, 64} lanes per row (the smallest that
+// holds a row's pairs / gammas, K <= 128), so a thread's (shard, row, index) comes
+// from shifts and one block-uniform division — no per-element integer division.
+// The rejection-sampled gammas (delta: one per thread; ps: one per thread) come first
+// in block order so their longer threads start early; the bulk normals follow.
+struct DrawPlan {
+    int lrn, lrg;                    // lanes per row: normal pairs, gamma row (Gpsi)
+    int nrb_n, nrb_p, nrb_g, nrb_s;  // row-blocks per shard: n rows, P rows (normals), P rows (Gpsi), Gps
+    int b_gdel, b_gps, b_gpsi, b_nz, b_nx, total;  // segment end blocks (cumulative); NL last
+};
+__host__ __device__ inline int lanes_for(int c) { return c <= 16 ? 16 : (c <= 32 ? 32 : 64); }
+__host__ __device__ inline DrawPlan draw_plan(const Dims &d) {
+    DrawPlan pl;
+    const int kp2 = (d.K + 1) / 2;
+    pl.lrn = lanes_for(kp2);
+    pl.lrg = lanes_for(d.K);
+    const int rpn = 256 / pl.lrn, rpg = 256 / pl.lrg;
+    pl.nrb_n = (d.n + rpn - 1) / rpn;
+    pl.nrb_p = (d.P + rpn - 1) / rpn;
+    pl.nrb_g = (d.P + rpg - 1) / rpg;
+    pl.nrb_s = (d.P + 255) / 256;
+    pl.b_gdel = (d.g * d.K + 255) / 256;          // Gdelta of all g shards
+    pl.b_gps = pl.b_gdel + d.G * pl.nrb_s;
+    pl.b_gpsi = pl.b_gps + d.G * pl.nrb_g;
+    pl.b_nz = pl.b_gpsi + d.G * pl.nrb_n;
+    pl.b_nx = pl.b_nz + pl.nrb_n;
+    pl.total = pl.b_nx + d.G * pl.nrb_p;
+    return pl;
 }
 
+// normals of one row: lane pair index pr = 0..kp2-1 -> out[2 pr], out[2 pr + 1]
+__device__ __forceinline__ void draw_normal_row(const Rng &rng, uint32_t site, uint32_t mg, uint32_t row,
+                                                uint32_t it, int K, int lane, int lr, double *out) {
+    const int kp2 = (K + 1) / 2;
+    for (int pr = lane; pr < kp2; pr += lr) {
+        double n0, n1;
+        rng.normal2(site, mg, row, (uint32_t)pr, it, n0, n1);
+        out[2 * pr] = n0;
+        if (2 * pr + 1 < K) out[2 * pr + 1] = n1;
+    }
+}
+
+// two launches per iteration: the gamma segments (rejection loops, more registers)
+// and the normal segments (high occupancy); b_off = first block of the launch
+template <bool GAMMAS>
 __global__ __launch_bounds__(256) void k_draws(Dims d, DrawsDev dr, int64_t iter) {
-    // 32-bit index arithmetic throughout (64-bit division is a long software sequence)
-    const DrawSeg sg = draw_segments(d);
-    const uint32_t snz = (uint32_t)sg.nz, snx = (uint32_t)sg.nx, snl = (uint32_t)sg.nl, sgpsi = (uint32_t)sg.gpsi,
-                   sgps = (uint32_t)sg.gps;
-    const uint32_t total = snz + snx + snl + sgpsi + sgps + (uint32_t)sg.gdel;
+    const DrawPlan pl = draw_plan(d);
     const Rng rng(d.seed);
     const uint32_t it = (uint32_t)iter;
-    const uint32_t kp2 = (d.K + 1) / 2, n = d.n, P = d.P, K = d.K, G = d.G;
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-        uint32_t x = e;
-        if (x < snz) {                                     // dc:104, K x n x g
-            const uint32_t pr = x % kp2, rest = x / kp2;
-            const uint32_t i = rest % n, m = rest / n;
-            if (m >= G) continue;
-            const uint32_t mg = d.shard0 + m;
-            double n0, n1;
-            rng.normal2(SITE_Z, mg, i, pr, it, n0, n1);
-            double *o = const_cast<double *>(dr.NZ) + ((size_t)mg * n + i) * K + 2 * pr;
-            o[0] = n0;
-            if (2 * pr + 1 < K) o[1] = n1;
-            continue;
-        }
-        x -= snz;
-        if (x < snx) {                                     // dc:126, K x n
-            const uint32_t pr = x % kp2, i = x / kp2;
-            if (i >= n) continue;
-            double n0, n1;
-            rng.normal2(SITE_X, 0, i, pr, it, n0, n1);
-            double *o = const_cast<double *>(dr.NX) + (size_t)i * K + 2 * pr;
-            o[0] = n0;
-            if (2 * pr + 1 < K) o[1] = n1;
-            continue;
-        }
-        x -= snx;
-        if (x < snl) {                                     // dc:142, K x P x g
-            const uint32_t pr = x % kp2, rest = x / kp2;
-            const uint32_t j = rest % P, m = rest / P;
-            if (m >= G) continue;
-            const uint32_t mg = d.shard0 + m;
-            double n0, n1;
-            rng.normal2(SITE_LAMBDA, mg, j, pr, it, n0, n1);
-            double *o = const_cast<double *>(dr.NL) + ((size_t)mg * P + j) * K + 2 * pr;
-            o[0] = n0;
-            if (2 * pr + 1 < K) o[1] = n1;
-            continue;
-        }
-        x -= snl;
-        if (x < sgpsi) {                                   // dc:150, device layout [g][P][K], shape df/2 + 1/2
-            const uint32_t k = x % K, rest = x / K;
-            const uint32_t j = rest % P, m = rest / P;
-            if (m >= G) continue;
-            const uint32_t mg = d.shard0 + m;
-            const_cast<double *>(dr.Gpsi)[((size_t)mg * P + j) * K + k] = rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, mg, j, k, it);
-            continue;
-        }
-        x -= sgpsi;
-        if (x < sgps) {                                    // dc:170, P x g, shape as + n/2
-            const uint32_t j = x % P, m = x / P;
-            if (m >= G) continue;
-            const uint32_t mg = d.shard0 + m;
-            const_cast<double *>(dr.Gps)[(size_t)mg * P + j] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg, j, 0, it);
-            continue;
-        }
-        x -= sgps;
-        if (x < (uint32_t)d.g * K) {                       // dc:158,163, K x g, all shards
-            const uint32_t h = x % K, mg = x / K;
-            const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - (int)h);
-            const_cast<double *>(dr.Gdelta)[(size_t)mg * K + h] = rng.gamma(shape, SITE_DELTA, mg, 0, h, it);
-        }
+    const int b = blockIdx.x + (GAMMAS ? 0 : pl.b_gpsi), t = threadIdx.x, K = d.K;
+    if (GAMMAS) {
+    if (b < pl.b_gdel) {                               // dc:158,163 delta, K x g, all shards
+        const int x = b * 256 + t;
+        if (x >= d.g * K) return;
+        const int h = x % K, mg = x / K;
+        const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - h);
+        const_cast<double *>(dr.Gdelta)[(size_t)mg * K + h] = rng.gamma(shape, SITE_DELTA, (uint32_t)mg, 0, (uint32_t)h, it);
+        return;
+    }
+    if (b < pl.b_gps) {                                // dc:170 ps, P x g, shape as + n/2
+        const int bb = b - pl.b_gdel, m = bb / pl.nrb_s, j = (bb % pl.nrb_s) * 256 + t;
+        if (j >= d.P) return;
+        const uint32_t mg = (uint32_t)(d.shard0 + m);
+        const_cast<double *>(dr.Gps)[(size_t)mg * d.P + j] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg, (uint32_t)j, 0, it);
+        return;
+    }
+    if (b < pl.b_gpsi) {                               // dc:150 psi, device layout [g][P][K]
+        const int bb = b - pl.b_gps, m = bb / pl.nrb_g, rb = bb % pl.nrb_g;
+        const int sh = pl.lrg == 16 ? 4 : (pl.lrg == 32 ? 5 : 6);
+        const int j = rb * (256 / pl.lrg) + (t >> sh), lane = t & (pl.lrg - 1);
+        if (j >= d.P) return;
+        const uint32_t mg = (uint32_t)(d.shard0 + m);
+        double *o = const_cast<double *>(dr.Gpsi) + ((size_t)mg * d.P + j) * K;
+        const double shape = d.df * 0.5 + 0.5;
+        for (int k = lane; k < K; k += pl.lrg) o[k] = rng.gamma(shape, SITE_PSI, mg, (uint32_t)j, (uint32_t)k, it);
+        return;
+    }
+    return;
+    }
+    const int sh = pl.lrn == 16 ? 4 : (pl.lrn == 32 ? 5 : 6), lane = t & (pl.lrn - 1), rsub = t >> sh;
+    if (b < pl.b_nx) {                                 // dc:104 Z (K x n x g), dc:126 X (K x n)
+        const bool xs = b >= pl.b_nz;
+        const int bb = xs ? b - pl.b_nz : b - pl.b_gpsi;
+        const int m = xs ? 0 : bb / pl.nrb_n, rb = xs ? bb : bb % pl.nrb_n;
+        const int i = rb * (256 / pl.lrn) + rsub;
+        if (i >= d.n) return;
+        const uint32_t mg = xs ? 0u : (uint32_t)(d.shard0 + m);
+        double *o = xs ? const_cast<double *>(dr.NX) + (size_t)i * K
+                       : const_cast<double *>(dr.NZ) + ((size_t)mg * d.n + i) * K;
+        draw_normal_row(rng, xs ? SITE_X : SITE_Z, mg, (uint32_t)i, it, K, lane, pl.lrn, o);
+        return;
+    }
+    {                                                  // dc:142 Lambda (K x P x g)
+        const int bb = b - pl.b_nx, m = bb / pl.nrb_p, rb = bb % pl.nrb_p;
+        const int j = rb * (256 / pl.lrn) + rsub;
+        if (j >= d.P) return;
+        const uint32_t mg = (uint32_t)(d.shard0 + m);
+        draw_normal_row(rng, SITE_LAMBDA, mg, (uint32_t)j, it, K, lane, pl.lrn,
+                        const_cast<double *>(dr.NL) + ((size_t)mg * d.P + j) * K);
     }
 }
 
@@ -1371,10 +1386,9 @@ void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s) {
     hipLaunchKernelGGL(k_eta, dim3(grid), dim3(256), 0, s, d, b.X, b.Z, eta_out);
 }
 void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s) {
-    const DrawSeg sg = draw_segments(d);
-    const int64_t total = sg.nz + sg.nx + sg.nl + sg.gpsi + sg.gps + sg.gdel;
-    const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_draws, dim3(grid), dim3(256), 0, s, d, dr, iter);
+    const DrawPlan pl = draw_plan(d);
+    hipLaunchKernelGGL(k_draws<true>, dim3(pl.b_gpsi), dim3(256), 0, s, d, dr, iter);
+    hipLaunchKernelGGL(k_draws<false>, dim3(pl.total - pl.b_gpsi), dim3(256), 0, s, d, dr, iter);
 }
 void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,
                      int64_t count, double *out, hipStream_t s) {
