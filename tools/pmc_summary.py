@@ -61,5 +61,21 @@ for k in sorted(set(fetch) | set(write) | set(mops)):
         # MfmaUtil (rocprofv3 derived): busy cycles summed over SIMDs / (GUI_ACTIVE x SIMDs)
         e["mfma_busy_frac"] = busy[k][0] / (gui[k][0] * 1024)
     out[k] = e
+# wave-state pass (quad-cycle units): active / issue-stalled / parked shares of wave time
+wrows = load(base + "_waves")
+if wrows:
+    wc = {c: per_kernel(wrows, c) for c in ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+                                            "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU",
+                                            "SQ_INSTS_LDS")}
+    for k, (cyc, _) in wc["SQ_WAVE_CYCLES"].items():
+        if cyc <= 0 or k not in out:
+            continue
+        e = out[k]
+        e["waves_per_dispatch"] = wc["SQ_WAVES"].get(k, (0, 0))[0]
+        e["valu_insts_per_wave"] = wc["SQ_INSTS_VALU"].get(k, (0, 0))[0] / max(1.0, e["waves_per_dispatch"])
+        e["lds_insts_per_wave"] = wc["SQ_INSTS_LDS"].get(k, (0, 0))[0] / max(1.0, e["waves_per_dispatch"])
+        for c, name in (("SQ_ACTIVE_INST_ANY", "active_frac"), ("SQ_WAIT_INST_ANY", "issue_stall_frac"),
+                        ("SQ_WAIT_ANY", "parked_frac"), ("SQ_ACTIVE_INST_VALU", "valu_active_frac")):
+            e[name] = wc[c].get(k, (0, 0))[0] / cyc
 json.dump({"source": base, "kernels": out}, sys.stdout, indent=1)
 print()

@@ -14,4 +14,5 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_${TAG}_fetch -o run -- $BENCH > $OUT/prof_${TAG}_fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_${TAG}_write -o run -- $BENCH > $OUT/prof_${TAG}_write.log 2>&1 || { echo "write pass failed"; exit 1; }
 timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/prof_${TAG}_mfma -o run -- $BENCH > $OUT/prof_${TAG}_mfma.log 2>&1 || { echo "mfma pass failed"; exit 1; }
+timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $OUT/prof_${TAG}_waves -o run -- $BENCH > $OUT/prof_${TAG}_waves.log 2>&1 || { echo "waves pass failed"; exit 1; }
 echo "profile $TAG ok"
