@@ -695,7 +695,25 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
 // dcfm_set_state).  Every global load of the row is issued up front.
 // psi o lambda^2 of the row -> cpart[m][j][:] (k_colsum sums the rows).
 // ============================================================================
-__global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict__ C,
+// sum of v over this lane's 16-lane DPP row (quad_perm xor 1, xor 2, then row_ror 4, 8)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double rowsum16(double v) {
+    v += dpp_d<0xB1>(v);     // quad_perm [1,0,3,2]
+    v += dpp_d<0x4E>(v);     // quad_perm [2,3,0,1]
+    v += dpp_d<0x124>(v);    // row_ror:4
+    v += dpp_d<0x128>(v);    // row_ror:8
+    return v;
+}
+
+#ifndef DCFM_LAMBDA_MINWAVES
+#define DCFM_LAMBDA_MINWAVES 1
+#endif
+__global__ __launch_bounds__(64, DCFM_LAMBDA_MINWAVES) void k_lambda(Dims d, const double *__restrict__ C,
                                                const double *__restrict__ E,
                                                const double *__restrict__ yy,
                                                const double *__restrict__ tau_cur,
@@ -704,7 +722,8 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
                                                double *__restrict__ omega,
                                                double *__restrict__ cpart, DrawsDev dr,
                                                int64_t iter) {
-    __shared__ __attribute__((aligned(16))) double LP[4][P2STRIDE];
+    // per system: the current column pair (L[r][k], L[r][k+1]) of every row r, then x
+    __shared__ __attribute__((aligned(16))) double LS[4][2 * KP];
     const int m = blockIdx.y;
     const int mg = d.shard0 + m;
     const int lane = threadIdx.x, qw = lane >> 4, l = lane & 15;
@@ -713,20 +732,19 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
     const int jj = valid ? j : 0;
     const int r0 = l, r1 = l + 16;
     const bool rv0 = valid && r0 < d.K, rv1 = valid && r1 < d.K;
-    const size_t rowoff = ((size_t)m * d.PP + jj) * KP;
-    const int64_t ti = iter - dr.first_iter;
-    const size_t drow = ((size_t)ti * d.g + mg) * d.P + jj;
-    // ---- every global load up front
-    const double psj = valid ? ps[(size_t)m * d.PP + jj] : 0.0;
-    const double tr0 = rv0 ? tau_cur[(size_t)mg * KP + r0] : 0.0, tr1 = rv1 ? tau_cur[(size_t)mg * KP + r1] : 0.0;
+    // 32-bit element offsets (base + 32-bit VGPR offset addressing; every array here is
+    // < 2^31 elements at the supported sizes) keep the per-lane address state small
+    const uint32_t rowoff = (uint32_t)(m * d.PP + jj) * KP;
+    const uint32_t ti = (uint32_t)(iter - dr.first_iter);
+    const uint32_t drow = (ti * (uint32_t)d.g + (uint32_t)mg) * (uint32_t)d.P + (uint32_t)jj;
+    const uint32_t toff = (uint32_t)mg * KP;
+    // ---- loads that form Q_j and b_j
+    const double psj = valid ? ps[(uint32_t)(m * d.PP + jj)] : 0.0;
+    double tr0 = rv0 ? tau_cur[toff + r0] : 0.0, tr1 = rv1 ? tau_cur[toff + r1] : 0.0;
     const double *pin = plam_src ? plam_src : psi;
     const double pin0 = rv0 ? pin[rowoff + r0] : 0.0, pin1 = rv1 ? pin[rowoff + r1] : 0.0;
-    const double c0 = valid ? C[rowoff + r0] : 0.0, c1 = valid ? C[rowoff + r1] : 0.0;
-    const double z0 = rv0 ? dr.NL[drow * d.K + r0] : 0.0, z1 = rv1 ? dr.NL[drow * d.K + r1] : 0.0;       // dc:142
-    const double G0 = rv0 ? dr.Gpsi[drow * d.K + r0] : 0.0, G1 = rv1 ? dr.Gpsi[drow * d.K + r1] : 0.0;   // dc:150
-    const double Gps = (valid && l == 0) ? dr.Gps[((size_t)ti * d.g + mg) * d.P + jj] : 0.0;           // dc:170
-    const double yyj = (valid && l == 0) ? yy[(size_t)m * d.PP + jj] : 0.0;
-    const double *Ea = E + ((size_t)m * KP + r0) * KP, *Eb = E + ((size_t)m * KP + r1) * KP;
+    double c0 = valid ? C[rowoff + r0] : 0.0, c1 = valid ? C[rowoff + r1] : 0.0;
+    const double *Ea = E + ((uint32_t)m * KP + r0) * KP, *Eb = E + ((uint32_t)m * KP + r1) * KP;
     constexpr int KH = KP / 2;       // rows < 16 only ever touch columns < 16 (lower triangle)
     double qa[KH], qb[KP];
 #pragma unroll
@@ -750,9 +768,11 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
         }
     }
     double bva = psj * c0, bvb = psj * c1;        // blam = ps_j eta' Y_j (dc:141)
-    double va = 0.0, vb = 0.0;
-    double *Lp = LP[qw];
-    // ---- factorisation, two pivots per step, forward solve fused
+    double va = 0.0, vb = 0.0;                    // v = L^{-1} blam (dc:143), rows r0, r1
+    double ia = 0.0, ib = 0.0;                    // 1 / L[r][r], rows r0, r1
+    double *Ls = LS[qw];
+    // ---- factorisation, two pivots per step, forward solve fused; the pair's L
+    //      column goes through the LDS staging row Ls (overwritten every step)
     static_for<KP / 2>([&](auto JC) {
         constexpr int jp = decltype(JC)::value, k = 2 * jp;
         double a, b, c2, bk, bk1;
@@ -775,7 +795,7 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
         const double i11 = rsqrt_f64(d11);
         const double l11 = d11 * i11;
         const double v0 = bk * i00, v1 = (bk1 - l10 * v0) * i11;
-        auto rowpiv = [&](auto &q, int r, double &bv, double &vr, double &lr0, double &lr1) {
+        auto rowpiv = [&](auto &q, int r, double &bv, double &vr, double &ir, double &lr0, double &lr1) {
             if (r > k + 1) {
                 lr0 = q[k] * i00;
                 lr1 = (q[k + 1] - lr0 * l10) * i11;
@@ -795,28 +815,25 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
                 d2 v;
                 v.x = lr0;
                 v.y = lr1;
-                *reinterpret_cast<d2 *>(Lp + pb2(jp) + 2 * (r - k)) = v;
+                *reinterpret_cast<d2 *>(Ls + 2 * r) = v;
             }
-            if (r == k) {
-                d2 v;
-                v.x = i00;
-                v.y = i11;
-                *reinterpret_cast<d2 *>(Lp + PACK2 + k) = v;
-                vr = v0;
-            }
-            if (r == k + 1) vr = v1;
+            if (r == k) { vr = v0; ir = i00; }
+            if (r == k + 1) { vr = v1; ir = i11; }
             if (r > k + 1) bv = fma(-lr1, v1, fma(-lr0, v0, bv));
         };
         double la0 = 0.0, la1 = 0.0, lb0, lb1;
-        if constexpr (k < 16) rowpiv(qa, r0, bva, va, la0, la1);
-        rowpiv(qb, r1, bvb, vb, lb0, lb1);
+        if constexpr (k < 16) rowpiv(qa, r0, bva, va, ia, la0, la1);
+        rowpiv(qb, r1, bvb, vb, ib, lb0, lb1);
 #pragma unroll
         for (int c = k + 2; c < KP; ++c) {
-            const d2 lc = *reinterpret_cast<const d2 *>(Lp + pb2(jp) + 2 * (c - k));
+            const d2 lc = *reinterpret_cast<const d2 *>(Ls + 2 * c);
             if constexpr (k < 16) {
                 if (c < KH) qa[c < KH ? c : 0] = fma(-la1, lc.y, fma(-la0, lc.x, qa[c < KH ? c : 0]));
             }
             qb[c] = fma(-lb1, lc.y, fma(-lb0, lc.x, qb[c]));
+#ifdef DCFM_LAMBDA_CHUNK
+            if ((c - k - 2) % DCFM_LAMBDA_CHUNK == DCFM_LAMBDA_CHUNK - 1) __builtin_amdgcn_sched_barrier(0);   // bound the hoisted reads
+#endif
         }
 #pragma unroll
         for (int c = k + 2; c < KP; ++c) {
@@ -824,46 +841,70 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
             asm volatile("" : "+v"(qb[c]));
         }
     });
-    // ---- back solve L' x = w, w = v + z (dc:142-144), two rows per step from the bottom
-    double wa = va + z0, wb = vb + z1;
+    // ---- the rest of the row's inputs (their latency hides under other waves' factorisations)
+    const uint32_t dk = drow * (uint32_t)d.K;
+    const double z0 = rv0 ? dr.NL[dk + r0] : 0.0, z1 = rv1 ? dr.NL[dk + r1] : 0.0;       // dc:142
+    const double G0 = rv0 ? dr.Gpsi[dk + r0] : 0.0, G1 = rv1 ? dr.Gpsi[dk + r1] : 0.0;   // dc:150
+    const double Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;                           // dc:170
+    const double yyj = (valid && l == 0) ? yy[(uint32_t)(m * d.PP + jj)] : 0.0;
+    {   // C and tau again from L2 rather than held across the factorisation
+        const double *C2 = C, *T2 = tau_cur;
+        asm volatile("" : "+s"(C2), "+s"(T2));
+        c0 = valid ? C2[rowoff + r0] : 0.0;
+        c1 = valid ? C2[rowoff + r1] : 0.0;
+        tr0 = rv0 ? T2[toff + r0] : 0.0;
+        tr1 = rv1 ? T2[toff + r1] : 0.0;
+    }
+    // ---- back solve L' x = w, w = v + z (dc:142-144), pivots (c, c-1) from the bottom.
+    //      x_c = (w_c - sum_{r>c} L[r][c] x_r) / L[c][c]: the sums over the rows below are
+    //      dot products across the 16 lanes (rowsum16); L stays in the lanes' registers.
+    const double wa = va + z0, wb = vb + z1;
     double xa = 0.0, xb = 0.0;
-    const int bra = pb2(r0 >> 1) - 2 * (r0 & ~1) + (r0 & 1);   // L[c][r0] at bra + 2c
-    const int brb = pb2(r1 >> 1) - 2 * (r1 & ~1) + (r1 & 1);
     static_for<KP / 2>([&](auto JC) {
-        constexpr int c = KP - 1 - 2 * decltype(JC)::value;     // pivots c, c-1
-        const double wc = (c >= 16) ? bcast16<(c >= 16 ? c - 16 : 0)>(wb) : bcast16<(c < 16 ? c : 0)>(wa);
-        const double wc1 = (c - 1 >= 16) ? bcast16<(c - 1 >= 16 ? c - 17 : 0)>(wb) : bcast16<(c - 1 < 16 ? c - 1 : 0)>(wa);
-        const d2 dd = *reinterpret_cast<const d2 *>(Lp + PACK2 + c - 1);   // {1/L[c-1][c-1], 1/L[c][c]}
-        const double xc = wc * dd.y;
-        const double lcc1 = Lp[pb2((c - 1) >> 1) + 2 * (c - ((c - 1) & ~1)) + ((c - 1) & 1)];
-        const double xc1 = (wc1 - lcc1 * xc) * dd.x;
-        if constexpr (c >= 16) {
-            if (r1 == c) xb = xc;
-            if (r1 == c - 1) xb = xc1;
-            if (r1 < c - 1) wb = fma(-Lp[brb + 2 * (c - 1)], xc1, fma(-Lp[brb + 2 * c], xc, wb));
+        constexpr int c = KP - 1 - 2 * decltype(JC)::value;     // odd: rows c, c-1 on the same side of 16
+        double pa = 0.0, pb = 0.0;
+        if constexpr (c < 16) {
+            if (r0 > c) { pa = qa[c < 16 ? c : 0] * xa; pb = qa[c < 16 ? c - 1 : 0] * xa; }
         }
-        if (r0 == c) xa = xc;
-        if (r0 == c - 1) xa = xc1;
-        if (r0 < c - 1) wa = fma(-Lp[bra + 2 * (c - 1)], xc1, fma(-Lp[bra + 2 * c], xc, wa));
+        pa = fma(qb[c], xb, pa);                  // r1 > c for c < 16; below the row for c >= 16
+        pb = fma(qb[c - 1], xb, pb);
+        if constexpr (c >= 16) {
+            if (r1 <= c) { pa = 0.0; pb = 0.0; }
+        }
+        pa = rowsum16(pa);
+        pb = rowsum16(pb);
+        double t = 0.0;
+        if constexpr (c >= 16) {
+            if (r1 == c) { xb = (wb - pa) * ib; t = qb[c - 1] * xb; }
+            const double tb = bcast16<(c >= 16 ? c - 16 : 0)>(t);
+            if (r1 == c - 1) xb = (wb - pb - tb) * ib;
+        } else {
+            if (r0 == c) { xa = (wa - pa) * ia; t = qa[c < 16 ? c - 1 : 0] * xa; }
+            const double tb = bcast16<(c < 16 ? c : 0)>(t);
+            if (r0 == c - 1) xa = (wa - pb - tb) * ia;
+        }
     });
     if (!rv0) xa = 0.0;
     if (!rv1) xb = 0.0;
-    // ---- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr  (x through the LDS scratch slots)
-    Lp[PACK2 + KP + r0] = xa;
-    Lp[PACK2 + KP + r1] = xb;
+    // ---- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr  (x through the staging row)
+    Ls[r0] = xa;
+    Ls[r1] = xb;
     double exa = 0.0, exb = 0.0;
+    // re-read the E rows from L2 (laundered pointers: keeping the first read's 48 doubles
+    // live across the factorisation would cost ~96 VGPRs)
+    const double *Ea2 = Ea, *Eb2 = Eb;
+    asm volatile("" : "+v"(Ea2), "+v"(Eb2));
 #pragma unroll
     for (int c = 0; c < KP; c += 2) {
-        const d2 ea = *reinterpret_cast<const d2 *>(Ea + c), eb = *reinterpret_cast<const d2 *>(Eb + c);
-        const d2 xv = *reinterpret_cast<const d2 *>(Lp + PACK2 + KP + c);
+        const d2 ea = *reinterpret_cast<const d2 *>(Ea2 + c), eb = *reinterpret_cast<const d2 *>(Eb2 + c);
+        const d2 xv = *reinterpret_cast<const d2 *>(Ls + c);
         exa += ea.x * xv.x;
         exa += ea.y * xv.y;
         exb += eb.x * xv.x;
         exb += eb.y * xv.y;
     }
     double contrib = xa * (exa - 2.0 * c0) + xb * (exb - 2.0 * c1);
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) contrib += __shfl_xor(contrib, o, 16);
+    contrib = rowsum16(contrib);
     // ---- psi (dc:150, tau of the previous iteration, Q11) and the outputs
     double psa = 0.0, psb = 0.0;
     if (rv0) psa = (1.0 / (d.df * 0.5 + 0.5 * (xa * xa * tr0))) * G0;
@@ -878,8 +919,8 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
         if (l == 0) {
             const double SS = yyj + contrib;
             const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;   // dc:170
-            ps[(size_t)m * d.PP + j] = psn;
-            omega[(size_t)m * d.PP + j] = 1.0 / psn;            // dc:171 (Q1)
+            ps[(uint32_t)(m * d.PP + j)] = psn;
+            omega[(uint32_t)(m * d.PP + j)] = 1.0 / psn;        // dc:171 (Q1)
         }
     }
 }
