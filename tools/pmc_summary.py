@@ -3,7 +3,10 @@
 HBM bytes per dispatch: FETCH_SIZE (KiB) x 1024 x 2 — the gfx950 correction of
 /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts exactly
 half of the bytes of a wide (16 B/lane) coalesced read — and WRITE_SIZE (KiB) x
-1024 as is.  Both include Infinity-Cache hits (memory-side requests), so on a
+1024 as is.  Calibrated here for the widths these kernels use (tools/calib/
+calib_fetch.hip, 2 GiB streamed, profiles/r01_fetch_calibration.txt): 8 B/lane and
+16 B/lane coalesced reads both report 0.500 of their bytes, 8 B/lane and 16 B/lane
+stores 1.000 — so the x2 / x1 corrections hold for every kernel in this library.  Both include Infinity-Cache hits (memory-side requests), so on a
 working set that stays MALL-resident they are an upper bound on HBM traffic.
 fp64 MFMA flops: SQ_INSTS_VALU_MFMA_MOPS_F64 x 512.
 Usage: python tools/pmc_summary.py gpurun_out/prof_TAG > profiles/..._pmc.json
