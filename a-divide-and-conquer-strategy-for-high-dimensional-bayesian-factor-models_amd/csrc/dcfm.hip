@@ -240,7 +240,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     d.as_ = c.as_; d.bs = c.bs; d.df = c.df; d.ad1 = c.ad1; d.bd1 = c.bd1; d.ad2 = c.ad2; d.bd2 = c.bd2;
     d.seed = c.seed;
     d.inject = (c.flags & DCFM_FLAG_INJECT_DRAWS) ? 1 : 0;
-    h->B = c.asm_batch > 0 ? c.asm_batch : 16;
+    h->B = c.asm_batch > 0 ? c.asm_batch : 32;
 
     Bufs &b = h->b;
     const size_t G = d.G, NP = d.NP, PP = d.PP, g = d.g, p = d.p, KP = d.kp;

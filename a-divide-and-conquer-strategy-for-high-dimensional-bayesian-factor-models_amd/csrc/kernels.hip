@@ -1090,8 +1090,10 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
                                                      double inv_eff, const int2 *__restrict__ tiles,
                                                      double *__restrict__ Sig) {
     __shared__ double As[2][AKC][ALD], Bs[2][AKC][ALD];
+    __shared__ int shard_of[2][ASM_TILE];      // shard of the tile's rows / columns (epilogue coef)
     const int2 T = tiles[xcd_remap(blockIdx.x, gridDim.x)];
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    shard_of[t >> 7][t & 127] = ((t < ASM_TILE ? T.x : T.y) * ASM_TILE + (t & 127)) / d.P;
     const int r = lane & 15, q = lane >> 4;
     const int p = d.p;
     const int wa = (wave >> 1) * 64, wb = (wave & 1) * 64;
@@ -1146,22 +1148,39 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
         if (more) lstore(buf ^ 1);
         __syncthreads();
     }
+    // epilogue: lower-triangle read-modify-write of the tile, loads issued together
+    // (predicated, no branches around them), shard test from the LDS table
     const int a0 = T.x * ASM_TILE + wa, b0 = T.y * ASM_TILE + wb;
+    int sb[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) sb[v] = shard_of[1][wb + 16 * v + r];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
+        double old[4][4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int a = a0 + 16 * u + q + 4 * g;
-            if (a >= p) continue;
-            const int sa = a / d.P;
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
                 const int b = b0 + 16 * v + r;
-                if (b > a || b >= p) continue;
-                const double coef = (b / d.P == sa) ? 1.0 : d.rho;
-                double val = coef * acc[u][v][g] * inv_eff;
-                if (a == b) val += wsum[a] * inv_eff;
-                Sig[(size_t)a * p + b] += val;
+                const bool live = a < p && b <= a;
+                old[g][v] = live ? Sig[(size_t)a * p + b] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int a = a0 + 16 * u + q + 4 * g;
+            const int sa = shard_of[0][wa + 16 * u + q + 4 * g];
+            const double dg = (a < p) ? wsum[a] * inv_eff : 0.0;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int b = b0 + 16 * v + r;
+                if (a < p && b <= a) {
+                    const double coef = (sb[v] == sa) ? 1.0 : d.rho;
+                    double val = coef * acc[u][v][g] * inv_eff;
+                    if (a == b) val += dg;
+                    Sig[(size_t)a * p + b] = old[g][v] + val;
+                }
             }
         }
     }

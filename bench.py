@@ -103,7 +103,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--thin", type=int, default=5)
-    ap.add_argument("--asm-batch", type=int, default=16)
+    ap.add_argument("--asm-batch", type=int, default=32)
     ap.add_argument("--g", type=int, default=64)
     ap.add_argument("--P", type=int, default=312)
     ap.add_argument("--n", type=int, default=1000)

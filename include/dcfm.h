@@ -67,7 +67,7 @@ typedef struct {
     int32_t rank;       /* this rank                                             */
     int32_t device;     /* HIP device ordinal this handle runs on                */
     uint32_t flags;     /* DCFM_FLAG_*                                           */
-    int32_t asm_batch;  /* saved samples per covariance-assembly flush (0 = 16)  */
+    int32_t asm_batch;  /* saved samples per covariance-assembly flush (0 = 32)  */
     int32_t reserved[7];
 } dcfm_config;
 
