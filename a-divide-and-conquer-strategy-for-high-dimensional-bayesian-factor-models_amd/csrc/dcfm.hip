@@ -38,6 +38,7 @@ struct dcfm_handle {
     hipEvent_t e_lam = nullptr, e_prep = nullptr, e_xchol = nullptr, e_batch = nullptr,
                e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
+    bool prep_valid = false;      // fused path: A / ZM hold the next iteration's Z operators
     bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
     int lb = 0;                   // Lb buffer being filled
@@ -267,10 +268,10 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     ALLOC(b.xa, KP * KP);
     ALLOC(b.xa_all, (size_t)nranks * KP * KP);
     ALLOC(b.XM, 2 * KP * KP);
-    ALLOC(b.xpart, (G + 7) / 8 * KP * KP);
+    ALLOC(b.xpart, 8 * KP * KP);          // k_deltaops: min(8, G) chunk sums
     {
         double *tk = nullptr;
-        ALLOC(tk, (G + 7) / 8 + 1);
+        ALLOC(tk, 1);
         b.ticket = reinterpret_cast<unsigned *>(tk);
     }
     ALLOC(b.C, G * PP * KP);
@@ -487,6 +488,7 @@ int dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s) {
     k_to_dev(d, s->delta, v);   if ((rc = up(h, h->b.delta, v))) return rc;
     k_to_dev(d, s->tauh, v);    if ((rc = up(h, h->b.tau, v))) return rc;
     h->plam_valid = true;
+    h->prep_valid = false;
     h->have_state = true;
     return DCFM_OK;
 }
@@ -627,7 +629,8 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     const int64_t end_iter = first_iter + n_iter;
     // one rank, K <= 32: prep and the X operators ride inside k_wprep / k_zxchol on the
     // main stream; otherwise they run on the side stream (with the xa all-gather)
-    const bool fused = d.nranks == 1 && d.kp == KP;
+    static const bool nofuse = [] { const char *e = std::getenv("DCFM_NOFUSE"); return e && e[0] == '1'; }();
+    const bool fused = d.nranks == 1 && d.kp == KP && !nofuse;
     // generated draws: batches [b0, b0 + DB) aligned to this call's first iteration,
     // queued on sdraw into a slot whose previous batch the sweep has finished with
     int rc_gen = DCFM_OK;
@@ -669,6 +672,11 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     int64_t batch0 = first_iter, batch_n = 0;
     if (!fused) {
         HIPC(h, hipEventRecord(h->e_lam, s));      // Lambda/omega of the previous iteration are final
+        h->prep_valid = false;
+    } else if (!h->prep_valid) {                   // operators of first_iter from the state as set
+        KTimer t(h, DCFM_K_PREP, s);
+        launch_colgram(d, b, false, s);
+        launch_deltaops(d, b, h->dr, first_iter, false, nullptr, nullptr, nullptr, nullptr, s);
     }
     for (int64_t it = first_iter; it < end_iter; ++it) {
         if (!d.inject && (it == first_iter || it == batch0 + batch_n)) {
@@ -681,7 +689,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         }
         const DrawsDev &dr = d.inject ? h->dr : h->gen[slot];
         if (fused) {
-            { KTimer t(h, DCFM_K_WPASS, s); launch_wprep(d, b, s); }
+            { KTimer t(h, DCFM_K_WPASS, s); launch_wpass(d, b, s); }
             { KTimer t(h, DCFM_K_ZDRAW, s); launch_zxchol(d, b, dr, it, s); }
             { KTimer t(h, DCFM_K_XRED, s);  launch_xred(d, b, s); }
         } else {
@@ -714,16 +722,26 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s);
         }
         h->plam_valid = false;
-        if (!fused) HIPC(h, hipEventRecord(h->e_lam, s));
-        { KTimer t(h, DCFM_K_COLSUM, s); launch_colsum(d, b, s); }
-        if (d.nranks > 1) {
-            KTimer t(h, DCFM_K_COMM, s);
-            NCCLC(h, ncclAllGather(b.sloc, b.sall, (size_t)d.G * KW, ncclDouble, h->comm, s));
-        }
-        {
-            KTimer t(h, DCFM_K_DELTA, s);
-            launch_delta(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
-                         b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);
+        if (fused) {   // + the next iteration's grams and Z operators
+            { KTimer t(h, DCFM_K_COLSUM, s); launch_colgram(d, b, true, s); }
+            {
+                KTimer t(h, DCFM_K_DELTA, s);
+                launch_deltaops(d, b, dr, it, true, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);
+            }
+            h->prep_valid = true;
+        } else {
+            HIPC(h, hipEventRecord(h->e_lam, s));
+            { KTimer t(h, DCFM_K_COLSUM, s); launch_colsum(d, b, s); }
+            if (d.nranks > 1) {
+                KTimer t(h, DCFM_K_COMM, s);
+                NCCLC(h, ncclAllGather(b.sloc, b.sall, (size_t)d.G * KW, ncclDouble, h->comm, s));
+            }
+            {
+                KTimer t(h, DCFM_K_DELTA, s);
+                launch_delta(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+                             b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);
+            }
         }
         if (!d.inject && it == batch0 + batch_n - 1) {      // the batch's last consumer is queued
             HIPC(h, hipEventRecord(h->e_used[slot], s));

@@ -56,8 +56,8 @@ struct Bufs {
     double *W, *A, *ZM, *Sp, *xin, *xall, *C, *E, *cpart, *sloc, *sall;
     double *Lb[2], *wsum[2], *Sigma;
     double *xa, *xa_all, *XM;          // per-rank sum of A, gathered sums, X-draw operators
-    double *xpart;                     // k_wprep group sums of A (ceil(G/8) x KP x KP)
-    unsigned *ticket;                  // k_wprep last-arrival tickets (0 between launches)
+    double *xpart;                     // k_deltaops chunk sums of A (8 x KP x KP)
+    unsigned *ticket;                  // k_deltaops last-arrival ticket (0 between launches)
     int2 *tiles;
     int ntiles, LDB;
 };
@@ -67,8 +67,11 @@ void launch_prep(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s);
-// fused one-rank narrow launches: k_prep + k_wpass, k_asum/k_xchol + k_zdraw
-void launch_wprep(const Dims &d, const Bufs &b, hipStream_t s);
+// fused one-rank narrow launches (kernels.hip: k_colgram, k_deltaops, k_zxchol)
+void launch_colgram(const Dims &d, const Bufs &b, bool colsum, hipStream_t s);
+void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool delta,
+                     const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
+                     hipStream_t s);
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_asum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);

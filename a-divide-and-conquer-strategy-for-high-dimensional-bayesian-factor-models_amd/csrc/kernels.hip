@@ -58,13 +58,13 @@ namespace dcfm {
 // ZM[m] = {M1, M2, U, NA}.  4 waves split the j reduction of A (fp64 MFMA 2x2 tiles).
 // ============================================================================
 constexpr int PREP_SMEM = 4 * KP * (KP + 1) + 3 * TS16;
-__device__ __forceinline__ void prep_shard(const Dims &d, const double *__restrict__ Lam,
-                                           const double *__restrict__ omega, double *__restrict__ A,
-                                           double *__restrict__ ZM, int m, double *smem) {
+// prep_gram: A_m (to HBM and LDS part[0]), NA, and Zprec's upper triangle into the
+// lower triangle of part[2]; prep_ops: the Z-draw operators from the LDS image.
+__device__ __forceinline__ void prep_gram(const Dims &d, const double *__restrict__ Lam,
+                                          const double *__restrict__ omega, double *__restrict__ A,
+                                          double *__restrict__ ZM, int m, double *smem) {
     // partial A per wave; later A, U, Zprec/T, scratch
     double (*part)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);
-    double *lds_l = smem + 4 * KP * (KP + 1), *lds_u = lds_l + 2 * TS16;
-    PHASE_T0();
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const int r = lane & 15, q = lane >> 4;
     const double *L = Lam + (size_t)m * d.PP * KP;
@@ -90,9 +90,7 @@ __device__ __forceinline__ void prep_shard(const Dims &d, const double *__restri
         part[wave][16 + a][r] = a10[g];
         part[wave][16 + a][16 + r] = a11[g];
     }
-    PHASE(0);
     __syncthreads();
-    PHASE(1);
     double *Am = A + (size_t)m * KP * KP;
     double *Zm = ZM + (size_t)m * 4 * KP * KP;
     double av[4];
@@ -100,7 +98,7 @@ __device__ __forceinline__ void prep_shard(const Dims &d, const double *__restri
     for (int u = 0; u < 4; ++u) {
         const int e = t + 256 * u, a = e / KP, b = e % KP;
         av[u] = (part[0][a][b] + part[1][a][b]) + (part[2][a][b] + part[3][a][b]);
-        __hip_atomic_store(Am + e, av[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // read by shard_sum_tree
+        Am[e] = av[u];
         Zm[3 * KP * KP + e] = -d.s1r * av[u];                       // NA
     }
     __syncthreads();
@@ -113,6 +111,29 @@ __device__ __forceinline__ void prep_shard(const Dims &d, const double *__restri
         if (a <= b) part[2][b][a] = (a == b ? 1.0 : 0.0) + (1.0 - d.rho) * av[u];
     }
     __syncthreads();
+}
+
+// the LDS image prep_gram leaves, from A_m in HBM (the operators run in a later launch)
+__device__ __forceinline__ void prep_load(const Dims &d, const double *__restrict__ A, int m, double *smem) {
+    double (*part)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);
+    const double *Am = A + (size_t)m * KP * KP;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int e = threadIdx.x + 256 * u;
+        const int a = e / KP, b = e % KP;
+        const double v = Am[e];
+        part[0][a][b] = v;
+        if (a <= b) part[2][b][a] = (a == b ? 1.0 : 0.0) + (1.0 - d.rho) * v;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void prep_ops(const Dims &d, double *__restrict__ ZM, int m, double *smem) {
+    double (*part)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);
+    double *lds_l = smem + 4 * KP * (KP + 1), *lds_u = lds_l + 2 * TS16;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    double *Zm = ZM + (size_t)m * 4 * KP * KP;
+    PHASE_T0();
     if (wave == 0) {                                                // U = L^{-1} -> part[1]
         PHASE(2);
         chol_inv32(part[2], part[1], part[3], lds_l, lds_u, lane);
@@ -141,6 +162,13 @@ __device__ __forceinline__ void prep_shard(const Dims &d, const double *__restri
     }
     PHASE(5);
     PHASE_END_AT(8);
+}
+
+__device__ __forceinline__ void prep_shard(const Dims &d, const double *__restrict__ Lam,
+                                           const double *__restrict__ omega, double *__restrict__ A,
+                                           double *__restrict__ ZM, int m, double *smem) {
+    prep_gram(d, Lam, omega, A, ZM, m, smem);
+    prep_ops(d, ZM, m, smem);
 }
 
 __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__ Lam,
@@ -414,101 +442,6 @@ __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict_
         for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * KP * KP + e];
         xprec_store(d, smem, e, v);
     }
-    __syncthreads();
-    xchol_factor(d, XM, smem);
-}
-
-// ============================================================================
-// Fused single-stream launches (one rank, K <= 32): the side-stream hops they
-// replace cost ~6 us of event latency each on the critical path.
-// k_wprep:  blocks [0, G) = k_prep shards (dispatched first) + the shard sum xa of A
-//           (shard_sum_tree), the rest k_wpass tiles.
-// k_zxchol: block 0 forms the X-draw operators from xa (k_xchol); the rest are k_zdraw tiles.
-// ============================================================================
-// xa = sum_m A_m over the local shards as a fixed two-level tree (groups of 8 shards in
-// shard order, then the groups in order), run by whichever prep blocks finish last:
-// after its A_m is out (device-scope release), a block takes a ticket for its group;
-// the last of the group sums the group into gpart, takes a ticket for the root, and the
-// last group-summer adds the group sums into xa.  No block waits on another.
-// The exchanged values (A_m, group sums) are written and read with agent-scope relaxed
-// atomics (sc1: coherent across the XCDs' L2s without write-back / invalidate), so the
-// hand-off needs only the stores' completion before the ticket — not __threadfence,
-// whose buffer_wbl2 / buffer_inv would flush and drop the wpass tiles' L2 contents.
-constexpr int SUM_GROUP = 8;
-__device__ __forceinline__ void st_agent(double *p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_agent(const double *p) {
-    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool last_arrival(unsigned *ticket, unsigned count, double *smem) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this thread's agent-scope stores are done
-    __syncthreads();
-    unsigned *flag = reinterpret_cast<unsigned *>(smem);
-    if (threadIdx.x == 0) {
-        const bool last =
-            __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == count - 1;
-        if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
-        *flag = last ? 1u : 0u;
-    }
-    __syncthreads();
-    const bool last = *flag != 0u;
-    __syncthreads();
-    return last;
-}
-__device__ __forceinline__ void shard_sum_tree(const Dims &d, const double *__restrict__ A,
-                                               double *__restrict__ gpart, unsigned *__restrict__ tickets,
-                                               double *__restrict__ xa, int m, double *smem) {
-    const int ng = (d.G + SUM_GROUP - 1) / SUM_GROUP, grp = m / SUM_GROUP;
-    const int g0 = grp * SUM_GROUP, g1 = min(d.G, g0 + SUM_GROUP);
-    if (!last_arrival(tickets + grp, (unsigned)(g1 - g0), smem)) return;
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < KP * KP / 256; ++u) {
-        const int e = t + 256 * u;
-        double v = 0.0;
-#pragma unroll 8
-        for (int mm = g0; mm < g1; ++mm) v += ld_agent(A + (size_t)mm * KP * KP + e);
-        st_agent(gpart + (size_t)grp * KP * KP + e, v);
-    }
-    if (!last_arrival(tickets + ng, (unsigned)ng, smem)) return;
-#pragma unroll
-    for (int u = 0; u < KP * KP / 256; ++u) {
-        const int e = t + 256 * u;
-        double v = 0.0;
-        for (int gg = 0; gg < ng; ++gg) v += ld_agent(gpart + (size_t)gg * KP * KP + e);
-        xa[e] = v;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_wprep(Dims d, const double *__restrict__ Y,
-                                               const double *__restrict__ Lam,
-                                               const double *__restrict__ omega, double *__restrict__ W,
-                                               double *__restrict__ A, double *__restrict__ ZM,
-                                               double *__restrict__ gpart, unsigned *__restrict__ tickets,
-                                               double *__restrict__ xa) {
-    __shared__ double smem[PREP_SMEM];
-    if ((int)blockIdx.x < d.G) {
-        prep_shard(d, Lam, omega, A, ZM, blockIdx.x, smem);
-        shard_sum_tree(d, A, gpart, tickets, xa, blockIdx.x, smem);
-        return;
-    }
-    const int vb = blockIdx.x - d.G;
-    wpass_tile<KP>(d, Y, Lam, omega, W, xcd_remap(vb, gridDim.x - d.G), 0);
-}
-
-constexpr int ZX_SMEM = ZDRAW_SMEM > XCHOL_SMEM ? ZDRAW_SMEM : XCHOL_SMEM;
-__global__ __launch_bounds__(256) void k_zxchol(Dims d, const double *__restrict__ W,
-                                                const double *__restrict__ ZM, const double *__restrict__ X,
-                                                double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
-                                                int64_t iter, const double *__restrict__ xa,
-                                                double *__restrict__ XM) {
-    __shared__ double smem[ZX_SMEM];
-    if (blockIdx.x > 0) {
-        zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blockIdx.x - 1, gridDim.x - 1), smem);
-        return;
-    }
-    for (int e = threadIdx.x; e < KP * KP; e += 256) xprec_store(d, smem, e, xa[e]);
     __syncthreads();
     xchol_factor(d, XM, smem);
 }
@@ -930,9 +863,10 @@ __global__ __launch_bounds__(64, DCFM_LAMBDA_MINWAVES) void k_lambda(Dims d, con
 // block = (shard m, 32 columns); 8 row groups x 4 independent accumulators each.
 // ============================================================================
 template <int KW>
-__global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict__ cpart, double *__restrict__ sloc) {
-    __shared__ double part[8][32];
-    const int m = blockIdx.x, k = 32 * blockIdx.y + (threadIdx.x & 31), grp = threadIdx.x >> 5;
+__device__ __forceinline__ void colsum_tile(const Dims &d, const double *__restrict__ cpart,
+                                            double *__restrict__ sloc, int m, int kt, double *smem) {
+    double (*part)[32] = reinterpret_cast<double (*)[32]>(smem);
+    const int k = 32 * kt + (threadIdx.x & 31), grp = threadIdx.x >> 5;
     const double *cp = cpart + (size_t)m * d.PP * KW + k;
     double s4[4] = {0.0, 0.0, 0.0, 0.0};
     int j = grp;
@@ -950,23 +884,10 @@ __global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict
         sloc[(size_t)m * KW + k] = tt;
     }
 }
-
-// ============================================================================
-__global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict__ cpart,
-                                                double *__restrict__ sloc) {
-    __shared__ double part[8][KP];
-    const int m = blockIdx.x, k = threadIdx.x & 31, grp = threadIdx.x >> 5;
-    const int nb = (d.P + 7) >> 3;
-    double s = 0.0;
-    for (int b = grp; b < nb; b += 8) s += cpart[((size_t)m * (d.PP >> 3) + b) * KP + k];
-    part[grp][k] = s;
-    __syncthreads();
-    if (threadIdx.x < KP) {
-        double t = 0.0;
-#pragma unroll
-        for (int g2 = 0; g2 < 8; ++g2) t += part[g2][threadIdx.x];
-        sloc[(size_t)m * KP + threadIdx.x] = t;
-    }
+template <int KW>
+__global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict__ cpart, double *__restrict__ sloc) {
+    __shared__ double smem[8 * 32];
+    colsum_tile<KW>(d, cpart, sloc, blockIdx.x, blockIdx.y, smem);
 }
 
 // ============================================================================
@@ -996,15 +917,11 @@ __device__ __forceinline__ double delta_chain(const Dims &d, int l, double T, do
     return dnew;
 }
 
-__global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__ sall,
-                                               const double *__restrict__ delta_in,
-                                               const double *__restrict__ tau_in,
-                                               double *__restrict__ delta_out,
-                                               double *__restrict__ tau_out,
-                                               DrawsDev dr,
-                                               int64_t iter) {
-    const int m = blockIdx.x;   // global shard
-    const int t = threadIdx.x;
+// one wave = one global shard m, lane l
+__device__ __forceinline__ void delta_shard(const Dims &d, const double *__restrict__ sall,
+                                            const double *__restrict__ delta_in, const double *__restrict__ tau_in,
+                                            double *__restrict__ delta_out, double *__restrict__ tau_out,
+                                            const DrawsDev &dr, int64_t iter, int m, int t) {
     if (t < 64) {
         const int l = t;
         const int lk = l < KP ? l : 0;
@@ -1050,6 +967,136 @@ __global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__
             }
         }
     }
+}
+
+__global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__ sall,
+                                               const double *__restrict__ delta_in,
+                                               const double *__restrict__ tau_in,
+                                               double *__restrict__ delta_out,
+                                               double *__restrict__ tau_out,
+                                               DrawsDev dr,
+                                               int64_t iter) {
+    delta_shard(d, sall, delta_in, tau_in, delta_out, tau_out, dr, iter, blockIdx.x, threadIdx.x);
+}
+
+// ============================================================================
+// Fused single-stream launches (one rank, K <= 32).  Cross-stream event hand-offs
+// cost ~6 us each on the critical path, and latency-bound work slows ~2x when it
+// shares CUs with the MFMA-bound Y passes, so the small per-shard K x K work rides
+// in the launches that leave the GPU idle, and the X operators in front of a Y pass:
+//   k_colgram:  blocks [0, G) = A_m grams (prep_gram), the rest k_colsum tiles
+//   k_deltaops: blocks [0, nxs) = the shard sum xa of A (chunk sums, then the last
+//               arrival adds them in chunk order); then G blocks of Z operators from
+//               A_m (prep_ops); the rest k_delta (4 shards per block, one wave each)
+//   k_zxchol:   block 0 = the X operators from xa (k_xchol), the rest k_zdraw tiles
+// The gram and operators are those of the NEXT iteration (they read this iteration's
+// Lambda and ps); dcfm_run runs a prologue after set_state.
+// ============================================================================
+__global__ __launch_bounds__(256) void k_colgram(Dims d, const double *__restrict__ cpart,
+                                                 double *__restrict__ sloc, const double *__restrict__ Lam,
+                                                 const double *__restrict__ omega, double *__restrict__ A,
+                                                 double *__restrict__ ZM) {
+    __shared__ double smem[PREP_SMEM];
+    if ((int)blockIdx.x < d.G) {
+        prep_gram(d, Lam, omega, A, ZM, blockIdx.x, smem);
+        return;
+    }
+    colsum_tile<KP>(d, cpart, sloc, blockIdx.x - d.G, 0, smem);
+}
+
+
+// The chunk sums are handed to the last arrival with agent-scope relaxed atomics (sc1:
+// coherent across the XCDs' L2s without write-back / invalidate), ordered by the stores'
+// completion before the ticket — __threadfence's buffer_wbl2 / buffer_inv flush the XCD's
+// whole L2 and drop what co-resident blocks cache (measured +20 us next to a Y pass).
+constexpr int XSUM_BLOCKS = 8;
+__device__ __forceinline__ void st_agent(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double *p) {
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool last_arrival(unsigned *ticket, unsigned count, double *smem) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this thread's agent-scope stores are done
+    __syncthreads();
+    unsigned *flag = reinterpret_cast<unsigned *>(smem);
+    if (threadIdx.x == 0) {
+        const bool last =
+            __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == count - 1;
+        if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+        *flag = last ? 1u : 0u;
+    }
+    __syncthreads();
+    const bool last = *flag != 0u;
+    __syncthreads();
+    return last;
+}
+
+// blocks [0, nxs) of k_deltaops: chunk sums of A over the local shards into xpart, then
+// the last arrival adds them in chunk order into xa (k_zxchol forms the X operators)
+__device__ __forceinline__ void xsum_tree(const Dims &d, const double *__restrict__ A, double *__restrict__ xpart,
+                                          unsigned *__restrict__ ticket, double *__restrict__ xa, int j, int nxs,
+                                          double *smem) {
+    const int t = threadIdx.x;
+    const int chunk = (d.G + nxs - 1) / nxs, m0 = j * chunk, m1 = min(d.G, m0 + chunk);
+    double v[KP * KP / 256];
+#pragma unroll
+    for (int u = 0; u < KP * KP / 256; ++u) {
+        const int e = t + 256 * u;
+        double acc = 0.0;
+#pragma unroll 8
+        for (int m = m0; m < m1; ++m) acc += A[(size_t)m * KP * KP + e];
+        v[u] = acc;
+        st_agent(xpart + (size_t)j * KP * KP + e, acc);
+    }
+    if (!last_arrival(ticket, (unsigned)nxs, smem)) return;
+#pragma unroll
+    for (int u = 0; u < KP * KP / 256; ++u) {
+        const int e = t + 256 * u;
+        double acc = 0.0;
+        for (int jj = 0; jj < nxs; ++jj) acc += (jj == j) ? v[u] : ld_agent(xpart + (size_t)jj * KP * KP + e);
+        xa[e] = acc;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_deltaops(Dims d, const double *__restrict__ sall,
+                                                  const double *__restrict__ delta_in,
+                                                  const double *__restrict__ tau_in,
+                                                  double *__restrict__ delta_out, double *__restrict__ tau_out,
+                                                  DrawsDev dr, int64_t iter, const double *__restrict__ A,
+                                                  double *__restrict__ ZM, double *__restrict__ xpart,
+                                                  unsigned *__restrict__ ticket, double *__restrict__ xa) {
+    __shared__ double smem[PREP_SMEM];
+    const int nxs = d.G < XSUM_BLOCKS ? d.G : XSUM_BLOCKS;
+    int b = blockIdx.x;
+    if (b < nxs) {
+        xsum_tree(d, A, xpart, ticket, xa, b, nxs, smem);
+        return;
+    }
+    b -= nxs;
+    if (b < d.G) {
+        prep_load(d, A, b, smem);
+        prep_ops(d, ZM, b, smem);
+        return;
+    }
+    const int m = (b - d.G) * 4 + (threadIdx.x >> 6);
+    if (m < d.g) delta_shard(d, sall, delta_in, tau_in, delta_out, tau_out, dr, iter, m, threadIdx.x & 63);
+}
+
+constexpr int ZX_SMEM = ZDRAW_SMEM > XCHOL_SMEM ? ZDRAW_SMEM : XCHOL_SMEM;
+__global__ __launch_bounds__(256) void k_zxchol(Dims d, const double *__restrict__ W,
+                                                const double *__restrict__ ZM, const double *__restrict__ X,
+                                                double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
+                                                int64_t iter, const double *__restrict__ xa,
+                                                double *__restrict__ XM) {
+    __shared__ double smem[ZX_SMEM];
+    if (blockIdx.x > 0) {
+        zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blockIdx.x - 1, gridDim.x - 1), smem);
+        return;
+    }
+    for (int e = threadIdx.x; e < KP * KP; e += 256) xprec_store(d, smem, e, xa[e]);
+    __syncthreads();
+    xchol_factor(d, XM, smem);
 }
 
 // ============================================================================
@@ -1371,10 +1418,18 @@ void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
     hipLaunchKernelGGL(k_zdraw, dim3((d.NP / 128) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
                        dr, iter);
 }
-void launch_wprep(const Dims &d, const Bufs &b, hipStream_t s) {
+void launch_colgram(const Dims &d, const Bufs &b, bool colsum, hipStream_t s) {
     if (d.kp != KP) return;
-    hipLaunchKernelGGL(k_wprep, dim3(d.G + (d.NP / 128) * d.G), dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W, b.A,
-                       b.ZM, b.xpart, b.ticket, b.xa);
+    hipLaunchKernelGGL(k_colgram, dim3(d.G + (colsum ? d.G : 0)), dim3(256), 0, s, d, b.cpart, b.sloc, b.Lam,
+                       b.omega, b.A, b.ZM);
+}
+void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool delta,
+                     const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
+                     hipStream_t s) {
+    if (d.kp != KP) return;
+    const int nxs = d.G < XSUM_BLOCKS ? d.G : XSUM_BLOCKS;
+    hipLaunchKernelGGL(k_deltaops, dim3(nxs + d.G + (delta ? (d.g + 3) / 4 : 0)), dim3(256), 0, s, d, b.sall,
+                       delta_in, tau_in, delta_out, tau_out, dr, iter, b.A, b.ZM, b.xpart, b.ticket, b.xa);
 }
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return;

@@ -114,7 +114,14 @@ extern __device__ unsigned long long g_phase[32];
             for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_phase[(b) + k_], ph_acc_[k_]);      \
     } while (0)
 #define PHASE_END() PHASE_END_AT(0)
+// block-role completion stamps of one launch: slot 24 = ~(earliest block start), slot s = latest end
+#define STAMP_START() do { if (threadIdx.x == 0) atomicMax(&g_phase[24], ~(unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
+#define STAMP_END(s) do { if (threadIdx.x == 0) atomicMax(&g_phase[(s)], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
+#define STAMP_START2() do { if (threadIdx.x == 0) atomicMax(&g_phase[28], ~(unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
 #else
+#define STAMP_START2() (void)0
+#define STAMP_START() (void)0
+#define STAMP_END(s) (void)0
 #define PHASE_END_AT(b) (void)0
 #define PHASE_T0() (void)0
 #define PHASE(k) (void)0
