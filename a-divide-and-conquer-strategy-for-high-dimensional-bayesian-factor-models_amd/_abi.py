@@ -32,7 +32,7 @@ K_COUNT = 14
 # every symbol include/dcfm.h declares
 EXPORTS = (
     "dcfm_create", "dcfm_destroy", "dcfm_last_error", "dcfm_abi_version",
-    "dcfm_comm_unique_id", "dcfm_comm_init", "dcfm_set_data", "dcfm_set_state",
+    "dcfm_comm_unique_id", "dcfm_comm_init", "dcfm_comm_init_loopback", "dcfm_set_data", "dcfm_set_state",
     "dcfm_set_draws", "dcfm_run", "dcfm_synchronize", "dcfm_get_state", "dcfm_get_sigma",
     "dcfm_get_sigma_cols",
     "dcfm_saved_samples", "dcfm_set_profiling", "dcfm_set_profiling_mask", "dcfm_get_kernel_stats",
@@ -93,6 +93,7 @@ def load_library(path: Path | None = None):
         "dcfm_abi_version": (C.c_int, []),
         "dcfm_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
         "dcfm_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8)]),
+        "dcfm_comm_init_loopback": (C.c_int, [C.POINTER(vp), C.c_int32]),
         "dcfm_set_data": (C.c_int, [vp, _DP]),
         "dcfm_set_state": (C.c_int, [vp, C.POINTER(DcfmStateView)]),
         "dcfm_set_draws": (C.c_int, [vp, C.POINTER(DcfmDrawsView), C.c_int64, C.c_int64]),

@@ -8,7 +8,11 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -21,6 +25,34 @@ using namespace dcfm;
 namespace {
 
 struct ProfRec { int kid; hipEvent_t a, b; };
+
+// In-process loopback collectives (dcfm_comm_init_loopback): n handles on one device,
+// one host thread per rank, the same all-gather / all-reduce semantics as the RCCL
+// communicators — so the multi-rank sweep runs and is parity-tested on a single GPU.
+// Per collective: every rank posts its send pointer and a "ready" event (barrier), copies
+// every other rank's slice in on its own stream after that rank's event, posts a "done"
+// event (barrier), waits for every rank's "done" (no send buffer is reused before all
+// ranks read it), and a last barrier frees the posting slots for the next collective.
+struct LoopGroup {
+    int n;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    std::vector<const double *> send;
+    std::vector<hipEvent_t> ready, done;
+    explicit LoopGroup(int n_) : n(n_), send(n_, nullptr), ready(n_, nullptr), done(n_, nullptr) {}
+    bool barrier(std::unique_lock<std::mutex> &lk) {
+        const uint64_t my = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        return cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != my; });
+    }
+};
 
 }  // namespace
 
@@ -35,6 +67,8 @@ struct dcfm_handle {
     hipStream_t sasm = nullptr;       // covariance assembly, overlapping later iterations
     ncclComm_t comm = nullptr, comm_side = nullptr, comm_asm = nullptr;
     bool comm_ok = false;
+    std::shared_ptr<LoopGroup> loop;  // loopback collectives instead of RCCL (testing)
+    hipEvent_t lp_ready = nullptr, lp_done = nullptr;
     hipEvent_t e_lam = nullptr, e_prep = nullptr, e_xchol = nullptr, e_batch = nullptr,
                e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
@@ -107,6 +141,70 @@ static int dalloc(dcfm_handle *h, double **p, size_t n) {
 }
 
 static int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+// ---------------------------------------------------------------------------
+// collectives: RCCL communicator per stream (CH_*), or the in-process loopback group
+// ---------------------------------------------------------------------------
+enum { CH_MAIN = 0, CH_SIDE = 1, CH_ASM = 2 };
+
+static int loop_allgather(dcfm_handle *h, const double *send, double *recv, size_t count, hipStream_t s) {
+    LoopGroup &G = *h->loop;
+    const int r = h->d.rank;
+    HIPC(h, hipEventRecord(h->lp_ready, s));
+    {
+        std::unique_lock<std::mutex> lk(G.mu);
+        G.send[r] = send;
+        G.ready[r] = h->lp_ready;
+        if (!G.barrier(lk)) return fail(h, DCFM_ERR_RCCL, "loopback all-gather: ranks did not meet");
+    }
+    for (int k = 0; k < G.n; ++k) {
+        double *dst = recv + (size_t)k * count;
+        if (G.send[k] == dst) continue;                      // in place
+        if (k != r) HIPC(h, hipStreamWaitEvent(s, G.ready[k], 0));
+        HIPC(h, hipMemcpyAsync(dst, G.send[k], count * sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+    HIPC(h, hipEventRecord(h->lp_done, s));
+    {
+        std::unique_lock<std::mutex> lk(G.mu);
+        G.done[r] = h->lp_done;
+        if (!G.barrier(lk)) return fail(h, DCFM_ERR_RCCL, "loopback all-gather: ranks did not meet");
+    }
+    for (int k = 0; k < G.n; ++k)
+        if (k != r) HIPC(h, hipStreamWaitEvent(s, G.done[k], 0));
+    {
+        std::unique_lock<std::mutex> lk(G.mu);
+        if (!G.barrier(lk)) return fail(h, DCFM_ERR_RCCL, "loopback all-gather: ranks did not meet");
+    }
+    return DCFM_OK;
+}
+
+// recv = concatenation over ranks of count doubles (send may be recv + rank * count)
+static int coll_allgather(dcfm_handle *h, int ch, const double *send, double *recv, size_t count, hipStream_t s) {
+    if (h->loop) return loop_allgather(h, send, recv, count, s);
+    ncclComm_t c = ch == CH_MAIN ? h->comm : (ch == CH_SIDE ? h->comm_side : h->comm_asm);
+    NCCLC(h, ncclAllGather(send, recv, count, ncclDouble, c, s));
+    return DCFM_OK;
+}
+
+// buf = sum over ranks of buf (in rank order for the loopback group)
+static int coll_allreduce_sum(dcfm_handle *h, int ch, double *buf, size_t count, hipStream_t s) {
+    if (!h->loop) {
+        ncclComm_t c = ch == CH_MAIN ? h->comm : (ch == CH_SIDE ? h->comm_side : h->comm_asm);
+        NCCLC(h, ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c, s));
+        return DCFM_OK;
+    }
+    void *q = nullptr;
+    HIPC(h, hipMalloc(&q, (size_t)h->loop->n * count * sizeof(double)));
+    double *all = static_cast<double *>(q);
+    int rc = loop_allgather(h, buf, all, count, s);
+    if (rc == DCFM_OK) {
+        launch_sum_slices(all, h->loop->n, count, buf, s);
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "loopback all-reduce: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(all);
+    return rc;
+}
 
 // ---------------------------------------------------------------------------
 // profiling helpers
@@ -341,6 +439,8 @@ void dcfm_destroy(dcfm_handle *h) {
     for (hipEvent_t e : {h->e_lam, h->e_prep, h->e_xchol, h->e_batch, h->e_free[0], h->e_free[1], h->e_drawn[0],
                          h->e_drawn[1], h->e_used[0], h->e_used[1]})
         if (e) (void)hipEventDestroy(e);
+    if (h->lp_ready) (void)hipEventDestroy(h->lp_ready);
+    if (h->lp_done) (void)hipEventDestroy(h->lp_done);
     if (h->comm_asm) ncclCommDestroy(h->comm_asm);
     if (h->comm_side) ncclCommDestroy(h->comm_side);
     if (h->comm) ncclCommDestroy(h->comm);
@@ -373,6 +473,28 @@ int dcfm_comm_init(dcfm_handle *h, const uint8_t id[128]) {
     NCCLC(h, ncclCommSplit(h->comm, 0, h->d.rank, &h->comm_side, nullptr));
     NCCLC(h, ncclCommSplit(h->comm, 0, h->d.rank, &h->comm_asm, nullptr));
     h->comm_ok = true;
+    return DCFM_OK;
+}
+
+int dcfm_comm_init_loopback(dcfm_handle *const *hs, int32_t n) {
+    if (!hs || n < 1) return fail(nullptr, DCFM_ERR_INVALID, "null handles or n < 1");
+    for (int r = 0; r < n; ++r) {
+        if (!hs[r]) return fail(nullptr, DCFM_ERR_INVALID, "null handle %d", r);
+        if (hs[r]->d.nranks != n || hs[r]->d.rank != r)
+            return fail(hs[r], DCFM_ERR_INVALID, "handle %d: nranks %d rank %d, expected %d / %d", r,
+                        hs[r]->d.nranks, hs[r]->d.rank, n, r);
+        if (hs[r]->cfg.device != hs[0]->cfg.device)
+            return fail(hs[r], DCFM_ERR_INVALID, "loopback ranks must share one device");
+    }
+    auto G = std::make_shared<LoopGroup>(n);
+    for (int r = 0; r < n; ++r) {
+        dcfm_handle *h = hs[r];
+        HIPC(h, hipSetDevice(h->cfg.device));
+        if (!h->lp_ready) HIPC(h, hipEventCreateWithFlags(&h->lp_ready, hipEventDisableTiming));
+        if (!h->lp_done) HIPC(h, hipEventCreateWithFlags(&h->lp_done, hipEventDisableTiming));
+        h->loop = G;
+        h->comm_ok = true;
+    }
     return DCFM_OK;
 }
 
@@ -586,12 +708,13 @@ static int flush_batch(dcfm_handle *h) {
     if (d.nranks > 1) {
         KTimer t(h, DCFM_K_COMM, h->sasm);
         const size_t rows = (size_t)d.G * d.P;
-        NCCLC(h, ncclGroupStart());
-        NCCLC(h, ncclAllGather(b.Lb[lb] + (size_t)d.rank * rows * b.LDB, b.Lb[lb], rows * b.LDB, ncclDouble,
-                               h->comm_asm, h->sasm));
-        NCCLC(h, ncclAllGather(b.wsum[lb] + (size_t)d.rank * rows, b.wsum[lb], rows, ncclDouble, h->comm_asm,
-                               h->sasm));
-        NCCLC(h, ncclGroupEnd());
+        if (!h->loop) NCCLC(h, ncclGroupStart());
+        int rc = coll_allgather(h, CH_ASM, b.Lb[lb] + (size_t)d.rank * rows * b.LDB, b.Lb[lb], rows * b.LDB,
+                                h->sasm);
+        if (rc == DCFM_OK)
+            rc = coll_allgather(h, CH_ASM, b.wsum[lb] + (size_t)d.rank * rows, b.wsum[lb], rows, h->sasm);
+        if (!h->loop) NCCLC(h, ncclGroupEnd());
+        if (rc) return rc;
     }
     const int kext = round_up(h->batch * d.K, 16);   // k_assemble chunk
     const double effsamp = (double)h->cfg.mcmc / (double)h->cfg.thin;   // dc:45 (Q8)
@@ -700,7 +823,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             { KTimer t(h, DCFM_K_XCHOL, ss); launch_asum(d, b, ss); }
             if (d.nranks > 1) {
                 KTimer t(h, DCFM_K_COMM, ss);
-                NCCLC(h, ncclAllGather(b.xa, b.xa_all, KW * KW, ncclDouble, h->comm_side, ss));
+                if (int rc = coll_allgather(h, CH_SIDE, b.xa, b.xa_all, KW * KW, ss)) return rc;
             }
             { KTimer t(h, DCFM_K_XCHOL, ss); launch_xchol(d, b, ss); }
             HIPC(h, hipEventRecord(h->e_xchol, ss));
@@ -711,7 +834,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             { KTimer t(h, DCFM_K_XRED, s);   launch_xred(d, b, s); }
             if (d.nranks > 1) {
                 KTimer t(h, DCFM_K_COMM, s);
-                NCCLC(h, ncclAllGather(b.xin, b.xall, (size_t)d.NP * KW, ncclDouble, h->comm, s));
+                if (int rc = coll_allgather(h, CH_MAIN, b.xin, b.xall, (size_t)d.NP * KW, s)) return rc;
             }
             HIPC(h, hipStreamWaitEvent(s, h->e_xchol, 0));
         }
@@ -735,7 +858,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             { KTimer t(h, DCFM_K_COLSUM, s); launch_colsum(d, b, s); }
             if (d.nranks > 1) {
                 KTimer t(h, DCFM_K_COMM, s);
-                NCCLC(h, ncclAllGather(b.sloc, b.sall, (size_t)d.G * KW, ncclDouble, h->comm, s));
+                if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.sall, (size_t)d.G * KW, s)) return rc;
             }
             {
                 KTimer t(h, DCFM_K_DELTA, s);
@@ -799,10 +922,8 @@ int dcfm_get_sigma_cols(dcfm_handle *h, int64_t col0, int64_t ncols, double *out
     launch_sigma_cols(h->b.Sigma, d.p, (int)col0, (int)ncols, tmp, h->stream);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "sigma_cols: %s", hipGetErrorString(e));
-    if (rc == DCFM_OK && d.nranks > 1) {   // each element is owned by exactly one rank: the sum is exact
-        ncclResult_t r = ncclAllReduce(tmp, tmp, n, ncclDouble, ncclSum, h->comm_asm, h->stream);
-        if (r != ncclSuccess) rc = fail(h, DCFM_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
-    }
+    if (rc == DCFM_OK && d.nranks > 1)   // each element is owned by exactly one rank: the sum is exact
+        rc = coll_allreduce_sum(h, CH_ASM, tmp, n, h->stream);
     if (rc == DCFM_OK) {
         e = hipMemcpyAsync(out, tmp, n * sizeof(double), hipMemcpyDeviceToHost, h->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(h->stream);

@@ -89,6 +89,8 @@ void launch_assemble(const Dims &d, const Bufs &b, const double *Lb, const doubl
 void launch_sigma_cols(const double *S, int p, int c0, int nc, double *out, hipStream_t s);
 void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s);
 void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s);
+// dst[i] = sum_k src[k * count + i] in slice order (loopback all-reduce)
+void launch_sum_slices(const double *src, int ns, size_t count, double *dst, hipStream_t s);
 void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,
                      int64_t count, double *out, hipStream_t s);
 

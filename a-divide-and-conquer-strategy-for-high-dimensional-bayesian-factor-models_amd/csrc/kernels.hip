@@ -1505,6 +1505,18 @@ void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s
     hipLaunchKernelGGL(k_draws<true>, dim3(pl.b_gpsi), dim3(256), 0, s, d, dr, iter);
     hipLaunchKernelGGL(k_draws<false>, dim3(pl.total - pl.b_gpsi), dim3(256), 0, s, d, dr, iter);
 }
+__global__ __launch_bounds__(256) void k_sum_slices(const double *__restrict__ src, int ns, size_t count,
+                                                   double *__restrict__ dst) {
+    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < count; i += (size_t)gridDim.x * 256) {
+        double v = 0.0;
+        for (int k = 0; k < ns; ++k) v += src[(size_t)k * count + i];
+        dst[i] = v;
+    }
+}
+void launch_sum_slices(const double *src, int ns, size_t count, double *dst, hipStream_t s) {
+    const int grid = (int)std::min<size_t>((count + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_sum_slices, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, src, ns, count, dst);
+}
 void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,
                      int64_t count, double *out, hipStream_t s) {
     const int grid = (int)std::min<int64_t>((count + 255) / 256, 8192);

@@ -90,6 +90,15 @@ class Sampler:
         self._check(self.lib.dcfm_comm_init(self.h, buf))
 
     # -- inputs ----------------------------------------------------------------
+    @staticmethod
+    def comm_loopback(samplers):
+        """In-process loopback communicator over ``samplers`` (ranks 0..n-1 of one chain
+        on one device): each sampler must then be driven from its own thread."""
+        n = len(samplers)
+        arr = (C.c_void_p * n)(*[s_.h.value for s_ in samplers])
+        lib = samplers[0].lib
+        _abi.check(lib, None, lib.dcfm_comm_init_loopback(arr, n))
+
     def set_data(self, Yd_local):
         Y = _f64F(Yd_local)
         if Y.shape != (self.n, self.P, self.g_local):

@@ -109,6 +109,11 @@ int  dcfm_abi_version(void);
  * dcfm_comm_init.  Not needed when nranks == 1. */
 int  dcfm_comm_unique_id(uint8_t out[128]);
 int  dcfm_comm_init(dcfm_handle *h, const uint8_t id[128]);
+/* Test communicator: the n handles (nranks = n, ranks 0..n-1, one device) exchange
+ * through device copies inside this process instead of RCCL, each handle driven by
+ * its own host thread — the multi-rank sweep on a single GPU.  Same collective
+ * semantics and call order as dcfm_comm_init. */
+int  dcfm_comm_init_loopback(dcfm_handle *const *handles, int32_t n);
 
 /* ---- inputs -------------------------------------------------------------- */
 /* Yd(:,:,shard0+1 : shard0+g_local) after dc:48-59, n x P x g_local.        */
