@@ -750,10 +750,11 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     const size_t KW = d.kp;
     const size_t nkg = (size_t)d.g * KW;
     const int64_t end_iter = first_iter + n_iter;
-    // one rank, K <= 32: prep and the X operators ride inside k_wprep / k_zxchol on the
-    // main stream; otherwise they run on the side stream (with the xa all-gather)
+    // K <= 32: the per-shard operators ride in the fused launches on the main stream
+    // (k_colgram, k_deltaops, k_zxchol); K > 32 (or DCFM_NOFUSE=1): prep and the X
+    // operators run on the side stream
     static const bool nofuse = [] { const char *e = std::getenv("DCFM_NOFUSE"); return e && e[0] == '1'; }();
-    const bool fused = d.nranks == 1 && d.kp == KP && !nofuse;
+    const bool fused = d.kp == KP && !nofuse;
     // generated draws: batches [b0, b0 + DB) aligned to this call's first iteration,
     // queued on sdraw into a slot whose previous batch the sweep has finished with
     int rc_gen = DCFM_OK;
@@ -800,6 +801,8 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         KTimer t(h, DCFM_K_PREP, s);
         launch_colgram(d, b, false, s);
         launch_deltaops(d, b, h->dr, first_iter, false, nullptr, nullptr, nullptr, nullptr, s);
+        if (d.nranks > 1)
+            if (int rc = coll_allgather(h, CH_MAIN, b.xa, b.xa_all, KW * KW, s)) return rc;
     }
     for (int64_t it = first_iter; it < end_iter; ++it) {
         if (!d.inject && (it == first_iter || it == batch0 + batch_n)) {
@@ -815,6 +818,10 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             { KTimer t(h, DCFM_K_WPASS, s); launch_wpass(d, b, s); }
             { KTimer t(h, DCFM_K_ZDRAW, s); launch_zxchol(d, b, dr, it, s); }
             { KTimer t(h, DCFM_K_XRED, s);  launch_xred(d, b, s); }
+            if (d.nranks > 1) {
+                KTimer t(h, DCFM_K_COMM, s);
+                if (int rc = coll_allgather(h, CH_MAIN, b.xin, b.xall, (size_t)d.NP * KW, s)) return rc;
+            }
         } else {
             // side stream: A_m, R_m, Rx from this iteration's incoming Lambda, omega (dc:98-100,112-118)
             HIPC(h, hipStreamWaitEvent(ss, h->e_lam, 0));
@@ -847,10 +854,18 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         h->plam_valid = false;
         if (fused) {   // + the next iteration's grams and Z operators
             { KTimer t(h, DCFM_K_COLSUM, s); launch_colgram(d, b, true, s); }
+            if (d.nranks > 1) {
+                KTimer t(h, DCFM_K_COMM, s);
+                if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.sall, (size_t)d.G * KW, s)) return rc;
+            }
             {
                 KTimer t(h, DCFM_K_DELTA, s);
                 launch_deltaops(d, b, dr, it, true, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
                                 b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);
+            }
+            if (d.nranks > 1) {
+                KTimer t(h, DCFM_K_COMM, s);
+                if (int rc = coll_allgather(h, CH_MAIN, b.xa, b.xa_all, KW * KW, s)) return rc;
             }
             h->prep_valid = true;
         } else {

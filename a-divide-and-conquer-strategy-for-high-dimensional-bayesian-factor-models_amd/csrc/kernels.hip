@@ -988,7 +988,9 @@ __global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__
 //   k_deltaops: blocks [0, nxs) = the shard sum xa of A (chunk sums, then the last
 //               arrival adds them in chunk order); then G blocks of Z operators from
 //               A_m (prep_ops); the rest k_delta (4 shards per block, one wave each)
-//   k_zxchol:   block 0 = the X operators from xa (k_xchol), the rest k_zdraw tiles
+//   k_zxchol:   block 0 = the X operators from the ranks' xa (k_xchol), the rest k_zdraw tiles
+// With several ranks the main stream all-gathers xa after k_deltaops, the X message
+// after k_xred and the column sums after k_colgram (RCCL, same order on every rank).
 // The gram and operators are those of the NEXT iteration (they read this iteration's
 // Lambda and ps); dcfm_run runs a prologue after set_state.
 // ============================================================================
@@ -1087,14 +1089,18 @@ constexpr int ZX_SMEM = ZDRAW_SMEM > XCHOL_SMEM ? ZDRAW_SMEM : XCHOL_SMEM;
 __global__ __launch_bounds__(256) void k_zxchol(Dims d, const double *__restrict__ W,
                                                 const double *__restrict__ ZM, const double *__restrict__ X,
                                                 double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
-                                                int64_t iter, const double *__restrict__ xa,
+                                                int64_t iter, const double *__restrict__ xa_all,
                                                 double *__restrict__ XM) {
     __shared__ double smem[ZX_SMEM];
     if (blockIdx.x > 0) {
         zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blockIdx.x - 1, gridDim.x - 1), smem);
         return;
     }
-    for (int e = threadIdx.x; e < KP * KP; e += 256) xprec_store(d, smem, e, xa[e]);
+    for (int e = threadIdx.x; e < KP * KP; e += 256) {   // the ranks' shard sums, in rank order
+        double v = xa_all[e];
+        for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * KP * KP + e];
+        xprec_store(d, smem, e, v);
+    }
     __syncthreads();
     xchol_factor(d, XM, smem);
 }
@@ -1434,7 +1440,7 @@ void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return;
     hipLaunchKernelGGL(k_zxchol, dim3(1 + (d.NP / 128) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp, dr,
-                       iter, b.xa, b.XM);
+                       iter, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
     const int total = d.NP * d.kp;
