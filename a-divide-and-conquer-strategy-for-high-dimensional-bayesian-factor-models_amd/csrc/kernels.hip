@@ -628,20 +628,6 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
 // dcfm_set_state).  Every global load of the row is issued up front.
 // psi o lambda^2 of the row -> cpart[m][j][:] (k_colsum sums the rows).
 // ============================================================================
-// sum of v over this lane's 16-lane DPP row (quad_perm xor 1, xor 2, then row_ror 4, 8)
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double rowsum16(double v) {
-    v += dpp_d<0xB1>(v);     // quad_perm [1,0,3,2]
-    v += dpp_d<0x4E>(v);     // quad_perm [2,3,0,1]
-    v += dpp_d<0x124>(v);    // row_ror:4
-    v += dpp_d<0x128>(v);    // row_ror:8
-    return v;
-}
 
 #ifndef DCFM_LAMBDA_MINWAVES
 #define DCFM_LAMBDA_MINWAVES 1

@@ -16,6 +16,8 @@
 //              Cholesky of Q_j (8x8 blocks per thread), fused forward   dc:156,169-171
 //              solve, blocked back solve; psi, SS identity, ps, omega
 //   k_delta    MGP chain over up to 128 factors (2 per lane)            dc:155-165
+#include <cstdlib>
+
 #include "dcfm_internal.h"
 #include "philox.h"
 #include "linalg.h"
@@ -525,6 +527,241 @@ __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
 }
 
 // ============================================================================
+// k_lambda_t: one 256-thread workgroup per loading row j, MFMA-tiled.   dc:140-145 (+150,156,169-171)
+// Q_j's lower triangle (nb = ceil(K/16) tile rows) as 16x16 tiles held in registers in
+// the fp64 MFMA C/D layout (lane (c, q) holds tile[q + 4g][c], g = 0..3), tile t (row-major
+// lower order) on wave t % 4, slot t / 4.  Per block column J:
+//   a. the diagonal tile goes to LDS;  b. wave 0 factors and inverts it (chol_inv16:
+//   U_JJ = L_JJ^{-1}) and advances the forward solve v_J = U_JJ b_J;  c. the panel tiles
+//   become L_IJ = A_IJ U_JJ' (one 16x16x16 MFMA product each, A_IJ through LDS into the
+//   A-operand layout), staged row-major in LDS, and update b_I -= L_IJ v_J;  d. every
+//   trailing tile takes A_IK -= L_IJ L_KJ' (4 MFMAs, both operands read from the panel).
+// Three barriers per block column (the per-pivot kernel needs two per pivot).  The L
+// tiles stay in the registers for the blocked back solve x = L^{-T}(v + z); the epilogue
+// (psi, SS identity, ps, omega, cpart) is the one of k_lambda above.
+// ============================================================================
+#ifndef DCFM_LT_MINW
+#define DCFM_LT_MINW 3
+#endif
+template <int KW, int NB>
+__global__ __launch_bounds__(256, DCFM_LT_MINW) void k_lambda_t(
+    Dims d, const double *__restrict__ C, const double *__restrict__ E, const double *__restrict__ yy,
+    const double *__restrict__ tau_cur, const double *__restrict__ plam_src, double *__restrict__ Lam,
+    double *__restrict__ psi, double *__restrict__ ps, double *__restrict__ omega, double *__restrict__ cpart,
+    DrawsDev dr, int64_t iter) {
+    // NB = ceil(K/16) tile rows exactly (template: slot arrays and unrolled loops sized to it)
+    constexpr int NBM = NB, NTM = NBM * (NBM + 1) / 2, SL = (NTM + 3) / 4, LD = 17, TZ = 16 * LD;
+    __shared__ double Sd[TZ], Ud[TZ], Pn[NBM * TZ];
+    __shared__ double vb[KW], vx[KW], part[NBM * 16];
+    __shared__ double lds_l[32], lds_u[16];
+    const int j = blockIdx.x, m = blockIdx.y, mg = d.shard0 + m;
+    const int t = threadIdx.x, lane = t & 63, c16 = lane & 15, q = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);   // scalar: tile coordinates live in SGPRs
+    const int K = d.K;
+    constexpr int nb = NB, NT = NTM;
+    const double *Em = E + (size_t)m * KW * KW;
+    const size_t rowoff = ((size_t)m * d.PP + j) * KW;
+    const double psj = ps[(size_t)m * d.PP + j];
+    // ---- Q_j tiles (dc:141: ps_j eta2 + diag(Plam_j)), identity padding
+    d4 acc[SL];
+    int tI[SL], tK[SL];
+#pragma unroll
+    for (int sl = 0; sl < SL; ++sl) {
+        const int tt = 4 * sl + wave;
+        tI[sl] = -1;
+        tK[sl] = -1;
+        acc[sl] = d4{0.0, 0.0, 0.0, 0.0};
+        if (tt < NT) {
+            int I, Kc;
+            tile::tri_pair(tt, I, Kc);
+            tI[sl] = I;
+            tK[sl] = Kc;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int r = 16 * I + q + 4 * g, c = 16 * Kc + c16;
+                double val = (r == c) ? 1.0 : 0.0;
+                if (r < K && c < K) {
+                    val = psj * Em[(size_t)r * KW + c];
+                    if (r == c) {
+                        const double pl = plam_src ? plam_src[rowoff + r]
+                                                   : psi[rowoff + r] * tau_cur[(size_t)mg * KW + r];   // dc:176
+                        val = pl + val;
+                    }
+                }
+                acc[sl][g] = val;
+            }
+        }
+    }
+    if (t < KW) vb[t] = (t < K) ? psj * C[rowoff + t] : 0.0;          // blam (dc:141)
+    // ---- blocked factorisation with the forward solve
+    for (int J = 0; J < nb; ++J) {
+        const int td = J * (J + 1) / 2 + J, ow = td & 3, os = td >> 2;
+        if (wave == ow) {
+#pragma unroll
+            for (int sl = 0; sl < SL; ++sl)
+                if (sl == os) {
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) Sd[(q + 4 * g) * LD + c16] = acc[sl][g];
+                }
+        }
+        __syncthreads();
+        if (wave == 0) {
+            chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
+            __builtin_amdgcn_wave_barrier();
+            double v = 0.0;
+            if (lane < 16) {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) v = fma(Ud[lane * LD + c], vb[16 * J + c], v);   // U is lower
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane < 16) vb[16 * J + lane] = v;                       // v_J (dc:143)
+        }
+        __syncthreads();
+        // panel tiles (I, J), I > J, and the diagonal owner keeps U_JJ for the back solve
+#pragma unroll
+        for (int sl = 0; sl < SL; ++sl) {
+            if (tK[sl] == J && tI[sl] > J) {
+                double *P = Pn + tI[sl] * TZ;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) P[(q + 4 * g) * LD + c16] = acc[sl][g];   // A_IJ row-major
+                __builtin_amdgcn_wave_barrier();
+                d4 L = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4)       // L_IJ = A_IJ U_JJ':  A[i][k] = A_IJ[i][k], B[k][c] = U_JJ[c][k]
+                    L = mfma16x16x4(P[c16 * LD + 4 * s4 + q], Ud[c16 * LD + 4 * s4 + q], L);
+                acc[sl] = L;
+                __builtin_amdgcn_wave_barrier();
+                const double vJ = vb[16 * J + c16];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    P[(q + 4 * g) * LD + c16] = L[g];                  // L_IJ row-major
+                    const double sv = rowsum16(L[g] * vJ);             // (L_IJ v_J)[q + 4g]
+                    if (c16 == 0) vb[16 * tI[sl] + q + 4 * g] -= sv;
+                }
+            } else if (tK[sl] == J && tI[sl] == J) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) acc[sl][g] = Ud[(q + 4 * g) * LD + c16];   // U_JJ, C/D layout
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();
+        // trailing tiles (I, Kc), I >= Kc > J:  A_IK -= L_IJ L_KJ'
+#pragma unroll
+        for (int sl = 0; sl < SL; ++sl) {
+            if (tK[sl] > J) {
+                const double *PI = Pn + tI[sl] * TZ, *PK = Pn + tK[sl] * TZ;
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4)
+                    acc[sl] = mfma16x16x4(-PI[c16 * LD + 4 * s4 + q], PK[c16 * LD + 4 * s4 + q], acc[sl]);
+            }
+            __builtin_amdgcn_sched_barrier(0);   // one slot's operands live at a time
+        }
+    }
+    // ---- w = v + z (dc:142 normrnd), blocked back solve x_J = U_JJ' (w_J - sum_{I>J} L_IJ' x_I)
+    if (t < KW && t < K) vb[t] += dr.NL[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + t];
+    __syncthreads();
+    for (int J = nb - 1; J >= 0; --J) {
+#pragma unroll
+        for (int sl = 0; sl < SL; ++sl) {
+            if (tK[sl] == J && tI[sl] > J) {                           // part_I = L_IJ' x_I
+                double p = 0.0;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) p = fma(acc[sl][g], vx[16 * tI[sl] + q + 4 * g], p);
+                p += __shfl_xor(p, 16, 64);
+                p += __shfl_xor(p, 32, 64);
+                if (q == 0) part[tI[sl] * 16 + c16] = p;
+            }
+        }
+        __syncthreads();
+        const int td = J * (J + 1) / 2 + J, ow = td & 3, os = td >> 2;
+        if (wave == ow) {
+#pragma unroll
+            for (int sl = 0; sl < SL; ++sl)
+                if (sl == os) {                                        // x_J = U_JJ' y
+                    double p = 0.0;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int r = q + 4 * g;
+                        double y = vb[16 * J + r];
+                        for (int I = J + 1; I < nb; ++I) y -= part[I * 16 + r];
+                        p = fma(acc[sl][g], y, p);
+                    }
+                    p += __shfl_xor(p, 16, 64);
+                    p += __shfl_xor(p, 32, 64);
+                    if (q == 0) vx[16 * J + c16] = p;
+                }
+        }
+        __syncthreads();
+    }
+    // ---- epilogue: Lambda_j, psi_j (dc:150); SS, ps_j, omega_j follow in k_ss
+    if (t < KW) {
+        const int r = t;
+        const double xr = (r < K) ? vx[r] : 0.0;
+        double psir = 0.0;
+        if (r < K) {
+            const double tr = tau_cur[(size_t)mg * KW + r];
+            const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xr * xr * tr));
+            const double G = dr.Gpsi[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + r];
+            psir = scale * G;
+            psi[rowoff + r] = psir;
+        }
+        Lam[rowoff + r] = xr;
+        cpart[rowoff + r] = psir * (xr * xr);          // mat = psijh .* Lambda.^2 (dc:156)
+    }
+}
+
+// ============================================================================
+// k_ss: residual sums and ps / omega of 16 loading rows per block      dc:169-171
+//   SS_j = yy_j - 2 lambda_j . C_j + lambda_j E lambda_j'   (identity; no third Y pass)
+// T = Lambda_m(rows) E_m as fp64 MFMA (A = 16 loading rows, B = E read directly),
+// 16x16 output tiles dealt over the 4 waves, then row dot products with lambda.
+// ============================================================================
+template <int KW>
+__global__ __launch_bounds__(256) void k_ss(Dims d, const double *__restrict__ Lam, const double *__restrict__ C,
+                                            const double *__restrict__ E, const double *__restrict__ yy,
+                                            double *__restrict__ ps, double *__restrict__ omega, DrawsDev dr,
+                                            int64_t iter) {
+    __shared__ double sred[4][16], slc[16];
+    const int m = blockIdx.y, mg = d.shard0 + m, j0 = 16 * blockIdx.x;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c16 = lane & 15, q = lane >> 4;
+    const int K = d.K, nk = (K + 3) >> 2, nct = (K + 15) >> 4;
+    const double *Lm = Lam + ((size_t)m * d.PP + j0) * KW;            // rows j0.. (pad rows are zero)
+    const double *Em = E + (size_t)m * KW * KW;
+    double xe[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int ct = wave; ct < nct; ct += 4) {
+        d4 T = {0.0, 0.0, 0.0, 0.0};
+        for (int s4 = 0; s4 < nk; ++s4)
+            T = mfma16x16x4(Lm[(size_t)c16 * KW + 4 * s4 + q], Em[(size_t)(4 * s4 + q) * KW + 16 * ct + c16], T);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) xe[g] += rowsum16(T[g] * Lm[(size_t)(q + 4 * g) * KW + 16 * ct + c16]);
+    }
+    if (c16 == 0) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) sred[wave][q + 4 * g] = xe[g];
+    }
+    {   // lambda_j . C_j: row = t >> 4, 16 lanes over k
+        const int rr = t >> 4, l = t & 15;
+        const size_t ro = ((size_t)m * d.PP + j0 + rr) * KW;
+        double lc = 0.0;
+        for (int k = l; k < K; k += 16) lc = fma(Lam[ro + k], C[ro + k], lc);
+        lc = rowsum16(lc);
+        if (l == 0) slc[rr] = lc;
+    }
+    __syncthreads();
+    if (t < 16) {
+        const int j = j0 + t;
+        if (j < d.P) {
+            const double xEx = (sred[0][t] + sred[1][t]) + (sred[2][t] + sred[3][t]);
+            const double SS = yy[(size_t)m * d.PP + j] - 2.0 * slc[t] + xEx;
+            const double G = dr.Gps[((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j];
+            const double psn = (1.0 / (d.bs + 0.5 * SS)) * G;     // dc:170
+            ps[(size_t)m * d.PP + j] = psn;
+            omega[(size_t)m * d.PP + j] = 1.0 / psn;              // dc:171 (Q1)
+        }
+    }
+}
+
+// ============================================================================
 // block = (shard m, 32 columns); 8 row groups x 4 independent accumulators each.
 template <int KW>
 __global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict__ cpart, double *__restrict__ sloc) {
@@ -676,9 +913,28 @@ void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *tau_cur,
                    const double *plam_src, hipStream_t s) {
-    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_lambda<KW>, dim3(d.P, d.G), dim3(lambda_threads(KW)), 0, s, d, b.C,
-                                           b.E, b.yy, tau_cur, plam_src, b.Lam, b.psi, b.ps, b.omega, b.cpart, dr,
-                                           iter));
+    static const bool legacy = [] { const char *e = std::getenv("DCFM_LAMBDA_BLOCKED8"); return e && e[0] == '1'; }();
+    if (legacy) {
+        WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_lambda<KW>, dim3(d.P, d.G), dim3(lambda_threads(KW)), 0, s, d, b.C,
+                                               b.E, b.yy, tau_cur, plam_src, b.Lam, b.psi, b.ps, b.omega, b.cpart,
+                                               dr, iter));
+        return;
+    }
+    const dim3 grid(d.P, d.G);
+#define LT(KWV, NBV)                                                                                              \
+    hipLaunchKernelGGL((k_lambda_t<KWV, NBV>), grid, dim3(256), 0, s, d, b.C, b.E, b.yy, tau_cur, plam_src, b.Lam, \
+                       b.psi, b.ps, b.omega, b.cpart, dr, iter)
+    switch ((d.K + 15) / 16) {            // K = 33..128: 3..8 tile rows
+    case 3: LT(64, 3); break;
+    case 4: LT(64, 4); break;
+    case 5: LT(128, 5); break;
+    case 6: LT(128, 6); break;
+    case 7: LT(128, 7); break;
+    default: LT(128, 8); break;
+    }
+#undef LT
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_ss<KW>, dim3((d.P + 15) / 16, d.G), dim3(256), 0, s, d, b.Lam, b.C,
+                                           b.E, b.yy, b.ps, b.omega, dr, iter));
 }
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
                   const double *tau_in, double *delta_out, double *tau_out, hipStream_t s) {

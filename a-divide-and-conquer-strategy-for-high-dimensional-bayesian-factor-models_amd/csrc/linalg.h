@@ -314,10 +314,11 @@ __device__ __forceinline__ void chol16_step(double &a0, double &a1, double &a2, 
 // right-hand side of L U = I in R0..R3.  Step k: pivot by readlane, l_r by a DPP
 // quad broadcast, then one LDS round trip hands out column k of L (lds_l, 32 slots,
 // the upper 16 zero) and row k of U (lds_u, 16 slots).
-__device__ __forceinline__ void chol_inv16(const double (*Sm)[KP + 1], int o, double (*Ub)[KP + 1],
-                                           double *lds_l, double *lds_u, int lane) {
+template <int LDP>
+__device__ __forceinline__ void chol_inv16_p(const double *Sm, int o, double *Ub, double *lds_l, double *lds_u,
+                                             int lane) {
     const int r = lane >> 2, cg = lane & 3;
-    const double *srow = &Sm[o + r][o + cg];   // entries above the diagonal are never consumed
+    const double *srow = Sm + (o + r) * LDP + o + cg;   // entries above the diagonal are never consumed
     double a0 = srow[0], a1 = srow[4], a2 = srow[8], a3 = srow[12];
     double R0 = (cg == r) ? 1.0 : 0.0, R1 = (4 + cg == r) ? 1.0 : 0.0;
     double R2 = (8 + cg == r) ? 1.0 : 0.0, R3 = (12 + cg == r) ? 1.0 : 0.0;
@@ -330,8 +331,27 @@ __device__ __forceinline__ void chol_inv16(const double (*Sm)[KP + 1], int o, do
         chol16_step<3>(a0, a1, a2, a3, R0, R1, R2, R3, kk, r, cg, lds_l, lds_u);
         a0 = a1; a1 = a2; a2 = a3; a3 = 0.0;
     }
-    double *urow = &Ub[o + r][o + cg];
+    double *urow = Ub + (o + r) * LDP + o + cg;
     urow[0] = R0; urow[4] = R1; urow[8] = R2; urow[12] = R3;
+}
+__device__ __forceinline__ void chol_inv16(const double (*Sm)[KP + 1], int o, double (*Ub)[KP + 1],
+                                           double *lds_l, double *lds_u, int lane) {
+    chol_inv16_p<KP + 1>(&Sm[0][0], o, &Ub[0][0], lds_l, lds_u, lane);
+}
+
+// DPP helpers: a double from lane CTRL-permuted within its 16-lane row; sum over the row
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double rowsum16(double v) {
+    v += dpp_d<0xB1>(v);     // quad_perm [1,0,3,2]
+    v += dpp_d<0x4E>(v);     // quad_perm [2,3,0,1]
+    v += dpp_d<0x124>(v);    // row_ror:4
+    v += dpp_d<0x128>(v);    // row_ror:8
+    return v;
 }
 
 // U = L^{-1}, L = chol of the KP x KP (= 32) SPD matrix whose lower triangle is in
