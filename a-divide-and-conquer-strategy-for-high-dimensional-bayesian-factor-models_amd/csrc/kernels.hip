@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 // ============================================================================
 // k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA, Y pass 1
 // one wave = (shard m, 32 rows i = 2 M-tiles) x 32 k (even / odd k N-tiles) of
-// column tile kt = blockIdx.y (KW/32 tiles; the wide layouts re-read Y from L2/MALL),
+// column tile kt (KW/32 tiles, adjacent in the 1-D grid so the wide layouts re-read Y from L2),
 // reduction over j in chunks of 8: lane (r, q) holds Y[i0+r][8t+2q .. +1] (16 B);
 // k-step 2t uses element 0, 2t+1 element 1; the B operand (w_j L[j][2r], w_j L[j][2r+1])
 // uses the same j <-> (q, e) map.  Register double-buffered prefetch of 2 chunks.
@@ -256,7 +256,9 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
                                                const double *__restrict__ Lam,
                                                const double *__restrict__ omega,
                                                double *__restrict__ W) {
-    wpass_tile<KW>(d, Y, Lam, omega, W, xcd_remap(blockIdx.x, gridDim.x), blockIdx.y);
+    // 1-D grid, the KW/32 column tiles of one 128-row block adjacent (same XCD: Y from L2)
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    wpass_tile<KW>(d, Y, Lam, omega, W, w / (KW / 32), w % (KW / 32));
 }
 
 // ============================================================================
@@ -506,8 +508,8 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
 
 // ============================================================================
 // k_cpass: [C_m | E_m] = [Y_m | eta_m]' eta_m    fp64 MFMA, Y pass 2      dc:133,138,141
-// block = (shard m, 32-column tile of [Y | eta]) x (32-column tile kt of eta,
-// blockIdx.y); its 4 waves split the reduction over rows i, partial 32x32 tiles
+// block = (shard m, 32-column tile of [Y | eta]) x (32-column tile kt of eta, the
+// fastest index of the 1-D grid); its 4 waves split the reduction over rows i, partial 32x32 tiles
 // summed in LDS in a fixed order.
 // Lane (r, q) loads 16 B: Y[i][c0+2r .. +1] and eta[i][2r .. +1] (formed on the
 // fly from X and Z), i = 4s + q, so the MFMA tiles are even/odd columns x
@@ -568,10 +570,11 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
                                                const double *__restrict__ Z,
                                                double *__restrict__ C, double *__restrict__ E) {
     __shared__ double red[4][32][33];
-    const int nt = (d.PP + KW) >> 5;
+    // 1-D grid, the KW/32 eta column tiles of one [Y | eta] tile adjacent (same XCD,
+    // so the Y tile is fetched once and re-read from L2)
+    const int nt = (d.PP + KW) >> 5, nkt = KW / 32;
     const int w = xcd_remap(blockIdx.x, gridDim.x);
-    const int m = w / nt, tile = w % nt;
-    const int kt = blockIdx.y;
+    const int kt = w % nkt, m = (w / nkt) / nt, tile = (w / nkt) % nt;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c0 = tile * 32;
     const bool isE = c0 >= d.PP;
@@ -1398,7 +1401,7 @@ void launch_prep(const Dims &d, const Bufs &b, hipStream_t s) {
     hipLaunchKernelGGL(k_prep, dim3(d.G), dim3(256), 0, s, d, b.Lam, b.omega, b.A, b.ZM);
 }
 void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s) {
-    const dim3 grid((d.NP / 128) * d.G, d.kp / 32);
+    const dim3 grid((d.NP / 128) * d.G * (d.kp / 32));
     switch (d.kp) {
     case 32: hipLaunchKernelGGL(k_wpass<32>, grid, dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W); break;
     case 64: hipLaunchKernelGGL(k_wpass<64>, grid, dim3(256), 0, s, d, b.Y, b.Lam, b.omega, b.W); break;
@@ -1444,7 +1447,7 @@ void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
     hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(64), 0, s, d, b.xall, b.XM, b.X, dr, iter);
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
-    const dim3 grid(((d.PP + d.kp) / 32) * d.G, d.kp / 32);
+    const dim3 grid(((d.PP + d.kp) / 32) * d.G * (d.kp / 32));
     switch (d.kp) {
     case 32: hipLaunchKernelGGL(k_cpass<32>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
     case 64: hipLaunchKernelGGL(k_cpass<64>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;

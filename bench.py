@@ -66,7 +66,8 @@ def pmc_traffic(kernel, workload_tag):
     f = ROOT / "profiles" / f"r01_{workload_tag}_pmc.json"
     if not f.exists():
         return None, None
-    k = json.load(open(f))["kernels"].get(kernel, {})
+    ks = json.load(open(f))["kernels"]
+    k = ks.get(kernel) or next((v for name, v in ks.items() if name.startswith(kernel + "_")), {})   # k_lambda_t
     return k.get("hbm_bytes_per_dispatch"), str(f.relative_to(ROOT))
 
 
