@@ -626,9 +626,12 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
 // touches only qb (compile-time pruning; ~3x fewer VALU ops per row than a
 // 32-lane row).  Then Lambda_j = L' \ (v + z) (dc:143-144) right-looking from
 // the bottom, psi_j (dc:150), SS_j = yy_j - 2 x.C_j + x'E x and ps_j, omega_j
-// (dc:169-171).  Plam_j = psi_j o tau' (dc:176) is formed from the previous
-// iteration's psi and tau unless plam_src is given (first iteration after
-// dcfm_set_state).  Every global load of the row is issued up front.
+// (dc:169-171), with x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j from the solve itself
+// (x'Q_j x = |L'x|^2 = |w|^2), so E is read once.  Plam_j = psi_j o tau' (dc:176) is
+// formed from the previous iteration's psi and tau unless plam_src is given (first
+// iteration after dcfm_set_state).  Every global load of the row, the row's draws
+// included, is issued up front: with 2 waves per SIMD nothing else hides a load
+// issued after the factorisation (measured: 64 -> 53 us at c3).
 // psi o lambda^2 of the row -> cpart[m][j][:] (k_colsum sums the rows).
 // ============================================================================
 
@@ -660,12 +663,18 @@ __global__ __launch_bounds__(64, DCFM_LAMBDA_MINWAVES) void k_lambda(Dims d, con
     const uint32_t ti = (uint32_t)(iter - dr.first_iter);
     const uint32_t drow = (ti * (uint32_t)d.g + (uint32_t)mg) * (uint32_t)d.P + (uint32_t)jj;
     const uint32_t toff = (uint32_t)mg * KP;
-    // ---- loads that form Q_j and b_j
+    // ---- loads that form Q_j and b_j, and the row's draws (all issued up front: the
+    //      draws arrive during the Q build and factorisation instead of stalling the solve)
     const double psj = valid ? ps[(uint32_t)(m * d.PP + jj)] : 0.0;
-    double tr0 = rv0 ? tau_cur[toff + r0] : 0.0, tr1 = rv1 ? tau_cur[toff + r1] : 0.0;
+    const double tr0 = rv0 ? tau_cur[toff + r0] : 0.0, tr1 = rv1 ? tau_cur[toff + r1] : 0.0;
     const double *pin = plam_src ? plam_src : psi;
     const double pin0 = rv0 ? pin[rowoff + r0] : 0.0, pin1 = rv1 ? pin[rowoff + r1] : 0.0;
-    double c0 = valid ? C[rowoff + r0] : 0.0, c1 = valid ? C[rowoff + r1] : 0.0;
+    const double c0 = valid ? C[rowoff + r0] : 0.0, c1 = valid ? C[rowoff + r1] : 0.0;
+    const uint32_t dk = drow * (uint32_t)d.K;
+    const double z0 = rv0 ? dr.NL[dk + r0] : 0.0, z1 = rv1 ? dr.NL[dk + r1] : 0.0;       // dc:142
+    const double G0 = rv0 ? dr.Gpsi[dk + r0] : 0.0, G1 = rv1 ? dr.Gpsi[dk + r1] : 0.0;   // dc:150
+    const double Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;                           // dc:170
+    const double yyj = (valid && l == 0) ? yy[(uint32_t)(m * d.PP + jj)] : 0.0;
     const double *Ea = E + ((uint32_t)m * KP + r0) * KP, *Eb = E + ((uint32_t)m * KP + r1) * KP;
     constexpr int KH = KP / 2;       // rows < 16 only ever touch columns < 16 (lower triangle)
     double qa[KH], qb[KP];
@@ -763,20 +772,6 @@ __global__ __launch_bounds__(64, DCFM_LAMBDA_MINWAVES) void k_lambda(Dims d, con
             asm volatile("" : "+v"(qb[c]));
         }
     });
-    // ---- the rest of the row's inputs (their latency hides under other waves' factorisations)
-    const uint32_t dk = drow * (uint32_t)d.K;
-    const double z0 = rv0 ? dr.NL[dk + r0] : 0.0, z1 = rv1 ? dr.NL[dk + r1] : 0.0;       // dc:142
-    const double G0 = rv0 ? dr.Gpsi[dk + r0] : 0.0, G1 = rv1 ? dr.Gpsi[dk + r1] : 0.0;   // dc:150
-    const double Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;                           // dc:170
-    const double yyj = (valid && l == 0) ? yy[(uint32_t)(m * d.PP + jj)] : 0.0;
-    {   // C and tau again from L2 rather than held across the factorisation
-        const double *C2 = C, *T2 = tau_cur;
-        asm volatile("" : "+s"(C2), "+s"(T2));
-        c0 = valid ? C2[rowoff + r0] : 0.0;
-        c1 = valid ? C2[rowoff + r1] : 0.0;
-        tr0 = rv0 ? T2[toff + r0] : 0.0;
-        tr1 = rv1 ? T2[toff + r1] : 0.0;
-    }
     // ---- back solve L' x = w, w = v + z (dc:142-144), pivots (c, c-1) from the bottom.
     //      x_c = (w_c - sum_{r>c} L[r][c] x_r) / L[c][c]: the sums over the rows below are
     //      dot products across the 16 lanes (rowsum16); L stays in the lanes' registers.
@@ -808,24 +803,13 @@ __global__ __launch_bounds__(64, DCFM_LAMBDA_MINWAVES) void k_lambda(Dims d, con
     });
     if (!rv0) xa = 0.0;
     if (!rv1) xb = 0.0;
-    // ---- SS_j = yy_j + sum_r x_r (E x)_r - 2 x_r C_jr  (x through the staging row)
-    Ls[r0] = xa;
-    Ls[r1] = xb;
-    double exa = 0.0, exb = 0.0;
-    // re-read the E rows from L2 (laundered pointers: keeping the first read's 48 doubles
-    // live across the factorisation would cost ~96 VGPRs)
-    const double *Ea2 = Ea, *Eb2 = Eb;
-    asm volatile("" : "+v"(Ea2), "+v"(Eb2));
-#pragma unroll
-    for (int c = 0; c < KP; c += 2) {
-        const d2 ea = *reinterpret_cast<const d2 *>(Ea2 + c), eb = *reinterpret_cast<const d2 *>(Eb2 + c);
-        const d2 xv = *reinterpret_cast<const d2 *>(Ls + c);
-        exa += ea.x * xv.x;
-        exa += ea.y * xv.y;
-        exb += eb.x * xv.x;
-        exb += eb.y * xv.y;
-    }
-    double contrib = xa * (exa - 2.0 * c0) + xb * (exb - 2.0 * c1);
+    // ---- SS_j = yy_j - 2 x.C_j + x'E x (dc:169 by identity, no Y pass).  x = L'^{-1} w, so
+    //      x'Q_j x = |w|^2 and x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j: no E re-read.
+    double contrib = fma(wa, wa, wb * wb);
+    contrib = fma(-plam0 * xa, xa, contrib);
+    contrib = fma(-plam1 * xb, xb, contrib);
+    contrib = contrib / psj - 2.0 * fma(xa, c0, xb * c1);
+    contrib = valid ? contrib : 0.0;
     contrib = rowsum16(contrib);
     // ---- psi (dc:150, tau of the previous iteration, Q11) and the outputs
     double psa = 0.0, psb = 0.0;

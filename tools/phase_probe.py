@@ -22,7 +22,7 @@ buf = (C.c_ulonglong * 32)()
 smp.run(1, 10); smp.synchronize(); lib.dcfm_debug_phases(buf)
 T = 20
 smp.run(11, T); smp.synchronize(); lib.dcfm_debug_phases(buf)
-waves = ((P + 7) // 8) * g * 4 if K <= 32 else P * g * 3
+waves = ((P + 3) // 4) * g if K <= 32 else P * g * 3
 tot = sum(buf[:8])
 for k in range(8):
     if buf[k]:
