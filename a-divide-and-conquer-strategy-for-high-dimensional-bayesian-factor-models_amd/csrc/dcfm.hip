@@ -959,6 +959,157 @@ int dcfm_get_sigma(dcfm_handle *h, double *out) {
     return DCFM_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Error of Sigmaout against a truth U U' + diag(s) (north_star
+// check 2), without Sigmaout leaving the device.  Frobenius norms come from the first
+// pass of k_sigma_err; the operator norm of M = Sigmaout - Sigma0 is the largest
+// |eigenvalue| of the Lanczos tridiagonal T_m (symmetric M; full reorthogonalisation,
+// twice, on the host: p x m doubles), found by Sturm-sequence bisection.
+// ---------------------------------------------------------------------------
+static int sturm_below(const std::vector<double> &a, const std::vector<double> &b, double x) {
+    int cnt = 0;
+    double q = 1.0;
+    for (size_t i = 0; i < a.size(); ++i) {
+        q = a[i] - x - (i ? b[i - 1] * b[i - 1] / q : 0.0);
+        if (q == 0.0) q = -1e-300;
+        if (q < 0.0) ++cnt;
+    }
+    return cnt;
+}
+static double tridiag_extreme(const std::vector<double> &a, const std::vector<double> &b, bool largest) {
+    const size_t m = a.size();
+    double lo = 0.0, hi = 0.0;
+    for (size_t i = 0; i < m; ++i) {   // Gershgorin interval
+        const double rad = (i ? std::fabs(b[i - 1]) : 0.0) + (i + 1 < m ? std::fabs(b[i]) : 0.0);
+        lo = i ? std::min(lo, a[i] - rad) : a[i] - rad;
+        hi = i ? std::max(hi, a[i] + rad) : a[i] + rad;
+    }
+    for (int it = 0; it < 200 && hi - lo > 0.0; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (mid <= lo || mid >= hi) break;
+        const int c = sturm_below(a, b, mid);
+        if (largest ? (c == (int)m) : (c >= 1)) hi = mid;
+        else lo = mid;
+    }
+    return 0.5 * (lo + hi);
+}
+static uint64_t splitmix64(uint64_t &x) {
+    uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+int dcfm_sigma_error(dcfm_handle *h, const double *U, int32_t r, const double *sdiag, int32_t iters,
+                     uint64_t seed, double out[3]) {
+    if (!h || !sdiag || !out || (r > 0 && !U)) return fail(h, DCFM_ERR_INVALID, "null argument");
+    if (r < 0 || r > 32) return fail(h, DCFM_ERR_INVALID, "truth rank r = %d outside 0..32", r);
+    if (iters < 0) return fail(h, DCFM_ERR_INVALID, "iters = %d < 0", iters);
+    HIPC(h, hipSetDevice(h->cfg.device));
+    sync_all(h);
+    const Dims &d = h->d;
+    const int p = d.p;
+    const size_t P = (size_t)p;
+    const int m = std::min<int>(iters, p);
+    double *dev = nullptr;
+    const size_t ns = (size_t)sigma_err_splits(p);
+    {
+        void *q = nullptr;
+        HIPC(h, hipMalloc(&q, (P * (size_t)std::max(r, 1) + 5 * P + 3 * ns * P) * sizeof(double)));
+        dev = static_cast<double *>(q);
+    }
+    // U, s, v, then the summed outputs y | fro | tru (contiguous), then the split partials
+    double *dU = dev, *ds = dU + P * std::max(r, 1), *dv = ds + P, *dy = dv + P, *dfro = dy + P, *dtru = dfro + P;
+    double *py = dtru + P, *pfro = py + ns * P, *ptru = pfro + ns * P;
+    int rc = DCFM_OK;
+    auto hip_ok = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && rc == DCFM_OK) rc = fail(h, DCFM_ERR_HIP, "sigma_error %s: %s", what, hipGetErrorString(e));
+        return rc == DCFM_OK;
+    };
+    if (r > 0) hip_ok(hipMemcpy(dU, U, P * r * sizeof(double), hipMemcpyHostToDevice), "upload U");
+    hip_ok(hipMemcpy(ds, sdiag, P * sizeof(double), hipMemcpyHostToDevice), "upload s");
+    std::vector<double> V, y(P), fro(P), tru(P), alpha, beta;
+    // one pass: y = M v (v may be null: norms only); collective over ranks
+    auto pass = [&](const double *vh, bool first) {
+        if (rc) return false;
+        if (vh && !hip_ok(hipMemcpyAsync(dv, vh, P * sizeof(double), hipMemcpyHostToDevice, h->stream), "upload v"))
+            return false;
+        launch_sigma_err(h->b.Sigma, p, dU, r, ds, vh ? dv : nullptr, d.rank, d.nranks, first, vh ? py : nullptr,
+                         pfro, ptru, dy, h->stream);
+        if (!hip_ok(hipGetLastError(), "launch")) return false;
+        if (d.nranks > 1) {
+            if (vh && (rc = coll_allreduce_sum(h, CH_ASM, dy, P, h->stream))) return false;
+            if (first && (rc = coll_allreduce_sum(h, CH_ASM, dfro, P, h->stream))) return false;
+            if (first && (rc = coll_allreduce_sum(h, CH_ASM, dtru, P, h->stream))) return false;
+        }
+        if (vh) hip_ok(hipMemcpyAsync(y.data(), dy, P * sizeof(double), hipMemcpyDeviceToHost, h->stream), "y");
+        if (first) {
+            hip_ok(hipMemcpyAsync(fro.data(), dfro, P * sizeof(double), hipMemcpyDeviceToHost, h->stream), "fro");
+            hip_ok(hipMemcpyAsync(tru.data(), dtru, P * sizeof(double), hipMemcpyDeviceToHost, h->stream), "tru");
+        }
+        return hip_ok(hipStreamSynchronize(h->stream), "sync");
+    };
+    auto dot = [&](const double *a, const double *b) {
+        double acc = 0.0;
+        for (size_t i = 0; i < P; ++i) acc += a[i] * b[i];
+        return acc;
+    };
+    if (m == 0) {
+        pass(nullptr, true);
+    } else {
+        V.assign(P * (size_t)(m + 1), 0.0);
+        uint64_t st = seed ^ 0x5DEECE66Dull;
+        for (size_t i = 0; i < P; i += 2) {   // Box-Muller normals: a rotation-invariant start
+            const double u1 = ((splitmix64(st) >> 11) + 1.0) * 0x1.0p-53, u2 = (splitmix64(st) >> 11) * 0x1.0p-53;
+            const double rr = std::sqrt(-2.0 * std::log(u1));
+            V[i] = rr * std::cos(6.283185307179586 * u2);
+            if (i + 1 < P) V[i + 1] = rr * std::sin(6.283185307179586 * u2);
+        }
+        const double n0 = std::sqrt(dot(V.data(), V.data()));
+        for (size_t i = 0; i < P; ++i) V[i] /= n0;
+        double bprev = 0.0;
+        for (int j = 0; j < m; ++j) {
+            double *vj = V.data() + P * j, *vn = V.data() + P * (j + 1);
+            if (!pass(vj, j == 0)) break;
+            const double a = dot(y.data(), vj);
+            const double *vp = j ? vj - P : vj;
+            const double bp = j ? bprev : 0.0;
+            for (size_t i = 0; i < P; ++i) vn[i] = y[i] - a * vj[i] - bp * vp[i];
+            for (int rep = 0; rep < 2; ++rep)
+                for (int i2 = 0; i2 <= j; ++i2) {
+                    const double *vi = V.data() + P * i2;
+                    const double c = dot(vn, vi);
+                    for (size_t i = 0; i < P; ++i) vn[i] -= c * vi[i];
+                }
+            const double bn = std::sqrt(dot(vn, vn));
+            alpha.push_back(a);
+            double scale = std::fabs(a);
+            for (double x : alpha) scale = std::max(scale, std::fabs(x));
+            if (bn <= 1e-13 * std::max(scale, 1e-300)) break;   // invariant subspace: T is exact
+            beta.push_back(bn);
+            for (size_t i = 0; i < P; ++i) vn[i] /= bn;
+            bprev = bn;
+        }
+    }
+    if (rc == DCFM_OK) {
+        double fs = 0.0, ts = 0.0;
+        for (size_t i = 0; i < P; ++i) {
+            fs += fro[i];
+            ts += tru[i];
+        }
+        out[0] = std::sqrt(fs);
+        out[1] = std::sqrt(ts);
+        out[2] = 0.0;
+        if (!alpha.empty()) {
+            beta.resize(alpha.size() - 1);
+            out[2] = std::max(std::fabs(tridiag_extreme(alpha, beta, true)),
+                              std::fabs(tridiag_extreme(alpha, beta, false)));
+        }
+    }
+    (void)hipFree(dev);
+    return rc;
+}
+
 int dcfm_set_profiling(dcfm_handle *h, int enable) {
     return dcfm_set_profiling_mask(h, enable ? 0xFFFFFFFFu : 0u);
 }

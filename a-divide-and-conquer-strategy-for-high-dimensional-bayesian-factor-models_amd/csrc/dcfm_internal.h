@@ -88,6 +88,12 @@ void launch_assemble(const Dims &d, const Bufs &b, const double *Lb, const doubl
                      double inv_eff, hipStream_t s);
 void launch_sigma_cols(const double *S, int p, int c0, int nc, double *out, hipStream_t s);
 void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s);
+// sigma_err.hip: rows' sums of (Sigmaout - U U' - diag s) v, squares and truth squares
+// (partials [splits][p] in y / fro / tru; summed into out[0..p), out[p..2p), out[2p..3p))
+int sigma_err_splits(int p);
+void launch_sigma_err(const double *S, int p, const double *U, int R, const double *sdiag, const double *v,
+                      int rank, int nranks, bool first, double *y, double *fro, double *tru, double *out,
+                      hipStream_t s);
 void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s);
 // dst[i] = sum_k src[k * count + i] in slice order (loopback all-reduce)
 void launch_sum_slices(const double *src, int ns, size_t count, double *dst, hipStream_t s);

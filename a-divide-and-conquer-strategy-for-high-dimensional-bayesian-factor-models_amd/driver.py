@@ -139,3 +139,16 @@ def divideconquer(Y, g, k, BURNIN, MCMC, thin, rho, *, seed=0, hyper: Hyper = Hy
         return Sigmaout, {"varind": np.asarray(init.varind), "keep": keep, "n": n, "p": p, "P": P,
                           "K": K, "N": N, "seconds": elapsed}
     return Sigmaout
+
+
+def truth_factors(Lam0, sig2, Y, keep, varind):
+    """Truth Sigma0 = Lam0 Lam0' + diag(sig2) as (U, s) in Sigmaout's coordinates: kept
+    columns (dc:36-39), permuted by varind (dc:50-54), standardised by the sample
+    standard deviations (dc:57-59), so Sigma0_out = U U' + diag(s) — the low-rank form
+    dcfm_sigma_error takes."""
+    Y = np.asarray(Y, dtype=np.float64)
+    cols = np.asarray(keep)[np.asarray(varind)]
+    sd = Y[:, cols].std(axis=0, ddof=1)
+    U = np.asarray(Lam0, dtype=np.float64)[cols] / sd[:, None]
+    s = np.asarray(sig2, dtype=np.float64)[cols] / (sd * sd)
+    return U, s

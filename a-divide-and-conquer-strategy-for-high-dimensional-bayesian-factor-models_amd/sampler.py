@@ -167,6 +167,18 @@ class Sampler:
         self._check(self.lib.dcfm_get_sigma_cols(self.h, int(col0), int(ncols), _ptr(S)))
         return S
 
+    def sigma_error(self, U, s, iters: int = 60, seed: int = 1) -> dict:
+        """Frobenius / operator-norm error of Sigmaout against U U' + diag(s), on the device
+        (dcfm_sigma_error).  U: p x r truth factors in output coordinates, s: p."""
+        p = self.P * self.g
+        U = _f64F(np.asarray(U, dtype=np.float64).reshape(p, -1))
+        s = _f64F(np.asarray(s, dtype=np.float64).reshape(p))
+        out = np.zeros(3)
+        self._check(self.lib.dcfm_sigma_error(self.h, _ptr(U), U.shape[1], _ptr(s), int(iters),
+                                              int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(out)))
+        fro, tru, op = (float(x) for x in out)
+        return {"fro": fro, "op": op, "fro_rel": fro / tru if tru > 0 else float("nan"), "truth_fro": tru}
+
     def saved_samples(self) -> int:
         return int(self.lib.dcfm_saved_samples(self.h))
 

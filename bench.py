@@ -32,14 +32,15 @@ FP64_MFMA_PEAK_TFLOPS = 78.6      # MI355X dense fp64 matrix (spec; = fp64 vecto
 HBM_PEAK_GBS = 8000.0             # MI355X HBM3E spec
 
 
-def synth_data(n, p, k0=10, sparsity=0.7, seed=20161209):
-    """Sparse-factor synthetic data: Y = F L0' + E."""
+def synth_data(n, p, k0=10, sparsity=0.7, seed=20161209, factors=False):
+    """Sparse-factor synthetic data: Y = F L0' + E (with ``factors``: also L0, sig2)."""
     r = np.random.Generator(np.random.PCG64(seed))
     L0 = r.standard_normal((p, k0))
     L0[r.random((p, k0)) < sparsity] = 0.0
     sig2 = r.uniform(0.2, 1.0, size=p)
     F = r.standard_normal((n, k0))
-    return F @ L0.T + r.standard_normal((n, p)) * np.sqrt(sig2)[None, :]
+    Y = F @ L0.T + r.standard_normal((n, p)) * np.sqrt(sig2)[None, :]
+    return (Y, L0, sig2) if factors else Y
 
 
 def algorithmic_work(kname, d, n_launch_samples):
@@ -112,6 +113,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--err-iters", type=int, default=20,
+                    help="Lanczos steps of the on-device truth error after the timed region (0: off)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,7 +136,7 @@ def main():
     n_prof = 0 if args.no_profile else args.steps     # untimed per-kernel profiling pass
     N = args.warmup + n_prof + args.steps
     burnin, mcmc = 0, N
-    Y = synth_data(n, p)
+    Y, L0, sig2 = synth_data(n, p, factors=True)
     hyper = dcfm.Hyper()
     Yk, n, pk, P, K_, keep = dcfm.preprocess(Y, g, K * g)
     init = dcfm.driver._HostInitDraws(1, n, pk, g, K, hyper)
@@ -150,6 +153,7 @@ def main():
         smp.comm_init(obj[0])
     smp.set_data(Yd[:, :, s0:s0 + gl])
     smp.set_state(dcfm.local_state(state, s0, gl))
+    U_true, s_true = dcfm.truth_factors(L0, sig2, Y, keep, init.varind)
     del Y, Yk, Yd
 
     have_torch_gpu = torch.cuda.is_available()
@@ -188,6 +192,23 @@ def main():
     live = smp.kernel_stats().get(dominant) if dominant else None
     saved_prof = sum(1 for t in range(args.warmup + 1, args.warmup + 1 + n_prof) if t % thin == 0)
     saved_in_region = sum(1 for t in range(first_t, first_t + args.steps) if t % thin == 0)
+    # (3) after the timed region: the posterior-mean covariance error against the synthetic
+    #     truth on the device (dcfm_sigma_error) — one norms-only pass (its HBM rate: the full
+    #     p x p read from the stored triangle, 8 p^2 bytes) and a Lanczos operator norm
+    sig_err = None
+    if args.err_iters > 0:
+        sync()
+        te = time.perf_counter()
+        e0 = smp.sigma_error(U_true, s_true, iters=0)
+        t_pass = time.perf_counter() - te
+        te = time.perf_counter()
+        e1 = smp.sigma_error(U_true, s_true, iters=args.err_iters)
+        t_lz = time.perf_counter() - te
+        sig_err = {"fro_rel": round(e0["fro_rel"], 6), "op": round(e1["op"], 6),
+                   "lanczos_iters": args.err_iters, "pass_ms": round(t_pass * 1e3, 3),
+                   "pass_gbs": round(8.0 * p * p / t_pass / 1e9, 1),
+                   "lanczos_ms": round(t_lz * 1e3, 2),
+                   "note": "after the timed region; chain of warmup+steps iterations, not converged"}
     smp.close()
 
     if world > 1:
@@ -250,6 +271,8 @@ def main():
     if "k_assemble" in kern:
         out["assembly_mfma_util"] = round(kern["k_assemble"]["tflops"] / FP64_MFMA_PEAK_TFLOPS, 4)
     out["kernels"] = kern
+    if sig_err:
+        out["sigma_error"] = sig_err
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_run(n, p, g, K, rho, steps=args.cpu_steps, thin=thin)
     if rank == 0:

@@ -141,6 +141,15 @@ int  dcfm_get_sigma(dcfm_handle *h, double *out);
  * device scratch of only p x ncols.  Collective when nranks > 1. */
 int  dcfm_get_sigma_cols(dcfm_handle *h, int64_t col0, int64_t ncols, double *out);
 int64_t dcfm_saved_samples(const dcfm_handle *h);
+/* Error of Sigmaout against a truth Sigma0 = U U' + diag(s) given in the same permuted,
+ * standardised coordinates (U: p x r column-major, r <= 32; s: p), computed on the
+ * device (Sigmaout never leaves HBM; c5: 80 GB).  out[0] = ||Sigmaout - Sigma0||_F,
+ * out[1] = ||Sigma0||_F, out[2] = ||Sigmaout - Sigma0||_2 from `iters` Lanczos steps
+ * (seeded start, full reorthogonalisation; exact when iters >= p; 0 skips it).  The
+ * reference leaves this to the caller (Frobenius and
+ * operator-norm error against the synthetic truth).  Collective when nranks > 1. */
+int  dcfm_sigma_error(dcfm_handle *h, const double *U, int32_t r, const double *s, int32_t iters,
+                      uint64_t seed, double out[3]);
 
 /* ---- measurement --------------------------------------------------------- */
 /* Per-kernel HIP-event timing on the handle's stream (off by default).

@@ -20,7 +20,8 @@ DATA_SEED = 20161209
 
 
 def make_data(n: int, p: int, k0: int = 10, sparsity: float = 0.7, seed: int = DATA_SEED,
-              zero_cols: int = 0):
+              zero_cols: int = 0, factors: bool = False):
+    """Y (n x p) and Sigma0; with ``factors`` also (Lambda0, sigma0^2) of Sigma0."""
     r = np.random.Generator(np.random.PCG64(seed))
     Lam0 = r.standard_normal((p, k0))
     Lam0[r.random((p, k0)) < sparsity] = 0.0
@@ -32,6 +33,8 @@ def make_data(n: int, p: int, k0: int = 10, sparsity: float = 0.7, seed: int = D
     if zero_cols:
         cols = r.choice(p, size=zero_cols, replace=False)
         Y[:, cols] = 0.0
+    if factors:
+        return Y, Sigma0, Lam0, sig2
     return Y, Sigma0
 
 

@@ -140,3 +140,16 @@ def test_posterior_mean_recovers_truth():
     err = oracle.synth.cov_errors(Sig, truth)
     assert np.all(np.isfinite(Sig)) and err["fro_rel"] < 0.8, err
     assert np.allclose(np.diag(Sig), 1.0, atol=0.25)           # standardised units (dc:57-59)
+
+
+def test_truth_factors_match_dense_truth():
+    """driver.truth_factors (the low-rank form dcfm_sigma_error takes) equals the dense
+    truth in Sigmaout's coordinates (kept columns, varind order, standardised; dc:36-59)."""
+    import __graft_entry__ as ge
+    dcfm = ge.load_package()
+    from helpers import make_case
+    c = make_case(50, 90, 3, 4, seed=5, k0=4, zero_cols=3)
+    _, _, Lam0, sig2 = oracle.synth.make_data(50, 90, k0=4, zero_cols=3, factors=True)
+    U, s = dcfm.truth_factors(Lam0, sig2, c["Y"], c["keep"], c["init"].varind)
+    dense = oracle.synth.truth_in_output_space(c["Sigma0"], c["Y"], c["keep"], c["init"].varind)
+    np.testing.assert_allclose(U @ U.T + np.diag(s), dense, rtol=1e-13, atol=1e-13)
