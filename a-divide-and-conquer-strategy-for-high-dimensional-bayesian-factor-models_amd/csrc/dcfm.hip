@@ -304,15 +304,23 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     h->cfg = c;
     h->cfg.nranks = nranks;
     HIPC(h, hipSetDevice(c.device));
-    HIPC(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    // Stream priorities: the sweep chain (main, side) at the greatest priority, the draws
+    // a batch ahead and the covariance assembly at the least, so the dispatcher hands
+    // freed CUs to the latency-critical chain first (DCFM_STREAM_PRIO=0: all default).
+    int prio_lo = 0, prio_hi = 0;
+    {
+        const char *pe = std::getenv("DCFM_STREAM_PRIO");
+        if (!(pe && pe[0] == '0')) HIPC(h, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    }
+    HIPC(h, hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi));
     {   // DCFM_SERIALIZE=1: one stream for everything (isolated per-kernel timings)
         const char *ser = std::getenv("DCFM_SERIALIZE");
         if (ser && ser[0] == '1') {
             h->side = h->sasm = h->sdraw = h->stream;
         } else {
-            HIPC(h, hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-            HIPC(h, hipStreamCreateWithFlags(&h->sdraw, hipStreamNonBlocking));
-            HIPC(h, hipStreamCreateWithFlags(&h->sasm, hipStreamNonBlocking));
+            HIPC(h, hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_hi));
+            HIPC(h, hipStreamCreateWithPriority(&h->sdraw, hipStreamNonBlocking, prio_lo));
+            HIPC(h, hipStreamCreateWithPriority(&h->sasm, hipStreamNonBlocking, prio_lo));
         }
     }
     HIPC(h, hipEventCreateWithFlags(&h->e_lam, hipEventDisableTiming));

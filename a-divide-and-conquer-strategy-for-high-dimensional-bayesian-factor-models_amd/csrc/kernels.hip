@@ -1305,6 +1305,9 @@ __device__ __forceinline__ void draw_normal_row(const Rng &rng, uint32_t site, u
 // and the normal segments (high occupancy); b_off = first block of the launch
 template <bool GAMMAS>
 __global__ __launch_bounds__(256) void k_draws(Dims d, DrawsDev dr, int64_t iter) {
+#ifdef DCFM_VARIANT_NODRAWS
+    if (iter >= 0) return;   // development A/B only: the chain without RNG cost
+#endif
     const DrawPlan pl = draw_plan(d);
     const Rng rng(d.seed);
     const uint32_t it = (uint32_t)iter;

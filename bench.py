@@ -102,10 +102,10 @@ def cpu_baseline_run(n, p, g, K, rho, steps=5, thin=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=480)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--thin", type=int, default=5)
-    ap.add_argument("--asm-batch", type=int, default=32)
+    ap.add_argument("--asm-batch", type=int, default=96)
     ap.add_argument("--g", type=int, default=64)
     ap.add_argument("--P", type=int, default=312)
     ap.add_argument("--n", type=int, default=1000)
