@@ -538,7 +538,7 @@ __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
 //   trailing tile takes A_IK -= L_IJ L_KJ' (4 MFMAs, both operands read from the panel).
 // Three barriers per block column (the per-pivot kernel needs two per pivot).  The L
 // tiles stay in the registers for the blocked back solve x = L^{-T}(v + z); the epilogue
-// (psi, SS identity, ps, omega, cpart) is the one of k_lambda above.
+// forms psi, cpart and SS_j from |w|^2 (no E product), then ps, omega.
 // ============================================================================
 #ifndef DCFM_LT_MINW
 #define DCFM_LT_MINW 3
@@ -554,6 +554,7 @@ __global__ __launch_bounds__(256, DCFM_LT_MINW) void k_lambda_t(
     __shared__ double Sd[TZ], Ud[TZ], Pn[NBM * TZ];
     __shared__ double vb[KW], vx[KW], part[NBM * 16];
     __shared__ double lds_l[32], lds_u[16];
+    __shared__ double ein[5][KW];   // per row index r: NL, Gpsi, tau, C, Plam
     const int j = blockIdx.x, m = blockIdx.y, mg = d.shard0 + m;
     const int t = threadIdx.x, lane = t & 63, c16 = lane & 15, q = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);   // scalar: tile coordinates live in SGPRs
@@ -562,6 +563,26 @@ __global__ __launch_bounds__(256, DCFM_LT_MINW) void k_lambda_t(
     const double *Em = E + (size_t)m * KW * KW;
     const size_t rowoff = ((size_t)m * d.PP + j) * KW;
     const double psj = ps[(size_t)m * d.PP + j];
+    // the row's draws and epilogue inputs, issued with the Q_j loads: a load issued after
+    // the factorisation stalls the solve (nothing else hides it at 3 waves per SIMD)
+    // (parked in LDS, not registers: the NB = 7, 8 tile sets use every VGPR of 3 waves/SIMD)
+    const size_t drow = ((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j;
+    if (t < KW) {
+        double zr = 0.0, Gr = 0.0, trr = 0.0, cr = 0.0, plr = 0.0;
+        if (t < K) {
+            zr = dr.NL[drow * d.K + t];                                     // dc:142
+            Gr = dr.Gpsi[drow * d.K + t];                                   // dc:150
+            trr = tau_cur[(size_t)mg * KW + t];
+            cr = C[rowoff + t];
+            plr = plam_src ? plam_src[rowoff + t] : psi[rowoff + t] * trr;  // dc:176
+        }
+        ein[0][t] = zr;
+        ein[1][t] = Gr;
+        ein[2][t] = trr;
+        ein[3][t] = cr;
+        ein[4][t] = plr;
+    }
+    const double yyj = yy[(size_t)m * d.PP + j], Gps = dr.Gps[drow];   // dc:169-170
     // ---- Q_j tiles (dc:141: ps_j eta2 + diag(Plam_j)), identity padding
     d4 acc[SL];
     int tI[SL], tK[SL];
@@ -592,7 +613,7 @@ __global__ __launch_bounds__(256, DCFM_LT_MINW) void k_lambda_t(
             }
         }
     }
-    if (t < KW) vb[t] = (t < K) ? psj * C[rowoff + t] : 0.0;          // blam (dc:141)
+    if (t < KW) vb[t] = psj * ein[3][t];                              // blam (dc:141)
     // ---- blocked factorisation with the forward solve
     for (int J = 0; J < nb; ++J) {
         const int td = J * (J + 1) / 2 + J, ow = td & 3, os = td >> 2;
@@ -658,7 +679,7 @@ __global__ __launch_bounds__(256, DCFM_LT_MINW) void k_lambda_t(
         }
     }
     // ---- w = v + z (dc:142 normrnd), blocked back solve x_J = U_JJ' (w_J - sum_{I>J} L_IJ' x_I)
-    if (t < KW && t < K) vb[t] += dr.NL[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + t];
+    if (t < K) vb[t] += ein[0][t];
     __syncthreads();
     for (int J = nb - 1; J >= 0; --J) {
 #pragma unroll
@@ -693,20 +714,33 @@ __global__ __launch_bounds__(256, DCFM_LT_MINW) void k_lambda_t(
         }
         __syncthreads();
     }
-    // ---- epilogue: Lambda_j, psi_j (dc:150); SS, ps_j, omega_j follow in k_ss
+    // ---- epilogue: Lambda_j, psi_j (dc:150), and SS_j = yy_j - 2 x.C_j + x'E x (dc:169 by
+    //      identity) with x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j, since x'Q_j x = |w|^2
+    //      for x = L'^{-1} w: no Lambda_m E_m product (formerly k_ss), then ps_j, omega_j
+    double ssr = 0.0;
     if (t < KW) {
         const int r = t;
         const double xr = (r < K) ? vx[r] : 0.0;
         double psir = 0.0;
         if (r < K) {
-            const double tr = tau_cur[(size_t)mg * KW + r];
-            const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xr * xr * tr));
-            const double G = dr.Gpsi[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + r];
-            psir = scale * G;
+            const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xr * xr * ein[2][r]));
+            psir = scale * ein[1][r];
             psi[rowoff + r] = psir;
+            const double w = vb[r];
+            ssr = fma(w, w, -ein[4][r] * xr * xr) / psj - 2.0 * xr * ein[3][r];
         }
         Lam[rowoff + r] = xr;
         cpart[rowoff + r] = psir * (xr * xr);          // mat = psijh .* Lambda.^2 (dc:156)
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ssr += __shfl_xor(ssr, o, 64);
+    if (lane == 0) part[wave] = ssr;                   // part[] is free after the back solve
+    __syncthreads();
+    if (t == 0) {
+        const double SS = yyj + ((part[0] + part[1]) + (part[2] + part[3]));
+        const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;      // dc:170
+        ps[(size_t)m * d.PP + j] = psn;
+        omega[(size_t)m * d.PP + j] = 1.0 / psn;                 // dc:171 (Q1)
     }
 }
 
@@ -933,8 +967,6 @@ void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t ite
     default: LT(128, 8); break;
     }
 #undef LT
-    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_ss<KW>, dim3((d.P + 15) / 16, d.G), dim3(256), 0, s, d, b.Lam, b.C,
-                                           b.E, b.yy, b.ps, b.omega, dr, iter));
 }
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
                   const double *tau_in, double *delta_out, double *tau_out, hipStream_t s) {
