@@ -152,3 +152,26 @@ def truth_factors(Lam0, sig2, Y, keep, varind):
     U = np.asarray(Lam0, dtype=np.float64)[cols] / sd[:, None]
     s = np.asarray(sig2, dtype=np.float64)[cols] / (sd * sd)
     return U, s
+
+
+def output_columns(keep, varind):
+    """Input column index of each Sigmaout row/column: kept columns (dc:36-39) in the
+    varind order of the partition (dc:50-54) — Sigmaout's coordinates (quirk Q7)."""
+    return np.asarray(keep)[np.asarray(varind)]
+
+
+def unpermute_sigma(S, keep, varind, p_orig, sd=None, fill=0.0):
+    """Sigmaout back in the input's column order: S[a, b] goes to (cols[a], cols[b]) with
+    cols = output_columns(keep, varind); rows/columns of dropped (all-zero, dc:36-39)
+    columns get ``fill``.  With ``sd`` (the sample standard deviations of the kept
+    columns in Sigmaout's order, dc:57) the standardisation is undone: S_ab sd_a sd_b.
+    The reference returns the permuted, standardised matrix and leaves this to the
+    caller."""
+    S = np.asarray(S, dtype=np.float64)
+    cols = output_columns(keep, varind)
+    if sd is not None:
+        sd = np.asarray(sd, dtype=np.float64)
+        S = S * sd[:, None] * sd[None, :]
+    out = np.full((p_orig, p_orig), fill, dtype=np.float64)
+    out[np.ix_(cols, cols)] = S
+    return out

@@ -108,11 +108,14 @@ def main():
     ap.add_argument("--asm-batch", type=int, default=96)
     ap.add_argument("--g", type=int, default=64)
     ap.add_argument("--P", type=int, default=312)
-    ap.add_argument("--n", type=int, default=1000)
+    ap.add_argument("--n", "--nobs", dest="n", type=int, default=1000)   # --nobs under torchrun (--n is ambiguous there)
     ap.add_argument("--K", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--chains", action="store_true",
+                    help="one independent chain per rank (config c4: parallel chains, seed 1 + rank, no "
+                         "collectives; weak scaling) instead of splitting the shards of one chain")
     ap.add_argument("--err-iters", type=int, default=20,
                     help="Lanczos steps of the on-device truth error after the timed region (0: off)")
     args = ap.parse_args()
@@ -142,12 +145,16 @@ def main():
     init = dcfm.driver._HostInitDraws(1, n, pk, g, K, hyper)
     Yd = dcfm.partition_standardize(Yk, g, init.varind)
     state = dcfm.initial_state(n, P, K, g, rho, hyper, init)
-    gl = g // world
-    s0 = rank * gl
+    chains = args.chains
+    shard_ranks = 1 if chains else world        # ranks that split one chain's shards
+    gl = g // shard_ranks
+    s0 = 0 if chains else rank * gl
 
-    smp = dcfm.Sampler(n, P, g, K, rho, burnin, mcmc, thin, seed=1, nranks=world, rank=rank,
-                       device=local_rank, asm_batch=args.asm_batch)
-    if world > 1:
+    ndev = max(1, torch.cuda.device_count())     # counting devices does not initialise the GPU
+    smp = dcfm.Sampler(n, P, g, K, rho, burnin, mcmc, thin, seed=1 + (rank if chains else 0),
+                       nranks=shard_ranks, rank=0 if chains else rank, device=local_rank % ndev,
+                       asm_batch=args.asm_batch)
+    if shard_ranks > 1:
         obj = [dcfm.Sampler.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         smp.comm_init(obj[0])
@@ -216,8 +223,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    value = args.steps / dt
-    d = {"n": n, "P": P, "K": K, "G": gl, "p": p, "nranks": world}
+    value = args.steps / dt * (world if chains else 1)     # chains: iterations of all chains
+    d = {"n": n, "P": P, "K": K, "G": gl, "p": p, "nranks": shard_ranks}
     kern = {}
     roof = None
     def work_of(name, cnt, saved, iters):
@@ -258,14 +265,17 @@ def main():
                 "note": "achieved = algorithmic work per launch / mean HIP-event duration of this kernel, "
                         "events recorded around it alone inside the timed region"}
 
+    wtag = {(64, 312, 1000, 30): "c3", (8, 1250, 2000, 100): "c4", (256, 391, 2000, 30): "c5"}.get(
+        (g, P, n, K), "custom")
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "iter/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "higher_is_better": True, "scaling": "weak" if chains else "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (sparse factor model, seed 20161209; random init via driver dc:68-87)",
-        "config": {"workload": f"c3: p={p} (P={P} x g={g}), n={n}, K={K} (k={K * g}), rho={rho}, "
+        "config": {"workload": f"{wtag}: p={p} (P={P} x g={g}), n={n}, K={K} (k={K * g}), rho={rho}, "
                                f"thin={thin}, burnin=0 (assembly in timed region), asm_batch={args.asm_batch}",
-                   "global_batch": n, "parallelism": f"shards{g}/gpus{world}"},
+                   "global_batch": n,
+                   "parallelism": f"chains{world} (1 per GPU)" if chains else f"shards{g}/gpus{world}"},
         "roofline": roof,
     }
     if "k_assemble" in kern:

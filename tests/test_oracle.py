@@ -153,3 +153,20 @@ def test_truth_factors_match_dense_truth():
     U, s = dcfm.truth_factors(Lam0, sig2, c["Y"], c["keep"], c["init"].varind)
     dense = oracle.synth.truth_in_output_space(c["Sigma0"], c["Y"], c["keep"], c["init"].varind)
     np.testing.assert_allclose(U @ U.T + np.diag(s), dense, rtol=1e-13, atol=1e-13)
+
+
+def test_unpermute_sigma_restores_input_order():
+    """driver.unpermute_sigma undoes the output coordinates (Q7): the dense truth in
+    Sigmaout's permuted, standardised space maps back to Sigma0 on the kept columns."""
+    import __graft_entry__ as ge
+    dcfm = ge.load_package()
+    from helpers import make_case
+    c = make_case(40, 60, 4, 4, seed=9, k0=3, zero_cols=4)
+    S_out = oracle.synth.truth_in_output_space(c["Sigma0"], c["Y"], c["keep"], c["init"].varind)
+    cols = dcfm.output_columns(c["keep"], c["init"].varind)
+    sd = c["Y"][:, cols].std(axis=0, ddof=1)
+    back = dcfm.unpermute_sigma(S_out, c["keep"], c["init"].varind, 60, sd=sd, fill=np.nan)
+    keep = np.asarray(c["keep"])
+    np.testing.assert_allclose(back[np.ix_(keep, keep)], c["Sigma0"][np.ix_(keep, keep)], rtol=1e-13, atol=1e-13)
+    dropped = np.setdiff1d(np.arange(60), keep)
+    assert dropped.size and np.all(np.isnan(back[dropped]))
