@@ -347,6 +347,11 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     d.as_ = c.as_; d.bs = c.bs; d.df = c.df; d.ad1 = c.ad1; d.bd1 = c.bd1; d.ad2 = c.ad2; d.bd2 = c.bd2;
     d.seed = c.seed;
     d.inject = (c.flags & DCFM_FLAG_INJECT_DRAWS) ? 1 : 0;
+    // fused narrow chain on several ranks: column sums and the A sum travel in one message
+    const bool packed = nranks > 1 && d.kp == KP &&
+                        !([] { const char *e = std::getenv("DCFM_NOFUSE"); return e && e[0] == '1'; }());
+    d.sgap = packed ? KP * KP : 0;
+    d.xstride = packed ? d.G * KP + KP * KP : d.kp * d.kp;
     h->B = c.asm_batch > 0 ? c.asm_batch : 32;
 
     Bufs &b = h->b;
@@ -371,8 +376,17 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     ALLOC(b.Sp, G * NP * KP);
     ALLOC(b.xin, NP * KP);
     if (nranks > 1) { ALLOC(b.xall, (size_t)nranks * NP * KP); } else b.xall = b.xin;
-    ALLOC(b.xa, KP * KP);
-    ALLOC(b.xa_all, (size_t)nranks * KP * KP);
+    if (d.sgap) {   // packed message [sloc | xa] and its gather (dcfm_internal.h, Dims::sgap)
+        const size_t msg = (size_t)G * KP + KP * KP;
+        ALLOC(b.sloc, msg);
+        b.xa = b.sloc + (size_t)G * KP;
+        ALLOC(b.msg_all, (size_t)nranks * msg);
+        b.sall = b.msg_all;
+        b.xa_all = b.msg_all + (size_t)G * KP;
+    } else {
+        ALLOC(b.xa, KP * KP);
+        ALLOC(b.xa_all, (size_t)nranks * KP * KP);
+    }
     ALLOC(b.XM, 2 * KP * KP);
     ALLOC(b.xpart, 8 * KP * KP);          // k_deltaops: min(8, G) chunk sums
     {
@@ -383,8 +397,10 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     ALLOC(b.C, G * PP * KP);
     ALLOC(b.E, G * KP * KP);
     ALLOC(b.cpart, G * PP * KP);
-    ALLOC(b.sloc, G * KP);
-    if (nranks > 1) { ALLOC(b.sall, g * KP); } else b.sall = b.sloc;
+    if (!d.sgap) {
+        ALLOC(b.sloc, G * KP);
+        if (nranks > 1) { ALLOC(b.sall, g * KP); } else b.sall = b.sloc;
+    }
     ALLOC(b.Lb[0], p * (size_t)b.LDB);
     ALLOC(b.Lb[1], p * (size_t)b.LDB);
     ALLOC(b.wsum[0], p);
@@ -809,8 +825,10 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         KTimer t(h, DCFM_K_PREP, s);
         launch_colgram(d, b, false, s);
         launch_deltaops(d, b, h->dr, first_iter, false, nullptr, nullptr, nullptr, nullptr, s);
-        if (d.nranks > 1)
-            if (int rc = coll_allgather(h, CH_MAIN, b.xa, b.xa_all, KW * KW, s)) return rc;
+        if (d.nranks > 1)   // the packed message (column sums unused here) or the A sum alone
+            if (int rc = d.sgap ? coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)
+                                : coll_allgather(h, CH_MAIN, b.xa, b.xa_all, KW * KW, s))
+                return rc;
     }
     for (int64_t it = first_iter; it < end_iter; ++it) {
         if (!d.inject && (it == first_iter || it == batch0 + batch_n)) {
@@ -860,7 +878,23 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s);
         }
         h->plam_valid = false;
-        if (fused) {   // + the next iteration's grams and Z operators
+        if (fused && d.sgap) {   // several ranks: ONE all-gather of [column sums | A sum]
+            { KTimer t(h, DCFM_K_COLSUM, s); launch_colgram(d, b, true, s); }
+            {   // Z operators + the local A sum (independent of delta), then the message
+                KTimer t(h, DCFM_K_DELTA, s);
+                launch_deltaops(d, b, dr, it, false, nullptr, nullptr, nullptr, nullptr, s, true);
+            }
+            {
+                KTimer t(h, DCFM_K_COMM, s);
+                if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)) return rc;
+            }
+            {
+                KTimer t(h, DCFM_K_DELTA, s);
+                launch_deltaops(d, b, dr, it, true, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s, false);
+            }
+            h->prep_valid = true;
+        } else if (fused) {   // + the next iteration's grams and Z operators
             { KTimer t(h, DCFM_K_COLSUM, s); launch_colgram(d, b, true, s); }
             if (d.nranks > 1) {
                 KTimer t(h, DCFM_K_COMM, s);

@@ -43,6 +43,11 @@ struct Dims {
     double as_, bs, df, ad1, bd1, ad2, bd2;
     uint64_t seed;
     int inject;
+    // gathered-message layout of the fused several-rank chain: the per-rank message is
+    // [sloc G x KP | sum_m A_m KP x KP] (one all-gather per iteration for both), so rank
+    // r's column sums sit at r * (G*KP + KP*KP) and its A sum at that + G*KP.  sgap = KP*KP
+    // and xstride = G*KP + KP*KP there; sgap = 0, xstride = KW*KW for separate gathers.
+    int sgap, xstride;
 };
 
 // injected draws on device, [T][...] with T = n_iter of dcfm_set_draws
@@ -58,6 +63,7 @@ struct Bufs {
     double *xa, *xa_all, *XM;          // per-rank sum of A, gathered sums, X-draw operators
     double *xpart;                     // k_deltaops chunk sums of A (8 x KP x KP)
     unsigned *ticket;                  // k_deltaops last-arrival ticket (0 between launches)
+    double *msg_all;                   // packed gather target (fused, nranks > 1), else null
     int2 *tiles;
     int ntiles, LDB;
 };
@@ -69,9 +75,10 @@ void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s);
 // fused one-rank narrow launches (kernels.hip: k_colgram, k_deltaops, k_zxchol)
 void launch_colgram(const Dims &d, const Bufs &b, bool colsum, hipStream_t s);
+// ops: the xsum-tree + Z-operator blocks; delta: the delta/tau chain blocks (reads sall)
 void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool delta,
                      const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
-                     hipStream_t s);
+                     hipStream_t s, bool ops = true);
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_asum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);

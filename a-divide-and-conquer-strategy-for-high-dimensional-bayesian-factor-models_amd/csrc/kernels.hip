@@ -441,7 +441,7 @@ __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict_
     __shared__ double smem[XCHOL_SMEM];
     for (int e = threadIdx.x; e < KP * KP; e += 256) {
         double v = xa_all[e];
-        for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * KP * KP + e];
+        for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * d.xstride + e];
         xprec_store(d, smem, e, v);
     }
     __syncthreads();
@@ -890,6 +890,11 @@ __device__ __forceinline__ double delta_chain(const Dims &d, int l, double T, do
     return dnew;
 }
 
+// column sums of global shard mg in the gathered buffer (rank blocks padded by d.sgap)
+__device__ __forceinline__ size_t sall_off(const Dims &d, int mg) {
+    return (size_t)mg * KP + (d.sgap ? (size_t)(mg / d.G) * d.sgap : 0);
+}
+
 // one wave = one global shard m, lane l
 __device__ __forceinline__ void delta_shard(const Dims &d, const double *__restrict__ sall,
                                             const double *__restrict__ delta_in, const double *__restrict__ tau_in,
@@ -902,7 +907,7 @@ __device__ __forceinline__ void delta_shard(const Dims &d, const double *__restr
         if (d.K >= 2) {
             // shard 1 (index 0) with its own pre-update delta_h
             const double d0 = act ? delta_in[lk] : 1.0;
-            const double T0 = wave_suffix_sum(act ? tau_in[lk] * sall[lk] : 0.0, l);
+            const double T0 = wave_suffix_sum(act ? tau_in[lk] * sall[sall_off(d, 0) + lk] : 0.0, l);
             const double G0 = act ? delta_G(d, dr, iter, 0, l) : 1.0;
             const double id0 = 1.0 / d0;
             const double d0new = delta_chain(d, l, T0, G0, id0, id0);
@@ -910,7 +915,7 @@ __device__ __forceinline__ void delta_shard(const Dims &d, const double *__restr
             if (m != 0) {
                 const size_t o = (size_t)m * KP + lk;
                 const double dold = act ? delta_in[o] : 1.0;
-                const double Tm = wave_suffix_sum(act ? tau_in[o] * sall[o] : 0.0, l);
+                const double Tm = wave_suffix_sum(act ? tau_in[o] * sall[sall_off(d, m) + lk] : 0.0, l);
                 const double Gm = act ? delta_G(d, dr, iter, m, l) : 1.0;
                 const double idold = 1.0 / dold;
                 const double idref = (l == 0) ? idold : 1.0 / d0new;   // delta(1,:,m) | delta(h) (Q4)
@@ -927,7 +932,7 @@ __device__ __forceinline__ void delta_shard(const Dims &d, const double *__restr
                 for (int mm = 0; mm <= m; ++mm) {
                     const double dold = delta_in[(size_t)mm * KP];
                     const double tused = prefix * dold;
-                    const double bd = d.bd1 + (0.5 * (1.0 / dold)) * (tused * sall[(size_t)mm * KP]);
+                    const double bd = d.bd1 + (0.5 * (1.0 / dold)) * (tused * sall[sall_off(d, mm)]);
                     dnew = (1.0 / bd) * delta_G(d, dr, iter, mm, 0);
                     prefix = prefix * dnew;
                 }
@@ -1040,10 +1045,11 @@ __global__ __launch_bounds__(256) void k_deltaops(Dims d, const double *__restri
                                                   double *__restrict__ delta_out, double *__restrict__ tau_out,
                                                   DrawsDev dr, int64_t iter, const double *__restrict__ A,
                                                   double *__restrict__ ZM, double *__restrict__ xpart,
-                                                  unsigned *__restrict__ ticket, double *__restrict__ xa) {
+                                                  unsigned *__restrict__ ticket, double *__restrict__ xa,
+                                                  int ops) {
     __shared__ double smem[PREP_SMEM];
     const int nxs = d.G < XSUM_BLOCKS ? d.G : XSUM_BLOCKS;
-    int b = blockIdx.x;
+    int b = blockIdx.x + (ops ? 0 : nxs + d.G);   // !ops: the delta blocks alone
     if (b < nxs) {
         xsum_tree(d, A, xpart, ticket, xa, b, nxs, smem);
         return;
@@ -1071,7 +1077,7 @@ __global__ __launch_bounds__(256) void k_zxchol(Dims d, const double *__restrict
     }
     for (int e = threadIdx.x; e < KP * KP; e += 256) {   // the ranks' shard sums, in rank order
         double v = xa_all[e];
-        for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * KP * KP + e];
+        for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * d.xstride + e];
         xprec_store(d, smem, e, v);
     }
     __syncthreads();
@@ -1407,11 +1413,13 @@ void launch_colgram(const Dims &d, const Bufs &b, bool colsum, hipStream_t s) {
 }
 void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool delta,
                      const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
-                     hipStream_t s) {
+                     hipStream_t s, bool ops) {
     if (d.kp != KP) return;
     const int nxs = d.G < XSUM_BLOCKS ? d.G : XSUM_BLOCKS;
-    hipLaunchKernelGGL(k_deltaops, dim3(nxs + d.G + (delta ? (d.g + 3) / 4 : 0)), dim3(256), 0, s, d, b.sall,
-                       delta_in, tau_in, delta_out, tau_out, dr, iter, b.A, b.ZM, b.xpart, b.ticket, b.xa);
+    const int nb = (ops ? nxs + d.G : 0) + (delta ? (d.g + 3) / 4 : 0);
+    if (nb == 0) return;
+    hipLaunchKernelGGL(k_deltaops, dim3(nb), dim3(256), 0, s, d, b.sall, delta_in, tau_in, delta_out, tau_out, dr,
+                       iter, b.A, b.ZM, b.xpart, b.ticket, b.xa, ops ? 1 : 0);
 }
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return;

@@ -1,11 +1,13 @@
 """Per-rank restatement of libdcfm's multi-GPU exchange protocol (TEST INFRASTRUCTURE).
 
 libdcfm (csrc/dcfm.hip, dcfm_run) splits the g shards of one chain over
-nranks GPUs and exchanges, per iteration:
-  1. all-gather of [sum_{local m} (W_m - sqrt(1-rho) Z_m A_m') ; sum_{local m} A_m]
-     (n x K and K x K), summed in rank order -> replicated X draw  (dc:112-128)
-  2. all-gather of the per-shard column sums of psi o Lambda^2 (K per shard)
-     -> replicated delta/tau chain over ALL shards (quirks Q4/Q5)  (dc:155-165)
+nranks GPUs and exchanges, per iteration (the fused K <= 32 chain):
+  1. all-gather of sum_{local m} (W_m - sqrt(1-rho) Z_m A_m') (n x K), summed in rank
+     order -> replicated X draw  (dc:112-128)
+  2. ONE all-gather of [per-shard column sums of psi o Lambda^2 (K per shard) ;
+     sum_{local m} A_m of the NEXT iteration (from the new Lambda, omega; K x K)]
+     -> replicated delta/tau chain over ALL shards (quirks Q4/Q5, dc:155-165) and the
+     next iteration's Xprec (dc:117); before the first iteration the A sums alone
 and per assembly flush an all-gather of the saved Lambda rows and omega, after
 which each rank accumulates its round-robin share of lower-triangle tiles;
 dcfm_get_sigma sums the per-rank accumulators (all-reduce) and mirrors.
@@ -62,11 +64,15 @@ class RankChain:
         st["Z"] = np.moveaxis(np.swapaxes(Zk, 1, 2), 0, 2)
         Zg = np.swapaxes(Zk, 1, 2)
         Sr = (W - np.sqrt(1 - rho) * (Zg @ np.swapaxes(A, 1, 2))).sum(axis=0)
-        parts = all_gather_np(np.concatenate([Sr, A.sum(axis=0)]))      # exchange 1
-        tot = parts[0]
+        if not hasattr(self, "Asums"):                                   # before the first iteration
+            self.Asums = all_gather_np(A.sum(axis=0))
+        parts = all_gather_np(Sr)                                        # exchange 1
+        S = parts[0]
         for p_ in parts[1:]:
-            tot = tot + p_
-        S, Asum = tot[:self.n], tot[self.n:]
+            S = S + p_
+        Asum = self.Asums[0]
+        for p_ in self.Asums[1:]:
+            Asum = Asum + p_
         Rx = chol_upper(self.g * np.eye(K) + rho * Asum)
         vx = np.linalg.solve(Rx, (np.sqrt(rho) * S).T)
         st["X"] = np.linalg.solve(Rx.T, vx + d.NX).T
@@ -87,11 +93,15 @@ class RankChain:
         tau_loc = st["tauh"][:, 0, loc][None]
         st["psi"] = (1.0 / (hyper.df / 2 + 0.5 * (st["Lambda"] ** 2 * tau_loc))) * d.Gpsi[:, :, loc]
         colsum = (st["psi"] * st["Lambda"] ** 2).sum(axis=0)            # K x G
-        colsum_all = np.concatenate(all_gather_np(colsum.T), axis=0).T   # exchange 2 -> K x g
-        self._delta_tau(colsum_all, d.Gdelta)
         SS = self.yy - 2.0 * np.einsum("mjk,mjk->mj", lam, C) + np.einsum("mjk,mkl,mjl->mj", lam, E, lam)
         st["ps"][:, 0, :] = ((1.0 / (hyper.bs + 0.5 * SS)) * d.Gps[:, loc].T).T
         st["omega"] = 1.0 / st["ps"][:, 0, :]
+        Ln = np.ascontiguousarray(np.moveaxis(st["Lambda"], 2, 0))
+        An = np.swapaxes(Ln * st["omega"].T[:, :, None], 1, 2) @ Ln     # next iteration's A_m
+        msgs = all_gather_np(np.concatenate([colsum.T.reshape(-1), An.sum(axis=0).reshape(-1)]))   # exchange 2
+        colsum_all = np.concatenate([m_[:G * K].reshape(G, K) for m_ in msgs], axis=0).T   # K x g
+        self.Asums = [m_[G * K:].reshape(K, K) for m_ in msgs]
+        self._delta_tau(colsum_all, d.Gdelta)
         st["Plam"] = st["psi"] * st["tauh"][:, 0, loc][None]
 
     def _delta_tau(self, colsum_all, Gdelta):
