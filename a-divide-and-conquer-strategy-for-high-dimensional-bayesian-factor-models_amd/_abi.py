@@ -37,7 +37,7 @@ EXPORTS = (
     "dcfm_get_sigma_cols",
     "dcfm_saved_samples", "dcfm_sigma_error", "dcfm_set_profiling", "dcfm_set_profiling_mask", "dcfm_get_kernel_stats",
     "dcfm_kernel_name",
-    "dcfm_rng_fill",
+    "dcfm_rng_fill", "dcfm_set_data_raw", "dcfm_get_data", "dcfm_count_nonzero_columns",
 )
 
 
@@ -110,6 +110,10 @@ def load_library(path: Path | None = None):
         "dcfm_kernel_name": (C.c_char_p, [C.c_int]),
         "dcfm_rng_fill": (C.c_int, [C.c_int, C.c_uint64, C.c_int, C.c_double, C.c_int32, C.c_int32,
                                     C.c_int64, C.c_int64, _DP]),
+        "dcfm_set_data_raw": (C.c_int, [vp, _DP, C.c_int64, C.POINTER(C.c_int64), _DP, _DP]),
+        "dcfm_get_data": (C.c_int, [vp, _DP]),
+        "dcfm_count_nonzero_columns": (C.c_int, [C.c_int, _DP, C.c_int32, C.c_int64, C.POINTER(C.c_int32),
+                                                 _DP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -549,6 +549,111 @@ int dcfm_set_data(dcfm_handle *h, const double *Yd) {
     return DCFM_OK;
 }
 
+// device scratch freed on every return path of the ingest entry points
+struct DevScratch {
+    std::vector<void *> p;
+    ~DevScratch() { for (void *q : p) (void)hipFree(q); }
+    hipError_t alloc(void **q, size_t bytes) {
+        hipError_t e = hipMalloc(q, std::max<size_t>(bytes, 1));
+        if (e == hipSuccess) p.push_back(*q);
+        return e;
+    }
+};
+
+int dcfm_set_data_raw(dcfm_handle *h, const double *Y, int64_t p_in, const int64_t *cols, double *sd_out,
+                      double *dev_ms) {
+    if (!h || !Y || !cols) return fail(h, DCFM_ERR_INVALID, "null argument");
+    const Dims &d = h->d;
+    if (d.n < 2) return fail(h, DCFM_ERR_INVALID, "set_data_raw: var (dc:57) needs n >= 2");
+    const int64_t ncols = (int64_t)d.P * d.G;
+    for (int64_t c = 0; c < ncols; ++c)
+        if (cols[c] < 0 || cols[c] >= p_in)
+            return fail(h, DCFM_ERR_INVALID, "set_data_raw: cols[%lld] = %lld outside [0, %lld)", (long long)c,
+                        (long long)cols[c], (long long)p_in);
+    HIPC(h, hipSetDevice(h->cfg.device));
+    DevScratch sc;
+    void *qY = nullptr, *qc = nullptr, *qsd = nullptr, *qbad = nullptr;
+    const size_t ybytes = (size_t)d.n * (size_t)p_in * sizeof(double);
+    if (sc.alloc(&qY, ybytes) != hipSuccess || sc.alloc(&qc, ncols * sizeof(int64_t)) != hipSuccess ||
+        sc.alloc(&qsd, ncols * sizeof(double)) != hipSuccess || sc.alloc(&qbad, sizeof(int)) != hipSuccess)
+        return fail(h, DCFM_ERR_ALLOC, "set_data_raw: device scratch (%zu bytes of Y) failed", ybytes);
+    hipStream_t s = h->stream;
+    HIPC(h, hipMemcpyAsync(qY, Y, ybytes, hipMemcpyHostToDevice, s));
+    HIPC(h, hipMemcpyAsync(qc, cols, ncols * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPC(h, hipMemsetAsync(qbad, 0, sizeof(int), s));
+    hipEvent_t ea = get_event(h), eb = get_event(h);
+    if (!ea || !eb) return fail(h, DCFM_ERR_HIP, "set_data_raw: hipEventCreate failed");
+    HIPC(h, hipEventRecord(ea, s));
+    launch_stdize(d, static_cast<const double *>(qY), static_cast<const long long *>(qc), h->b.Y, h->b.yy,
+                  static_cast<double *>(qsd), static_cast<int *>(qbad), s);
+    HIPC(h, hipGetLastError());
+    HIPC(h, hipEventRecord(eb, s));
+    int bad = 0;
+    HIPC(h, hipMemcpyAsync(&bad, qbad, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPC(h, hipStreamSynchronize(s));
+    if (dev_ms) {
+        float ms = 0.f;
+        HIPC(h, hipEventElapsedTime(&ms, ea, eb));
+        *dev_ms = ms;
+    }
+    h->evpool.push_back(ea);
+    h->evpool.push_back(eb);
+    if (bad) {
+        h->have_data = false;
+        return fail(h, DCFM_ERR_INVALID, "a constant non-zero column has zero variance (dc:59 divides by zero, Q13)");
+    }
+    if (sd_out) HIPC(h, hipMemcpy(sd_out, qsd, ncols * sizeof(double), hipMemcpyDeviceToHost));
+    h->have_data = true;
+    return DCFM_OK;
+}
+
+int dcfm_get_data(dcfm_handle *h, double *Yd_local) {
+    if (!h || !Yd_local) return fail(h, DCFM_ERR_INVALID, "null argument");
+    if (!h->have_data) return fail(h, DCFM_ERR_INVALID, "get_data: no data set");
+    const Dims &d = h->d;
+    HIPC(h, hipSetDevice(h->cfg.device));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    std::vector<double> buf((size_t)d.NP * d.PP);
+    for (int m = 0; m < d.G; ++m) {
+        HIPC(h, hipMemcpy(buf.data(), h->b.Y + (size_t)m * d.NP * d.PP, buf.size() * sizeof(double),
+                          hipMemcpyDeviceToHost));
+        double *dst = Yd_local + (size_t)m * d.n * d.P;
+        for (int j = 0; j < d.P; ++j)
+            for (int i = 0; i < d.n; ++i) dst[(size_t)j * d.n + i] = buf[(size_t)i * d.PP + j];
+    }
+    return DCFM_OK;
+}
+
+int dcfm_count_nonzero_columns(int device, const double *Y, int32_t n, int64_t p, int32_t *nnz_out,
+                               double *dev_ms) {
+    if (!Y || !nnz_out || n < 0 || p < 0) return fail(nullptr, DCFM_ERR_INVALID, "count_nonzero_columns: bad argument");
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return fail(nullptr, DCFM_ERR_HIP, "hipSetDevice: %s", hipGetErrorString(e));
+    DevScratch sc;
+    void *qY = nullptr, *qn = nullptr;
+    const size_t ybytes = (size_t)n * (size_t)p * sizeof(double);
+    if (sc.alloc(&qY, ybytes) != hipSuccess || sc.alloc(&qn, (size_t)p * sizeof(int32_t)) != hipSuccess)
+        return fail(nullptr, DCFM_ERR_ALLOC, "count_nonzero_columns: device scratch (%zu bytes) failed", ybytes);
+    hipEvent_t ea = nullptr, eb = nullptr;
+    float ms = 0.f;
+    e = hipMemcpy(qY, Y, ybytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipEventCreate(&ea);
+    if (e == hipSuccess) e = hipEventCreate(&eb);
+    if (e == hipSuccess) e = hipEventRecord(ea, nullptr);
+    if (e == hipSuccess) {
+        launch_nnz_cols(static_cast<const double *>(qY), n, p, static_cast<int *>(qn), nullptr);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipEventRecord(eb, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(nnz_out, qn, (size_t)p * sizeof(int32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, ea, eb);
+    if (ea) (void)hipEventDestroy(ea);
+    if (eb) (void)hipEventDestroy(eb);
+    if (e != hipSuccess) return fail(nullptr, DCFM_ERR_HIP, "count_nonzero_columns: %s", hipGetErrorString(e));
+    if (dev_ms) *dev_ms = ms;
+    return DCFM_OK;
+}
+
 // P x K x G col-major (j,k,m) at j + P*k + P*K*m  <->  dev [m][j][k] (PP x KP)
 static void pk_to_dev(const Dims &d, const double *src, std::vector<double> &dst) {
     const int KP = d.kp;

@@ -101,6 +101,10 @@ int sigma_err_splits(int p);
 void launch_sigma_err(const double *S, int p, const double *U, int R, const double *sdiag, const double *v,
                       int rank, int nranks, bool first, double *y, double *fro, double *tru, double *out,
                       hipStream_t s);
+// ingest.hip: dc:31-34 column nnz counts; dc:50-59 partition + standardise into Y / yy
+void launch_nnz_cols(const double *Y, int n, long long p, int *nnz, hipStream_t s);
+void launch_stdize(const Dims &d, const double *Yraw, const long long *cols, double *Y, double *yy, double *sd,
+                   int *bad, hipStream_t s);
 void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s);
 // dst[i] = sum_k src[k * count + i] in slice order (loopback all-reduce)
 void launch_sum_slices(const double *src, int ns, size_t count, double *dst, hipStream_t s);

@@ -23,7 +23,7 @@ import time
 
 import numpy as np
 
-from .sampler import Hyper, Sampler
+from .sampler import Hyper, Sampler, count_nonzero_columns
 
 
 def preprocess(Y, g, k):
@@ -38,6 +38,28 @@ def preprocess(Y, g, k):
     if g < 1 or p % g or k % g:
         raise ValueError(f"P = p/g = {p}/{g} and K = k/g = {k}/{g} must be integers (dc:41)")
     return Y, n, p, p // g, k // g, keep
+
+
+def preprocess_device(Y, g, k, device=0):
+    """dc:29-41 with the column scan on the GPU (dcfm_count_nonzero_columns): returns
+    (n, p, P, K, keep) — the kept width and index; the data itself is not copied, since
+    dcfm_set_data_raw gathers the kept columns on the device through ``shard_columns``."""
+    Y = np.asarray(Y, dtype=np.float64)
+    if Y.ndim != 2:
+        raise ValueError("Y must be n x p (rows are observations, dc:30)")
+    n = Y.shape[0]
+    keep = np.flatnonzero(count_nonzero_columns(Y, device=device) != 0)    # dc:31-38
+    p = keep.size                                                          # dc:39
+    if g < 1 or p % g or k % g:
+        raise ValueError(f"P = p/g = {p}/{g} and K = k/g = {k}/{g} must be integers (dc:41)")
+    return n, p, p // g, k // g, keep
+
+
+def shard_columns(keep, varind, P, s0, gl):
+    """Input column of every (local shard, position) of shards [s0, s0+gl): dc:50-54's
+    Y(:, varind((m-1)*P+1 : m*P)) after the zero-column removal (dc:36), 0-based, shard-major
+    — the ``cols`` argument of dcfm_set_data_raw."""
+    return np.asarray(keep, dtype=np.int64)[np.asarray(varind)[s0 * P:(s0 + gl) * P]]
 
 
 def partition_standardize(Y, g, varind):
@@ -104,18 +126,27 @@ def local_state(state: dict, s0: int, gl: int) -> dict:
 
 def divideconquer(Y, g, k, BURNIN, MCMC, thin, rho, *, seed=0, hyper: Hyper = Hyper(),
                   init_draws=None, iter_draws=None, nranks=1, rank=0, device=0, comm_uid=None,
-                  asm_batch=0, return_info=False):
+                  asm_batch=0, return_info=False, device_ingest=True):
     """Sigmaout = divideconquer(Y,g,k,BURNIN,MCMC,thin,rho)   (divideconquer.m:1).
+
+    ``device_ingest`` (default): the zero-column scan and the partition/standardisation
+    (dc:31-59) run on the GPU (dcfm_count_nonzero_columns, dcfm_set_data_raw); False
+    keeps them on the host (NumPy) and uploads Yd.
 
     Multi-GPU: call on every rank with the same arguments plus nranks/rank/device
     and the 128-byte RCCL id (``Sampler.unique_id()`` on rank 0, broadcast by
     the caller).  Every rank returns the full Sigmaout.
     """
     t0 = time.perf_counter()                                     # dc:29 tic
-    Yk, n, p, P, K, keep = preprocess(Y, g, k)
+    if device_ingest:
+        Y = np.asarray(Y, dtype=np.float64)
+        n, p, P, K, keep = preprocess_device(Y, g, k, device=device)
+    else:
+        Yk, n, p, P, K, keep = preprocess(Y, g, k)
     N = BURNIN + MCMC                                            # dc:45
     init = init_draws if init_draws is not None else _HostInitDraws(seed, n, p, g, K, hyper)
-    Yd = partition_standardize(Yk, g, np.asarray(init.varind))
+    if not device_ingest:
+        Yd = partition_standardize(Yk, g, np.asarray(init.varind))
     state = initial_state(n, P, K, g, rho, hyper, init)
     gl = g // nranks
     s0 = rank * gl
@@ -126,7 +157,10 @@ def divideconquer(Y, g, k, BURNIN, MCMC, thin, rho, *, seed=0, hyper: Hyper = Hy
             if comm_uid is None:
                 raise ValueError("nranks > 1 needs comm_uid (Sampler.unique_id() from rank 0)")
             smp.comm_init(comm_uid)
-        smp.set_data(Yd[:, :, s0:s0 + gl])
+        if device_ingest:                                        # dc:48-59 on the device
+            smp.set_data_raw(Y, shard_columns(keep, init.varind, P, s0, gl))
+        else:
+            smp.set_data(Yd[:, :, s0:s0 + gl])
         smp.set_state(local_state(state, s0, gl))
         if iter_draws is not None:
             smp.set_draws(iter_draws, 1, N)

@@ -105,6 +105,29 @@ class Sampler:
             raise ValueError(f"Yd_local must be n x P x g_local = {(self.n, self.P, self.g_local)}, got {Y.shape}")
         self._check(self.lib.dcfm_set_data(self.h, _ptr(Y)))
 
+    def set_data_raw(self, Y, cols):
+        """On-device ingest (dc:48-59, dcfm_set_data_raw): Y is the raw n x p_in data,
+        ``cols`` the 0-based input column of every (local shard, position) pair, length
+        P * g_local (``shard_columns``).  Returns (sd, kernel_ms): the P x g_local sample
+        standard deviations and the standardise kernel's device time."""
+        Y = _f64F(Y)
+        if Y.ndim != 2 or Y.shape[0] != self.n:
+            raise ValueError(f"Y must be n x p_in with n = {self.n}, got {Y.shape}")
+        c = np.ascontiguousarray(np.asarray(cols, dtype=np.int64).reshape(-1))
+        if c.size != self.P * self.g_local:
+            raise ValueError(f"cols must hold P * g_local = {self.P * self.g_local} indices, got {c.size}")
+        sd = np.zeros((self.P, self.g_local), dtype=np.float64, order="F")
+        ms = C.c_double(0.0)
+        self._check(self.lib.dcfm_set_data_raw(self.h, _ptr(Y), Y.shape[1],
+                                               c.ctypes.data_as(C.POINTER(C.c_int64)), _ptr(sd), C.byref(ms)))
+        return sd, ms.value
+
+    def get_data(self) -> np.ndarray:
+        """Yd as the sweep holds it (n x P x g_local)."""
+        out = np.zeros((self.n, self.P, self.g_local), dtype=np.float64, order="F")
+        self._check(self.lib.dcfm_get_data(self.h, _ptr(out)))
+        return out
+
     def _shapes(self):
         n, P, K, gl, g = self.n, self.P, self.K, self.g_local, self.g
         return {"Lambda": (P, K, gl), "ps": (P, 1, gl), "omega": (P, gl), "psi": (P, K, gl),
@@ -198,6 +221,20 @@ class Sampler:
         cnt = (C.c_int64 * _abi.K_COUNT)()
         self._check(self.lib.dcfm_get_kernel_stats(self.h, ms, cnt))
         return {name: (ms[i], cnt[i]) for name, i in _abi.KERNEL_IDS.items()}
+
+
+def count_nonzero_columns(Y, device=0, return_ms=False):
+    """dc:31-34 on the device: nnz of every column of the n x p matrix Y (int32)."""
+    lib = _abi.load_library()
+    Y = _f64F(Y)
+    if Y.ndim != 2:
+        raise ValueError("Y must be n x p")
+    out = np.zeros(Y.shape[1], dtype=np.int32)
+    ms = C.c_double(0.0)
+    rc = lib.dcfm_count_nonzero_columns(int(device), _ptr(Y), Y.shape[0], Y.shape[1],
+                                        out.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(ms))
+    _abi.check(lib, None, rc)
+    return (out, ms.value) if return_ms else out
 
 
 def rng_fill(kind: str, count: int, *, seed=0, shape=1.0, site=15, shard=0, iteration=0, device=0):

@@ -118,6 +118,22 @@ int  dcfm_comm_init_loopback(dcfm_handle *const *handles, int32_t n);
 /* ---- inputs -------------------------------------------------------------- */
 /* Yd(:,:,shard0+1 : shard0+g_local) after dc:48-59, n x P x g_local.        */
 int  dcfm_set_data(dcfm_handle *h, const double *Yd_local);
+/* On-device ingest (replaces the host's dc:48-59): Y is the raw
+ * n x p_in matrix (column-major, after the caller's zero-column removal, dc:31-39, or
+ * before it — cols index Y's own columns); cols[m*P + j] (0-based) is the input column
+ * of local shard m, position j, i.e. keep(varind((shard0+m)*P + j)) - 1 in MATLAB terms.
+ * Y goes to HBM once; the kernel gathers, centres, scales by 1./sqrt(var) (n - 1) and
+ * lays Yd out for the sweep.  sd_out (nullable): P x g_local sample standard deviations
+ * (for unpermute_sigma); dev_ms (nullable): the kernel's device time.  A constant
+ * column (zero variance, Q13) is DCFM_ERR_INVALID; needs n >= 2. */
+int  dcfm_set_data_raw(dcfm_handle *h, const double *Y, int64_t p_in, const int64_t *cols,
+                       double *sd_out, double *dev_ms);
+/* Yd as the sweep holds it, n x P x g_local column-major (the layout of dcfm_set_data). */
+int  dcfm_get_data(dcfm_handle *h, double *Yd_local);
+/* dc:31-34 on the device: nnz_out[j] = nnz(Y(:,j)) for the n x p column-major Y (NaN
+ * counts as non-zero).  No handle: the kept width p (hence P = p/g) is not known yet. */
+int  dcfm_count_nonzero_columns(int device, const double *Y, int32_t n, int64_t p, int32_t *nnz_out,
+                                double *dev_ms);
 int  dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s);
 /* Draws for iterations first_iter .. first_iter+n_iter-1 (1-based, as iter). */
 int  dcfm_set_draws(dcfm_handle *h, const dcfm_draws_view *d, int64_t first_iter, int64_t n_iter);
