@@ -11,11 +11,12 @@ Import through the repo-root helper (the directory name has hyphens)::
 """
 from ._abi import DcfmError, load_library, EXPORTS, LIB_PATH
 from .sampler import Hyper, Sampler, rng_fill, count_nonzero_columns, STATE_FIELDS
+from . import diagnostics
 from .driver import divideconquer, preprocess, preprocess_device, shard_columns, partition_standardize, initial_state, local_state, truth_factors, output_columns, unpermute_sigma
 
 __all__ = [
     "DcfmError", "load_library", "EXPORTS", "LIB_PATH", "Hyper", "Sampler", "rng_fill",
     "STATE_FIELDS", "divideconquer", "preprocess", "partition_standardize", "initial_state",
     "local_state", "truth_factors", "output_columns", "unpermute_sigma", "count_nonzero_columns",
-    "preprocess_device", "shard_columns",
+    "preprocess_device", "shard_columns", "diagnostics",
 ]

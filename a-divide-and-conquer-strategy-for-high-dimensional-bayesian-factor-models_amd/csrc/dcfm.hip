@@ -92,6 +92,9 @@ struct dcfm_handle {
     bool used_pending[2] = {false, false};   // e_used[slot] recorded after the slot's last consumer
     int DB = 1;                              // iterations per draws batch
     size_t draw_iter_sz[6] = {};             // per-iteration doubles of NZ, NX, NL, Gpsi, Gdelta, Gps
+    // per-iteration chain trace (dcfm_set_trace): rows [trace_cap][4], partials [G][4]
+    double *trace = nullptr, *trace_part = nullptr;
+    int64_t trace_cap = 0, trace_n = 0;
     bool prof = false;
     uint32_t prof_mask = 0;       // kernel ids (bit DCFM_K_*) timed with events
     std::vector<ProfRec> recs;
@@ -470,6 +473,8 @@ void dcfm_destroy(dcfm_handle *h) {
     if (h->comm) ncclCommDestroy(h->comm);
     for (void *q : h->allocs) (void)hipFree(q);
     if (h->draws_mem) (void)hipFree(h->draws_mem);
+    if (h->trace) (void)hipFree(h->trace);
+    if (h->trace_part) (void)hipFree(h->trace_part);
     if (h->sasm && h->sasm != h->stream) (void)hipStreamDestroy(h->sasm);
     if (h->side && h->side != h->stream) (void)hipStreamDestroy(h->side);
     if (h->sdraw && h->sdraw != h->stream) (void)hipStreamDestroy(h->sdraw);
@@ -1033,6 +1038,10 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             h->used_pending[slot] = true;
         }
         h->cur ^= 1;
+        if (h->trace_n < h->trace_cap) {                                  // dcfm_set_trace
+            launch_trace(d, b, b.tau + h->cur * nkg, h->trace_part, h->trace + h->trace_n * 4, s);
+            h->trace_n += 1;
+        }
         HIPC(h, hipGetLastError());
         if (it % h->cfg.thin == 0 && it > h->cfg.burnin) {                // dc:180
             if (h->batch == 0 && h->asm_pending[h->lb]) {                 // buffer still being assembled
@@ -1052,6 +1061,32 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     int rc = flush_batch(h);
     if (rc) return rc;
     if (h->prof) collect_prof(h);
+    return DCFM_OK;
+}
+
+int dcfm_set_trace(dcfm_handle *h, int64_t capacity) {
+    if (!h || capacity < 0) return fail(h, DCFM_ERR_INVALID, "set_trace: bad argument");
+    HIPC(h, hipSetDevice(h->cfg.device));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    if (h->trace) (void)hipFree(h->trace);
+    if (h->trace_part) (void)hipFree(h->trace_part);
+    h->trace = h->trace_part = nullptr;
+    h->trace_cap = h->trace_n = 0;
+    if (capacity == 0) return DCFM_OK;
+    if (hipMalloc(&h->trace, (size_t)capacity * 4 * sizeof(double)) != hipSuccess ||
+        hipMalloc(&h->trace_part, (size_t)h->d.G * 4 * sizeof(double)) != hipSuccess)
+        return fail(h, DCFM_ERR_ALLOC, "set_trace: %lld rows", (long long)capacity);
+    h->trace_cap = capacity;
+    return DCFM_OK;
+}
+
+int dcfm_get_trace(dcfm_handle *h, double *out, int64_t *count) {
+    if (!h || !count) return fail(h, DCFM_ERR_INVALID, "get_trace: null argument");
+    HIPC(h, hipSetDevice(h->cfg.device));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    *count = h->trace_n;
+    if (out && h->trace_n)
+        HIPC(h, hipMemcpy(out, h->trace, (size_t)h->trace_n * 4 * sizeof(double), hipMemcpyDeviceToHost));
     return DCFM_OK;
 }
 

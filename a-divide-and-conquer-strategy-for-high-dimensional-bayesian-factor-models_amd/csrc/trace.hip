@@ -1,0 +1,60 @@
+// Per-iteration chain trace for convergence diagnostics across chains.
+//
+// The reference keeps no trace (it only accumulates Sigmaout, dc:180-196); to compare the
+// c4 configuration's parallel chains (split-R-hat, effective sample size) each chain needs
+// a few scalar summaries of its state per iteration.  After an iteration has finished
+// (dc:137-177 done), k_trace_part reduces this rank's local shards:
+//   q0 = sum_m sum_{j,h} Lambda_jh^2          ||Lambda||_F^2  (= tr(Lambda Lambda'))
+//   q1 = sum_m sum_j omega_j                  tr(Omega)  -> q0 + q1 = tr(Sigma draw, dc:185)
+//   q2 = sum_m sum_j log ps_j                 residual precisions (dc:170)
+//   q3 = sum_m sum_h log tau_h^m              the shrinkage process (dc:163)
+// one block per local shard (fixed in-order sums: deterministic), and k_trace_sum adds the
+// G partials in shard order into the trace row.  Ranks that split one chain's shards add
+// their rows (the host all-reduces).  Cost when enabled: one read of Lambda
+// (G x PP x KW doubles; 5 MB at c3), off by default.
+#include "dcfm_internal.h"
+
+namespace dcfm {
+
+__global__ __launch_bounds__(256) void k_trace_part(const double *__restrict__ Lam, const double *__restrict__ omega,
+                                                    const double *__restrict__ ps, const double *__restrict__ tau,
+                                                    int P, int PP, int KW, int K, int shard0,
+                                                    double *__restrict__ part) {
+    __shared__ double red[4][256];
+    const int m = blockIdx.x, t = threadIdx.x;
+    const double *L = Lam + (size_t)m * PP * KW;
+    double q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
+    const int nl = P * KW;                       // rows j < P (padding columns k >= K hold zeros)
+    for (int e = t; e < nl; e += 256) { const double v = L[e]; q0 += v * v; }
+    for (int j = t; j < P; j += 256) {
+        q1 += omega[(size_t)m * PP + j];
+        q2 += log(ps[(size_t)m * PP + j]);
+    }
+    for (int hh = t; hh < K; hh += 256) q3 += log(tau[(size_t)(shard0 + m) * KW + hh]);
+    red[0][t] = q0; red[1][t] = q1; red[2][t] = q2; red[3][t] = q3;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (t < s) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[q][t] += red[q][t + s];
+        }
+        __syncthreads();
+    }
+    if (t < 4) part[(size_t)m * 4 + t] = red[t][0];
+}
+
+__global__ __launch_bounds__(64) void k_trace_sum(const double *__restrict__ part, int G, double *__restrict__ row) {
+    const int q = threadIdx.x;
+    if (q >= 4) return;
+    double s = 0.0;
+    for (int m = 0; m < G; ++m) s += part[(size_t)m * 4 + q];
+    row[q] = s;
+}
+
+void launch_trace(const Dims &d, const Bufs &b, const double *tau_cur, double *part, double *row, hipStream_t s) {
+    hipLaunchKernelGGL(k_trace_part, dim3(d.G), dim3(256), 0, s, b.Lam, b.omega, b.ps, tau_cur, d.P, d.PP, d.kp,
+                       d.K, d.shard0, part);
+    hipLaunchKernelGGL(k_trace_sum, dim3(1), dim3(64), 0, s, part, d.G, row);
+}
+
+}  // namespace dcfm

@@ -205,6 +205,22 @@ class Sampler:
     def saved_samples(self) -> int:
         return int(self.lib.dcfm_saved_samples(self.h))
 
+    # -- chain trace (diagnostics across chains) -----------------------------------
+    TRACE_FIELDS = ("lambda_fro2", "tr_omega", "sum_log_ps", "sum_log_tau")
+
+    def set_trace(self, capacity: int):
+        """Record one row of TRACE_FIELDS per iteration of later runs (0 = off)."""
+        self._check(self.lib.dcfm_set_trace(self.h, int(capacity)))
+        self._trace_cap = int(capacity)
+
+    def get_trace(self) -> np.ndarray:
+        """(iterations recorded) x 4 array of this rank's local-shard sums."""
+        cnt = C.c_int64(0)
+        cap = getattr(self, "_trace_cap", 0)
+        out = np.zeros((max(cap, 1), 4), dtype=np.float64)
+        self._check(self.lib.dcfm_get_trace(self.h, _ptr(out), C.byref(cnt)))
+        return out[:cnt.value].copy()
+
     # -- measurement -----------------------------------------------------------------
     def set_profiling(self, on: bool):
         self._check(self.lib.dcfm_set_profiling(self.h, 1 if on else 0))

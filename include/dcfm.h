@@ -167,6 +167,16 @@ int64_t dcfm_saved_samples(const dcfm_handle *h);
 int  dcfm_sigma_error(dcfm_handle *h, const double *U, int32_t r, const double *s, int32_t iters,
                       uint64_t seed, double out[3]);
 
+/* ---- chain trace (convergence diagnostics across chains) ----
+ * dcfm_set_trace(h, cap): record one row per iteration of later dcfm_run calls, up to cap
+ * rows (0 = off, the default; resets the count).  Row = this rank's local-shard sums
+ *   [ ||Lambda||_F^2,  sum omega (= tr Omega),  sum log ps,  sum_m sum_h log tau_h^m ]
+ * after the iteration (tr of the iteration's Sigma draw = row[0] + row[1], dc:185); ranks
+ * that split one chain add their rows.  dcfm_get_trace: out (nullable) gets count x 4
+ * doubles, row-major. */
+int  dcfm_set_trace(dcfm_handle *h, int64_t capacity);
+int  dcfm_get_trace(dcfm_handle *h, double *out, int64_t *count);
+
 /* ---- measurement --------------------------------------------------------- */
 /* Per-kernel HIP-event timing on the handle's stream (off by default).
  * Kernel ids: DCFM_K_* below.  Times are accumulated device milliseconds. */
