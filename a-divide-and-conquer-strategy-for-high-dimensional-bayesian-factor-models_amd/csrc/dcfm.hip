@@ -92,8 +92,8 @@ struct dcfm_handle {
     bool used_pending[2] = {false, false};   // e_used[slot] recorded after the slot's last consumer
     int DB = 1;                              // iterations per draws batch
     size_t draw_iter_sz[6] = {};             // per-iteration doubles of NZ, NX, NL, Gpsi, Gdelta, Gps
-    // per-iteration chain trace (dcfm_set_trace): rows [trace_cap][4], partials [G][4]
-    double *trace = nullptr, *trace_part = nullptr;
+    // per-iteration chain trace (dcfm_set_trace): per-shard partials [trace_cap][G][4]
+    double *trace = nullptr;
     int64_t trace_cap = 0, trace_n = 0;
     bool prof = false;
     uint32_t prof_mask = 0;       // kernel ids (bit DCFM_K_*) timed with events
@@ -474,7 +474,6 @@ void dcfm_destroy(dcfm_handle *h) {
     for (void *q : h->allocs) (void)hipFree(q);
     if (h->draws_mem) (void)hipFree(h->draws_mem);
     if (h->trace) (void)hipFree(h->trace);
-    if (h->trace_part) (void)hipFree(h->trace_part);
     if (h->sasm && h->sasm != h->stream) (void)hipStreamDestroy(h->sasm);
     if (h->side && h->side != h->stream) (void)hipStreamDestroy(h->side);
     if (h->sdraw && h->sdraw != h->stream) (void)hipStreamDestroy(h->sdraw);
@@ -1039,7 +1038,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         }
         h->cur ^= 1;
         if (h->trace_n < h->trace_cap) {                                  // dcfm_set_trace
-            launch_trace(d, b, b.tau + h->cur * nkg, h->trace_part, h->trace + h->trace_n * 4, s);
+            launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4, s);
             h->trace_n += 1;
         }
         HIPC(h, hipGetLastError());
@@ -1069,12 +1068,10 @@ int dcfm_set_trace(dcfm_handle *h, int64_t capacity) {
     HIPC(h, hipSetDevice(h->cfg.device));
     HIPC(h, hipStreamSynchronize(h->stream));
     if (h->trace) (void)hipFree(h->trace);
-    if (h->trace_part) (void)hipFree(h->trace_part);
-    h->trace = h->trace_part = nullptr;
+    h->trace = nullptr;
     h->trace_cap = h->trace_n = 0;
     if (capacity == 0) return DCFM_OK;
-    if (hipMalloc(&h->trace, (size_t)capacity * 4 * sizeof(double)) != hipSuccess ||
-        hipMalloc(&h->trace_part, (size_t)h->d.G * 4 * sizeof(double)) != hipSuccess)
+    if (hipMalloc(&h->trace, (size_t)capacity * h->d.G * 4 * sizeof(double)) != hipSuccess)
         return fail(h, DCFM_ERR_ALLOC, "set_trace: %lld rows", (long long)capacity);
     h->trace_cap = capacity;
     return DCFM_OK;
@@ -1085,8 +1082,17 @@ int dcfm_get_trace(dcfm_handle *h, double *out, int64_t *count) {
     HIPC(h, hipSetDevice(h->cfg.device));
     HIPC(h, hipStreamSynchronize(h->stream));
     *count = h->trace_n;
-    if (out && h->trace_n)
-        HIPC(h, hipMemcpy(out, h->trace, (size_t)h->trace_n * 4 * sizeof(double), hipMemcpyDeviceToHost));
+    if (out && h->trace_n) {
+        const int G = h->d.G;
+        std::vector<double> part((size_t)h->trace_n * G * 4);
+        HIPC(h, hipMemcpy(part.data(), h->trace, part.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (int64_t t = 0; t < h->trace_n; ++t)
+            for (int q = 0; q < 4; ++q) {
+                double acc = 0.0;
+                for (int m = 0; m < G; ++m) acc += part[((size_t)t * G + m) * 4 + q];   // shard order
+                out[t * 4 + q] = acc;
+            }
+    }
     return DCFM_OK;
 }
 

@@ -106,7 +106,7 @@ void launch_nnz_cols(const double *Y, int n, long long p, int *nnz, hipStream_t 
 void launch_stdize(const Dims &d, const double *Yraw, const long long *cols, double *Y, double *yy, double *sd,
                    int *bad, hipStream_t s);
 // trace.hip: per-iteration chain summaries (||Lambda||_F^2, tr Omega, sum log ps, sum log tau)
-void launch_trace(const Dims &d, const Bufs &b, const double *tau_cur, double *part, double *row, hipStream_t s);
+void launch_trace(const Dims &d, const Bufs &b, const double *tau_cur, double *part, hipStream_t s);
 void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s);
 // dst[i] = sum_k src[k * count + i] in slice order (loopback all-reduce)
 void launch_sum_slices(const double *src, int ns, size_t count, double *dst, hipStream_t s);

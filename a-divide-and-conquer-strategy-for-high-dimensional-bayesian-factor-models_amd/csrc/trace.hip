@@ -8,9 +8,10 @@
 //   q1 = sum_m sum_j omega_j                  tr(Omega)  -> q0 + q1 = tr(Sigma draw, dc:185)
 //   q2 = sum_m sum_j log ps_j                 residual precisions (dc:170)
 //   q3 = sum_m sum_h log tau_h^m              the shrinkage process (dc:163)
-// one block per local shard (fixed in-order sums: deterministic), and k_trace_sum adds the
-// G partials in shard order into the trace row.  Ranks that split one chain's shards add
-// their rows (the host all-reduces).  Cost when enabled: one read of Lambda
+// one block per local shard (fixed in-order sums: deterministic) writing the shard's
+// partials [G][4] of the iteration's trace row; dcfm_get_trace adds them in shard order
+// on the host (a second, one-block summing launch cost 7.6 us per iteration on the
+// chain).  Ranks that split one chain's shards add their rows (the host all-reduces).  Cost when enabled: one read of Lambda
 // (G x PP x KW doubles; 5 MB at c3), off by default.
 #include "dcfm_internal.h"
 
@@ -43,18 +44,9 @@ __global__ __launch_bounds__(256) void k_trace_part(const double *__restrict__ L
     if (t < 4) part[(size_t)m * 4 + t] = red[t][0];
 }
 
-__global__ __launch_bounds__(64) void k_trace_sum(const double *__restrict__ part, int G, double *__restrict__ row) {
-    const int q = threadIdx.x;
-    if (q >= 4) return;
-    double s = 0.0;
-    for (int m = 0; m < G; ++m) s += part[(size_t)m * 4 + q];
-    row[q] = s;
-}
-
-void launch_trace(const Dims &d, const Bufs &b, const double *tau_cur, double *part, double *row, hipStream_t s) {
+void launch_trace(const Dims &d, const Bufs &b, const double *tau_cur, double *part, hipStream_t s) {
     hipLaunchKernelGGL(k_trace_part, dim3(d.G), dim3(256), 0, s, b.Lam, b.omega, b.ps, tau_cur, d.P, d.PP, d.kp,
                        d.K, d.shard0, part);
-    hipLaunchKernelGGL(k_trace_sum, dim3(1), dim3(64), 0, s, part, d.G, row);
 }
 
 }  // namespace dcfm
