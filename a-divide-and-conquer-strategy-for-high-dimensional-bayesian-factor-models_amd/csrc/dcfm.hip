@@ -952,8 +952,8 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         if (fused) {
             { KTimer t(h, DCFM_K_WPASS, s); launch_wpass(d, b, s); }
             { KTimer t(h, DCFM_K_ZDRAW, s); launch_zxchol(d, b, dr, it, s); }
-            { KTimer t(h, DCFM_K_XRED, s);  launch_xred(d, b, s); }
-            if (d.nranks > 1) {
+            if (d.nranks > 1) {   // one rank: k_xdraw sums the shard messages itself
+                { KTimer t(h, DCFM_K_XRED, s); launch_xred(d, b, s); }
                 KTimer t(h, DCFM_K_COMM, s);
                 if (int rc = coll_allgather(h, CH_MAIN, b.xin, b.xall, (size_t)d.NP * KW, s)) return rc;
             }
@@ -980,7 +980,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             }
             HIPC(h, hipStreamWaitEvent(s, h->e_xchol, 0));
         }
-        { KTimer t(h, DCFM_K_XDRAW, s);  launch_xdraw(d, b, dr, it, s); }
+        { KTimer t(h, DCFM_K_XDRAW, s);  launch_xdraw(d, b, dr, it, s, fused && d.nranks == 1); }
         { KTimer t(h, DCFM_K_CPASS, s);  launch_cpass(d, b, s); }
         {
             KTimer t(h, DCFM_K_LAMBDA, s);

@@ -449,30 +449,29 @@ __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict_
 }
 
 // ============================================================================
-// k_xdraw: X' = Tx S' + Ux eps' as fp64 MFMA (operators from k_xchol); S summed over
-// ranks in rank order.  One wave per 16 rows.                                 dc:119-128
+// k_xdraw: X' = Tx S' + Ux eps' as fp64 MFMA (operators from k_xchol).  S is the sum of
+// nsrc [NP][KP] slices: the ranks' gathered sums (xall, rank order), or — one rank, fused
+// chain — the G shard messages Sp themselves, which makes k_xred's launch unnecessary.
+// 16 rows per block: the 4 waves sum slices w, w+4, ... (fixed order), wave 0 adds the
+// partials in wave order and runs the MFMAs.                                  dc:119-128
 // ============================================================================
-__global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__ xall,
-                                              const double *__restrict__ XM,
-                                              double *__restrict__ X, DrawsDev dr, int64_t iter) {
+__global__ __launch_bounds__(256) void k_xdraw(Dims d, const double *__restrict__ src, int nsrc,
+                                               const double *__restrict__ XM,
+                                               double *__restrict__ X, DrawsDev dr, int64_t iter) {
     __shared__ double Ms[2][KP][KP + 1];
-    for (int e = threadIdx.x; e < 2 * KP * KP; e += 64) {
+    __shared__ d2 part[3][4][64];
+    for (int e = threadIdx.x; e < 2 * KP * KP; e += 256) {
         const int mat = e / (KP * KP), rem = e % (KP * KP);
         Ms[mat][rem / KP][rem % KP] = XM[e];
     }
-    __syncthreads();
-    const int lane = threadIdx.x, c = lane & 15, q = lane >> 4;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, q = lane >> 4;
     const int i0 = blockIdx.x * 16, i = i0 + c;
     const bool live = i < d.n;
     const size_t stride = (size_t)d.NP * KP;
     d2 sv[4], ev[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        sv[t] = *reinterpret_cast<const d2 *>(xall + (size_t)i * KP + 8 * t + 2 * q);
-        for (int rk = 1; rk < d.nranks; ++rk)
-            sv[t] += *reinterpret_cast<const d2 *>(xall + rk * stride + (size_t)i * KP + 8 * t + 2 * q);
-    }
-    {   // eps of dc:126 (draw buffer)
+    for (int t = 0; t < 4; ++t) sv[t] = d2{0.0, 0.0};
+    if (w == 0) {   // eps of dc:126 (draw buffer), in flight during the sum
         const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -481,6 +480,22 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
             ev[t].y = (live && kk + 1 < d.K) ? nx[kk + 1] : 0.0;
         }
     }
+    const double *base = src + (size_t)i * KP + 2 * q;
+#pragma unroll 4
+    for (int rk = w; rk < nsrc; rk += 4) {
+        const double *p = base + rk * stride;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) sv[t] += *reinterpret_cast<const d2 *>(p + 8 * t);
+    }
+    if (w > 0) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) part[w - 1][t][lane] = sv[t];
+    }
+    __syncthreads();
+    if (w > 0) return;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        for (int r = 0; r < 3; ++r) sv[t] += part[r][t][lane];
     d4 ax[2];
     ax[0] = ax[1] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1437,9 +1452,14 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
     if (d.kp != KP) return wide::launch_xchol(d, b, s);
     hipLaunchKernelGGL(k_xchol, dim3(1), dim3(256), 0, s, d, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
 }
-void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
+                  bool from_shards) {
     if (d.kp != KP) return wide::launch_xdraw(d, b, dr, iter, s);
-    hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(64), 0, s, d, b.xall, b.XM, b.X, dr, iter);
+    if (from_shards)   // one rank: sum the G shard messages here (no k_xred)
+        hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(256), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter);
+    else
+        hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(256), 0, s, d, b.xall, d.nranks, b.XM, b.X, dr,
+                           iter);
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(((d.PP + d.kp) / 32) * d.G * (d.kp / 32));
