@@ -171,3 +171,36 @@ def test_ingest_c3_size_rates(dcfm):
     print(f"\nk_nnz_cols {ms_nnz * 1e3:.1f} us ({b / ms_nnz / 1e6:.0f} GB/s); "
           f"k_stdize {min(ms_std, ms_std2) * 1e3:.1f} us ({2 * b / min(ms_std, ms_std2) / 1e6:.0f} GB/s, "
           "read + write)")
+
+
+def test_ingest_c5_size_sampled_columns(dcfm):
+    """c5's full shape (n = 2,000, p = 100,096 = 391 x 256: 1.6 GB raw, > 2^31 elements of
+    index space in the flattened input): nnz scan and standardise, checked on 96 sampled
+    output columns against the host formula (size-independent per-column property)."""
+    n, g, P, K = 2000, 256, 391, 30
+    p = g * P
+    r = np.random.default_rng(11)
+    Y = np.empty((n, p), order="F")
+    for c0 in range(0, p, 8192):                      # chunked fill keeps host peaks low
+        c1 = min(p, c0 + 8192)
+        Y[:, c0:c1] = r.standard_normal((n, c1 - c0)) * 2.0 + 0.5
+    Y[:, 77] = 0.0
+    nnz = dcfm.count_nonzero_columns(Y)
+    assert nnz[77] == 0 and (np.delete(nnz, 77) == n).all()
+    keep = np.flatnonzero(nnz != 0)                   # p - 1 kept: ingest the first p - 1 + a repeat
+    cols_all = np.concatenate([keep, keep[:1]])       # P*g indices (any columns may repeat)
+    varind = r.permutation(p)
+    smp = dcfm.Sampler(n, P, g, K, 0.5, 0, 1, 1, inject_draws=True)
+    try:
+        sd, _ = smp.set_data_raw(Y, dcfm.shard_columns(cols_all, varind, P, 0, g))
+        Yd = smp.get_data()
+    finally:
+        smp.close()
+    pick = r.choice(p, size=96, replace=False)
+    for q in pick:
+        m, j = divmod(q, P)
+        col = cols_all[varind[q]]
+        x = Y[:, col]
+        want = (x - x.mean()) * (1.0 / np.sqrt(x.var(ddof=1)))
+        assert rel_err(Yd[:, j, m], want) < YD_TOL
+        assert abs(sd[j, m] - x.std(ddof=1)) < 1e-12 * x.std(ddof=1)
