@@ -38,7 +38,7 @@ EXPORTS = (
     "dcfm_saved_samples", "dcfm_sigma_error", "dcfm_set_profiling", "dcfm_set_profiling_mask", "dcfm_get_kernel_stats",
     "dcfm_kernel_name",
     "dcfm_rng_fill", "dcfm_set_data_raw", "dcfm_get_data", "dcfm_count_nonzero_columns",
-    "dcfm_set_trace", "dcfm_get_trace",
+    "dcfm_set_trace", "dcfm_get_trace", "dcfm_init_state",
 )
 
 
@@ -114,6 +114,7 @@ def load_library(path: Path | None = None):
         "dcfm_set_data_raw": (C.c_int, [vp, _DP, C.c_int64, C.POINTER(C.c_int64), _DP, _DP]),
         "dcfm_get_data": (C.c_int, [vp, _DP]),
         "dcfm_set_trace": (C.c_int, [vp, C.c_int64]),
+        "dcfm_init_state": (C.c_int, [vp]),
         "dcfm_get_trace": (C.c_int, [vp, _DP, C.POINTER(C.c_int64)]),
         "dcfm_count_nonzero_columns": (C.c_int, [C.c_int, _DP, C.c_int32, C.c_int64, C.POINTER(C.c_int32),
                                                  _DP]),

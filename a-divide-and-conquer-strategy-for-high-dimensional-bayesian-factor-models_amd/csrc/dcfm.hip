@@ -611,6 +611,20 @@ int dcfm_set_data_raw(dcfm_handle *h, const double *Y, int64_t p_in, const int64
     return DCFM_OK;
 }
 
+int dcfm_init_state(dcfm_handle *h) {
+    if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
+    HIPC(h, hipSetDevice(h->cfg.device));
+    sync_all(h);
+    launch_init_state(h->d, h->b, h->stream);
+    HIPC(h, hipGetLastError());
+    HIPC(h, hipStreamSynchronize(h->stream));
+    h->cur = 0;
+    h->plam_valid = true;      // Plam = psi o tau' was formed (dc:86), as set_state's caller Plam
+    h->prep_valid = false;
+    h->have_state = true;
+    return DCFM_OK;
+}
+
 int dcfm_get_data(dcfm_handle *h, double *Yd_local) {
     if (!h || !Yd_local) return fail(h, DCFM_ERR_INVALID, "null argument");
     if (!h->have_data) return fail(h, DCFM_ERR_INVALID, "get_data: no data set");

@@ -108,6 +108,8 @@ void launch_stdize(const Dims &d, const double *Yraw, const long long *cols, dou
                    int *bad, hipStream_t s);
 // trace.hip: per-iteration chain summaries (||Lambda||_F^2, tr Omega, sum log ps, sum log tau)
 void launch_trace(const Dims &d, const Bufs &b, const double *tau_cur, double *part, hipStream_t s);
+// init.hip: dc:68-87 initial state from Philox (iteration-0 counters), delta/tau buffer 0
+void launch_init_state(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s);
 // dst[i] = sum_k src[k * count + i] in slice order (loopback all-reduce)
 void launch_sum_slices(const double *src, int ns, size_t count, double *dst, hipStream_t s);

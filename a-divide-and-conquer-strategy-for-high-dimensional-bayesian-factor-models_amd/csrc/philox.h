@@ -28,6 +28,12 @@ enum RngSite : uint32_t {
     SITE_PSI = 4,    // dc:150  Ga(df/2+0.5)
     SITE_DELTA = 5,  // dc:158,163  Ga(ad + ...)
     SITE_PS = 6,     // dc:170  Ga(as+n/2)
+    SITE_INIT_PS = 7,     // dc:69  Ga(as)     P x 1 x g   (dcfm_init_state, iter 0)
+    SITE_INIT_X = 8,      // dc:71  N(0,1)     n x K
+    SITE_INIT_PSI = 9,    // dc:73  Ga(df/2)   P x K x g
+    SITE_INIT_Z = 10,     // dc:80  N(0,1)     n x K x g
+    SITE_INIT_D1 = 11,    // dc:83  Ga(ad1)    delta(1,:,m)
+    SITE_INIT_D2 = 12,    // dc:83  Ga(ad2)    delta(2:K,:,m)
     SITE_DIAG = 15,  // dcfm_rng_fill
 };
 

@@ -95,6 +95,14 @@ class _HostInitDraws:
                 self.delta0[1:, m] = r.standard_gamma(hyper.ad2, size=K - 1)
 
 
+class _HostVarind:
+    """dc:50 varind = randperm(p) alone (the first draw of _HostInitDraws' stream)."""
+
+    def __init__(self, seed, p):
+        r = np.random.Generator(np.random.PCG64(np.random.SeedSequence([int(seed), 0, 0])))
+        self.varind = r.permutation(p)
+
+
 def initial_state(n, P, K, g, rho, hyper: Hyper, init) -> dict:
     """dc:68-87 from standard variates ``init`` (fields varind, ps0, X0, psi0, Z0, delta0)."""
     ps = (1.0 / hyper.bs) * np.asarray(init.ps0)                 # dc:69
@@ -126,12 +134,14 @@ def local_state(state: dict, s0: int, gl: int) -> dict:
 
 def divideconquer(Y, g, k, BURNIN, MCMC, thin, rho, *, seed=0, hyper: Hyper = Hyper(),
                   init_draws=None, iter_draws=None, nranks=1, rank=0, device=0, comm_uid=None,
-                  asm_batch=0, return_info=False, device_ingest=True):
+                  asm_batch=0, return_info=False, device_ingest=True, device_init=True):
     """Sigmaout = divideconquer(Y,g,k,BURNIN,MCMC,thin,rho)   (divideconquer.m:1).
 
     ``device_ingest`` (default): the zero-column scan and the partition/standardisation
     (dc:31-59) run on the GPU (dcfm_count_nonzero_columns, dcfm_set_data_raw); False
-    keeps them on the host (NumPy) and uploads Yd.
+    keeps them on the host (NumPy) and uploads Yd.  ``device_init`` (default, unless
+    ``init_draws`` are injected): the initial state of dc:68-87 is drawn on the GPU from
+    the Philox stream (dcfm_init_state); only varind (dc:50) is drawn on the host.
 
     Multi-GPU: call on every rank with the same arguments plus nranks/rank/device
     and the 128-byte RCCL id (``Sampler.unique_id()`` on rank 0, broadcast by
@@ -144,10 +154,16 @@ def divideconquer(Y, g, k, BURNIN, MCMC, thin, rho, *, seed=0, hyper: Hyper = Hy
     else:
         Yk, n, p, P, K, keep = preprocess(Y, g, k)
     N = BURNIN + MCMC                                            # dc:45
-    init = init_draws if init_draws is not None else _HostInitDraws(seed, n, p, g, K, hyper)
+    on_device_init = device_init and init_draws is None
+    if init_draws is not None:
+        init = init_draws
+    elif on_device_init:                                         # dc:50 only; dc:68-87 on the GPU
+        init = _HostVarind(seed, p)
+    else:
+        init = _HostInitDraws(seed, n, p, g, K, hyper)
     if not device_ingest:
         Yd = partition_standardize(Yk, g, np.asarray(init.varind))
-    state = initial_state(n, P, K, g, rho, hyper, init)
+    state = None if on_device_init else initial_state(n, P, K, g, rho, hyper, init)
     gl = g // nranks
     s0 = rank * gl
     smp = Sampler(n, P, g, K, rho, BURNIN, MCMC, thin, hyper=hyper, seed=seed, nranks=nranks,
@@ -161,7 +177,10 @@ def divideconquer(Y, g, k, BURNIN, MCMC, thin, rho, *, seed=0, hyper: Hyper = Hy
             smp.set_data_raw(Y, shard_columns(keep, init.varind, P, s0, gl))
         else:
             smp.set_data(Yd[:, :, s0:s0 + gl])
-        smp.set_state(local_state(state, s0, gl))
+        if state is None:
+            smp.init_state()
+        else:
+            smp.set_state(local_state(state, s0, gl))
         if iter_draws is not None:
             smp.set_draws(iter_draws, 1, N)
         smp.run(1, N)                                            # dc:90-197

@@ -149,6 +149,10 @@ class Sampler:
             setattr(view, f, _ptr(a))
         self._check(self.lib.dcfm_set_state(self.h, C.byref(view)))
 
+    def init_state(self):
+        """dc:68-87 on the device from the Philox stream (dcfm_init_state), instead of set_state."""
+        self._check(self.lib.dcfm_init_state(self.h))
+
     def set_draws(self, draws: dict, first_iter: int, n_iter: int):
         """draws: full-g arrays NZ (K,n,g,T), NX (K,n,T), NL (K,P,g,T), Gpsi (P,K,g,T),
         Gdelta (K,g,T), Gps (P,g,T) — the layout of oracle.IterDraws.stacked()."""

@@ -135,6 +135,13 @@ int  dcfm_get_data(dcfm_handle *h, double *Yd_local);
 int  dcfm_count_nonzero_columns(int device, const double *Y, int32_t n, int64_t p, int32_t *nnz_out,
                                 double *dev_ms);
 int  dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s);
+/* Initial state on the device (dc:68-87), instead of dcfm_set_state:
+ * ps = Ga(as)/bs, omega = ps (Q1), X, Z ~ N(0,1), psijh = (2/df) Ga(df/2), delta(1) =
+ * bd1 Ga(ad1), delta(2:K) = bd2 Ga(ad2), tauh = cumprod, Plam = psijh .* tauh', Lambda = 0,
+ * from the handle's Philox key at iteration-0 counters (sites 7-12; variate e of a shard
+ * = MATLAB linear index e inside that shard's array, counter row e/32, index e%32 — as
+ * dcfm_rng_fill, which reproduces them).  Identical on any number of ranks. */
+int  dcfm_init_state(dcfm_handle *h);
 /* Draws for iterations first_iter .. first_iter+n_iter-1 (1-based, as iter). */
 int  dcfm_set_draws(dcfm_handle *h, const dcfm_draws_view *d, int64_t first_iter, int64_t n_iter);
 
