@@ -576,10 +576,11 @@ int dcfm_set_data_raw(dcfm_handle *h, const double *Y, int64_t p_in, const int64
                         (long long)cols[c], (long long)p_in);
     HIPC(h, hipSetDevice(h->cfg.device));
     DevScratch sc;
-    void *qY = nullptr, *qc = nullptr, *qsd = nullptr, *qbad = nullptr;
+    void *qY = nullptr, *qc = nullptr, *qsd = nullptr, *qbad = nullptr, *qmi = nullptr;
     const size_t ybytes = (size_t)d.n * (size_t)p_in * sizeof(double);
     if (sc.alloc(&qY, ybytes) != hipSuccess || sc.alloc(&qc, ncols * sizeof(int64_t)) != hipSuccess ||
-        sc.alloc(&qsd, ncols * sizeof(double)) != hipSuccess || sc.alloc(&qbad, sizeof(int)) != hipSuccess)
+        sc.alloc(&qsd, ncols * sizeof(double)) != hipSuccess || sc.alloc(&qbad, sizeof(int)) != hipSuccess ||
+        sc.alloc(&qmi, 2 * ncols * sizeof(double)) != hipSuccess)
         return fail(h, DCFM_ERR_ALLOC, "set_data_raw: device scratch (%zu bytes of Y) failed", ybytes);
     hipStream_t s = h->stream;
     HIPC(h, hipMemcpyAsync(qY, Y, ybytes, hipMemcpyHostToDevice, s));
@@ -589,7 +590,7 @@ int dcfm_set_data_raw(dcfm_handle *h, const double *Y, int64_t p_in, const int64
     if (!ea || !eb) return fail(h, DCFM_ERR_HIP, "set_data_raw: hipEventCreate failed");
     HIPC(h, hipEventRecord(ea, s));
     launch_stdize(d, static_cast<const double *>(qY), static_cast<const long long *>(qc), h->b.Y, h->b.yy,
-                  static_cast<double *>(qsd), static_cast<int *>(qbad), s);
+                  static_cast<double *>(qsd), static_cast<int *>(qbad), static_cast<double *>(qmi), s);
     HIPC(h, hipGetLastError());
     HIPC(h, hipEventRecord(eb, s));
     int bad = 0;

@@ -105,7 +105,7 @@ void launch_sigma_err(const double *S, int p, const double *U, int R, const doub
 // ingest.hip: dc:31-34 column nnz counts; dc:50-59 partition + standardise into Y / yy
 void launch_nnz_cols(const double *Y, int n, long long p, int *nnz, hipStream_t s);
 void launch_stdize(const Dims &d, const double *Yraw, const long long *cols, double *Y, double *yy, double *sd,
-                   int *bad, hipStream_t s);
+                   int *bad, double *mean_inv, hipStream_t s);
 // trace.hip: per-iteration chain summaries (||Lambda||_F^2, tr Omega, sum log ps, sum log tau)
 void launch_trace(const Dims &d, const Bufs &b, const double *tau_cur, double *part, hipStream_t s);
 // init.hip: dc:68-87 initial state from Philox (iteration-0 counters), delta/tau buffer 0

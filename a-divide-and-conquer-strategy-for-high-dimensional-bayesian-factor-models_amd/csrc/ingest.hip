@@ -2,17 +2,16 @@
 // moved next to the sweep, so a raw n x p matrix goes to HBM once and Yd is formed there.
 //
 //   k_nnz_cols  dc:31-34   nnzcol(j) = nnz(Y(:,j))  (NaN counts as non-zero, as nnz does)
-//   k_stdize    dc:50-59   Yd(:,:,m) = Y(:,varind(block m)); Md = mean; VYd = var (n-1);
-//                          Yd = (Yd - Md) .* (1./sqrt(VYd))  -> the sweep's [G][NP][PP] layout,
-//                          padding zero-filled, plus yy = sum_i Yd_ij^2 (the residual-SS
-//                          identity's input, formerly computed on the host in dcfm_set_data)
+//   k_colstats  dc:57      Md = mean, VYd = var (n-1) of Yd(:,j,m) = Y(:,varind(...)), and
+//                          yy = sum_i Yd_ij^2 (the residual-SS identity's input)
+//   k_stdize    dc:50-59   Yd = (Yd - Md) .* (1./sqrt(VYd)) -> the sweep's [G][NP][PP]
+//                          layout, padding zero-filled
 //
 // Both are one-time HBM passes.  Input columns are contiguous n-vectors (MATLAB column
 // major), so every read is a 64-lane run of 512 B; k_stdize's output is [i][j] (j fastest),
 // so a 64-row x 16-column tile is transposed through LDS and written as 128 B row runs.
-// Algorithmic bytes: k_nnz_cols 8 n p;  k_stdize 8 n P G (read) + 8 NP PP G (write) + the
-// two statistics passes, which re-read a block's 16 columns from L2 (16 x n x 8 B = 128 KB
-// at n = 1,000).
+// Algorithmic bytes: k_nnz_cols 8 n p;  k_colstats 8 n P G (its 2nd / 3rd passes re-read
+// the wave's column from L2);  k_stdize 8 n P G read + 8 NP PP G write.
 #include "dcfm_internal.h"
 
 namespace dcfm {
@@ -42,94 +41,109 @@ __global__ __launch_bounds__(256) void k_nnz_cols(const double *__restrict__ Y, 
     if (lane == 0) nnz[c] = cnt;
 }
 
-constexpr int ST_COLS = 16;            // output columns per block (1,280 blocks at c3)
-constexpr int ST_CPW = ST_COLS / 4;    // columns per wave
-constexpr int ST_RG = 256 / ST_COLS;   // row groups of the transposed write
+constexpr int CS_R = 32;   // doubles per lane of a register-resident column (n <= 2,048)
 
-// grid (cdiv(PP, ST_COLS), G); cols[m * P + j] = input column of local shard m, position j
-__global__ __launch_bounds__(256) void k_stdize(const double *__restrict__ Yraw, int n, const long long *__restrict__ cols,
-                                                int P, int NP, int PP, double *__restrict__ Y,
-                                                double *__restrict__ yy, double *__restrict__ sd,
-                                                int *__restrict__ bad) {
+// k_colstats: one wave per output column (m, j): dc:57 two-pass mean and var (n - 1) of
+// the gathered input column, then sum_i Yd_ij^2 of the standardised column -> mean /
+// 1/sqrt(var) / yy / sd; up to n = 2,048 (every BASELINE config) the column is loaded once
+// into registers (32 loads in flight per lane) and the three passes run there.  Columns are independent waves, so the grid
+// has P*G waves however few shards there are (c4: 10,000; the old fused kernel had 16
+// columns per block and a serial chain per wave: 223 us at c4).
+__global__ __launch_bounds__(256) void k_colstats(const double *__restrict__ Yraw, int n,
+                                                  const long long *__restrict__ cols, int P, int G, int PP,
+                                                  double *__restrict__ mean_inv, double *__restrict__ yy,
+                                                  double *__restrict__ sd, int *__restrict__ bad) {
+    const int lane = threadIdx.x & 63;
+    const long long q = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);   // m * P + j
+    if (q >= (long long)P * G) return;
+    const int m = (int)(q / P), j = (int)(q % P);
+    const double *x = Yraw + cols[q] * (long long)n;
+    double mu, var, inv, ys;
+    if (n <= 64 * CS_R) {   // the column held in registers: one memory read, all loads in flight
+        double v[CS_R];
+#pragma unroll
+        for (int r = 0; r < CS_R; ++r) v[r] = lane + 64 * r < n ? x[lane + 64 * r] : 0.0;
+        double s0 = 0.0;
+#pragma unroll
+        for (int r = 0; r < CS_R; ++r) s0 += v[r];
+        mu = wave_sum64(s0) / n;
+        double q0 = 0.0;
+#pragma unroll
+        for (int r = 0; r < CS_R; ++r) {
+            const double a = lane + 64 * r < n ? v[r] - mu : 0.0;
+            q0 += a * a;
+        }
+        var = wave_sum64(q0) / (n - 1);
+        inv = 1.0 / sqrt(var);                              // dc:59 1./sqrt(VYd)
+        double y0 = 0.0;                                    // yy of the standardised column
+#pragma unroll
+        for (int r = 0; r < CS_R; ++r) {
+            const double a = lane + 64 * r < n ? (v[r] - mu) * inv : 0.0;
+            y0 += a * a;
+        }
+        ys = wave_sum64(y0);
+    } else {                // long columns: three passes, the 2nd and 3rd from L2
+        double s0 = 0.0, s1 = 0.0;
+        int i = lane;
+        for (; i + 64 < n; i += 128) { s0 += x[i]; s1 += x[i + 64]; }
+        if (i < n) s0 += x[i];
+        mu = wave_sum64(s0 + s1) / n;
+        double q0 = 0.0, q1 = 0.0;
+        for (i = lane; i + 64 < n; i += 128) {
+            const double a = x[i] - mu, b = x[i + 64] - mu;
+            q0 += a * a;
+            q1 += b * b;
+        }
+        if (i < n) { const double a = x[i] - mu; q0 += a * a; }
+        var = wave_sum64(q0 + q1) / (n - 1);
+        inv = 1.0 / sqrt(var);
+        double y0 = 0.0, y1 = 0.0;
+        for (i = lane; i + 64 < n; i += 128) {
+            const double a = (x[i] - mu) * inv, b = (x[i + 64] - mu) * inv;
+            y0 += a * a;
+            y1 += b * b;
+        }
+        if (i < n) { const double a = (x[i] - mu) * inv; y0 += a * a; }
+        ys = wave_sum64(y0 + y1);
+    }
+    if (lane == 0) {
+        if (var == 0.0) atomicOr(bad, 1);                   // Q13: dc:59 divides by zero
+        mean_inv[2 * q] = mu;
+        mean_inv[2 * q + 1] = inv;
+        yy[(size_t)m * PP + j] = ys;
+        if (sd) sd[q] = sqrt(var);
+    }
+}
+
+// k_stdize: dc:58-59 (Yd - Md) .* (1./sqrt(VYd)) into [G][NP][PP], a 64-row x 16-column
+// tile per block (grid (PP/16, NP/64, G)) transposed through LDS; padding rows / columns
+// written as zeros.  A pure stream: 8nP read (MALL / HBM) + 8 NP PP write per shard.
+constexpr int ST_COLS = 16;
+__global__ __launch_bounds__(256) void k_stdize(const double *__restrict__ Yraw, int n,
+                                                const long long *__restrict__ cols, int P, int NP, int PP,
+                                                const double *__restrict__ mean_inv, double *__restrict__ Y) {
     __shared__ double tile[ST_COLS][65];
-    __shared__ double s_mean[ST_COLS], s_inv[ST_COLS];
-    __shared__ double s_yy[ST_RG][ST_COLS];
-    const int m = blockIdx.y, j0 = blockIdx.x * ST_COLS;
+    const int m = blockIdx.z, j0 = blockIdx.x * ST_COLS, i0 = blockIdx.y * 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-
-    // column base pointers of this wave's ST_CPW columns (null past P: padding columns)
-    const double *src[ST_CPW];
+    const int i = i0 + lane;
 #pragma unroll
-    for (int c = 0; c < ST_CPW; ++c) {
-        const int j = j0 + w * ST_CPW + c;
-        src[c] = j < P ? Yraw + cols[(long long)m * P + j] * (long long)n : nullptr;
-    }
-    // dc:57 Md = mean(Yd), VYd = var(Yd) (two-pass, n - 1); the wave's columns advance
-    // together so ST_CPW independent loads per lane are in flight in each pass
-    double mu[ST_CPW], q[ST_CPW];
-#pragma unroll
-    for (int c = 0; c < ST_CPW; ++c) mu[c] = 0.0;
-    for (int i = lane; i < n; i += 64) {
-#pragma unroll
-        for (int c = 0; c < ST_CPW; ++c)
-            if (src[c]) mu[c] += src[c][i];
-    }
-#pragma unroll
-    for (int c = 0; c < ST_CPW; ++c) { mu[c] = wave_sum64(mu[c]) / n; q[c] = 0.0; }
-    for (int i = lane; i < n; i += 64) {
-#pragma unroll
-        for (int c = 0; c < ST_CPW; ++c)
-            if (src[c]) { const double a = src[c][i] - mu[c]; q[c] += a * a; }
-    }
-#pragma unroll
-    for (int c = 0; c < ST_CPW; ++c) {
-        const int jl = w * ST_CPW + c;
-        double inv = 0.0;
-        if (src[c]) {
-            const double var = wave_sum64(q[c]) / (n - 1);
-            if (var == 0.0 && lane == 0) atomicOr(bad, 1);      // Q13: dc:59 divides by zero
-            inv = 1.0 / sqrt(var);                              // dc:59 1./sqrt(VYd)
-            if (sd && lane == 0) sd[(long long)m * P + j0 + jl] = sqrt(var);
+    for (int c = 0; c < ST_COLS / 4; ++c) {                 // wave w reads columns w*4 .. w*4+3
+        const int jl = w * (ST_COLS / 4) + c, j = j0 + jl;
+        double v = 0.0;
+        if (j < P && i < n) {
+            const long long q = (long long)m * P + j;
+            v = (Yraw[cols[q] * (long long)n + i] - mean_inv[2 * q]) * mean_inv[2 * q + 1];
         }
-        if (lane == 0) { s_mean[jl] = src[c] ? mu[c] : 0.0; s_inv[jl] = inv; }
+        tile[jl][lane] = v;
     }
     __syncthreads();
-
-    // dc:58-59 centre and scale, transposed through LDS into [i][j]
-    const int tc = threadIdx.x % ST_COLS, tr = threadIdx.x / ST_COLS;
-    const int jw = j0 + tc;
-    double acc = 0.0;
+    const int tc = threadIdx.x % ST_COLS, tr = threadIdx.x / ST_COLS, jw = j0 + tc;
+    if (jw >= PP) return;
     double *Ym = Y + (size_t)m * NP * PP;
-    for (int i0 = 0; i0 < NP; i0 += 64) {
-        const int i = i0 + lane;
 #pragma unroll
-        for (int c = 0; c < ST_CPW; ++c) {
-            const int jl = w * ST_CPW + c;
-            double v = 0.0;
-            if (src[c] && i < n) v = (src[c][i] - s_mean[jl]) * s_inv[jl];
-            tile[jl][lane] = v;
-        }
-        __syncthreads();
-        if (jw < PP) {
-#pragma unroll
-            for (int r = 0; r < 64 / ST_RG; ++r) {
-                const int il = tr + ST_RG * r, ii = i0 + il;
-                if (ii < NP) {
-                    const double v = tile[tc][il];
-                    Ym[(size_t)ii * PP + jw] = v;
-                    acc += v * v;
-                }
-            }
-        }
-        __syncthreads();
-    }
-    s_yy[tr][tc] = acc;
-    __syncthreads();
-    if (threadIdx.x < ST_COLS && j0 + (int)threadIdx.x < PP) {
-        double s = 0.0;
-#pragma unroll
-        for (int r = 0; r < ST_RG; ++r) s += s_yy[r][threadIdx.x];
-        yy[(size_t)m * PP + j0 + threadIdx.x] = s;
+    for (int r = 0; r < 64 / (256 / ST_COLS); ++r) {
+        const int il = tr + (256 / ST_COLS) * r, ii = i0 + il;
+        if (ii < NP) Ym[(size_t)ii * PP + jw] = tile[tc][il];
     }
 }
 
@@ -139,9 +153,12 @@ void launch_nnz_cols(const double *Y, int n, long long p, int *nnz, hipStream_t 
 }
 
 void launch_stdize(const Dims &d, const double *Yraw, const long long *cols, double *Y, double *yy, double *sd,
-                   int *bad, hipStream_t s) {
-    hipLaunchKernelGGL(k_stdize, dim3((d.PP + ST_COLS - 1) / ST_COLS, d.G), dim3(256), 0, s, Yraw, d.n, cols,
-                       d.P, d.NP, d.PP, Y, yy, sd, bad);
+                   int *bad, double *mean_inv, hipStream_t s) {
+    const long long ncol = (long long)d.P * d.G;
+    hipLaunchKernelGGL(k_colstats, dim3((unsigned)((ncol + 3) / 4)), dim3(256), 0, s, Yraw, d.n, cols, d.P, d.G, d.PP,
+                       mean_inv, yy, sd, bad);
+    hipLaunchKernelGGL(k_stdize, dim3((d.PP + ST_COLS - 1) / ST_COLS, (d.NP + 63) / 64, d.G), dim3(256), 0, s, Yraw,
+                       d.n, cols, d.P, d.NP, d.PP, mean_inv, Y);
 }
 
 }  // namespace dcfm

@@ -42,6 +42,7 @@ CASES = {
     "g1": (25, 20, 1, 4, 0),
     "many_shards": (20, 96, 12, 3, 0),
     "wide_P": (130, 400, 2, 40, 0),           # P = 200 spans 7 column tiles, n > 64 rows
+    "long_n": (2100, 40, 2, 3, 0),            # n > 2,048: k_colstats' three-pass path
 }
 
 
