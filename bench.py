@@ -163,16 +163,18 @@ def main():
         obj = [dcfm.Sampler.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         smp.comm_init(obj[0])
+    cols = dcfm.shard_columns(keep, init.varind, P, s0, gl)
+    smp.set_data_raw(Y, cols)                 # first launches load the code objects
     t_ing = time.perf_counter()
-    _, ms_std = smp.set_data_raw(Y, dcfm.shard_columns(keep, init.varind, P, s0, gl))
+    _, ms_std = smp.set_data_raw(Y, cols)
     t_ing = time.perf_counter() - t_ing
     ingest = {"k_nnz_cols_us": round(ms_nnz * 1e3, 1),
               "k_nnz_cols_gbs": round(8.0 * n * p / (ms_nnz * 1e-3) / 1e9, 1) if ms_nnz > 0 else None,
-              "k_stdize_us": round(ms_std * 1e3, 1),
-              "k_stdize_gbs": round(16.0 * n * P * gl / (ms_std * 1e-3) / 1e9, 1) if ms_std > 0 else None,
+              "k_colstats_k_stdize_us": round(ms_std * 1e3, 1),
+              "k_colstats_k_stdize_gbs": round(16.0 * n * P * gl / (ms_std * 1e-3) / 1e9, 1) if ms_std > 0 else None,
               "set_data_raw_ms_incl_pcie": round(t_ing * 1e3, 1),
               "note": "one-time, before the timed region; GB/s = algorithmic bytes (8np read for the scan; "
-                      "8nP read + 8nP write per rank for the standardise) / kernel time"}
+                      "8nP read + 8nP write per rank for stats + standardise) / kernel time, second call"}
     t_init = time.perf_counter()
     smp.init_state()                          # dcfm_init_state: Philox, iteration-0 counters
     ingest["init_state_ms"] = round((time.perf_counter() - t_init) * 1e3, 2)
