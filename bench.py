@@ -129,7 +129,18 @@ def main():
     import torch
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("gloo")    # rendezvous + timing only; data path is RCCL in libdcfm
+        # rendezvous + timing only (the data path is RCCL inside libdcfm).  Gloo prints its
+        # "connected to N peer ranks" banner on fd 1; route it to stderr so stdout carries
+        # exactly the one JSON line.
+        sys.stdout.flush()
+        saved_fd = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved_fd, 1)
+            os.close(saved_fd)
 
     import __graft_entry__ as ge
     dcfm = ge.load_package()
