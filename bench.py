@@ -59,6 +59,15 @@ def algorithmic_work(kname, d, n_launch_samples):
     return 0.0, 0.0, "hbm"
 
 
+def binding_roof(flops, nbytes):
+    """The roof a kernel's algorithmic work hits first: "hbm" when moving its bytes at the
+    HBM peak takes longer than its flops at the fp64 peak, else "mfma" (k_lambda is HBM-bound
+    at K = 30 — 4.3 us of bytes vs 3.7 us of flops — and MFMA-bound at K = 100)."""
+    if flops <= 0.0:
+        return "hbm"
+    return "hbm" if nbytes / (HBM_PEAK_GBS * 1e9) >= flops / (FP64_MFMA_PEAK_TFLOPS * 1e12) else "mfma"
+
+
 def pmc_traffic(kernel, workload_tag):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the
     same workload (profiles/r01_<tag>_pmc.json, written by tools/pmc_summary.py from
@@ -286,10 +295,11 @@ def main():
         """Algorithmic (flops, bytes, bound) per launch: per-iteration work spread over the
         launches of one iteration (the Y-pass / row kernels run as two shard groups)."""
         if name == "k_assemble":
-            return algorithmic_work(name, d, saved / max(cnt, 1))
-        fl, by, bound = algorithmic_work(name, d, 0)
+            fl, by, _ = algorithmic_work(name, d, saved / max(cnt, 1))
+            return fl, by, binding_roof(fl, by)
+        fl, by, _ = algorithmic_work(name, d, 0)
         per_iter = max(cnt, 1) / max(iters, 1)
-        return fl / per_iter, by / per_iter, bound
+        return fl / per_iter, by / per_iter, binding_roof(fl, by)
 
     if stats:
         for name, (ms, cnt) in stats.items():
