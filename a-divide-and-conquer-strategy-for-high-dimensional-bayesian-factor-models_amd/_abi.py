@@ -34,7 +34,7 @@ EXPORTS = (
     "dcfm_create", "dcfm_destroy", "dcfm_last_error", "dcfm_abi_version",
     "dcfm_comm_unique_id", "dcfm_comm_init", "dcfm_comm_init_loopback", "dcfm_set_data", "dcfm_set_state",
     "dcfm_set_draws", "dcfm_run", "dcfm_synchronize", "dcfm_get_state", "dcfm_get_sigma",
-    "dcfm_get_sigma_cols",
+    "dcfm_get_sigma_cols", "dcfm_sigma_block",
     "dcfm_saved_samples", "dcfm_sigma_error", "dcfm_set_profiling", "dcfm_set_profiling_mask", "dcfm_get_kernel_stats",
     "dcfm_kernel_name",
     "dcfm_rng_fill", "dcfm_set_data_raw", "dcfm_get_data", "dcfm_count_nonzero_columns",
@@ -103,6 +103,7 @@ def load_library(path: Path | None = None):
         "dcfm_get_state": (C.c_int, [vp, C.POINTER(DcfmStateView)]),
         "dcfm_get_sigma": (C.c_int, [vp, _DP]),
         "dcfm_get_sigma_cols": (C.c_int, [vp, C.c_int64, C.c_int64, _DP]),
+        "dcfm_sigma_block": (C.c_int, [vp, C.POINTER(C.c_int64)]),
         "dcfm_saved_samples": (C.c_int64, [vp]),
         "dcfm_sigma_error": (C.c_int, [vp, _DP, C.c_int32, _DP, C.c_int32, C.c_uint64, _DP]),
         "dcfm_set_profiling": (C.c_int, [vp, C.c_int]),

@@ -68,6 +68,7 @@ struct dcfm_handle {
     ncclComm_t comm = nullptr, comm_side = nullptr, comm_asm = nullptr;
     bool comm_ok = false;
     std::shared_ptr<LoopGroup> loop;  // loopback collectives instead of RCCL (testing)
+    std::vector<int> Tb;              // Sigma tile-row boundaries of all ranks (block-sharded)
     hipEvent_t lp_ready = nullptr, lp_done = nullptr;
     hipEvent_t e_lam = nullptr, e_prep = nullptr, e_xchol = nullptr, e_batch = nullptr,
                e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
@@ -80,6 +81,8 @@ struct dcfm_handle {
     int batch = 0;                // saved samples pending in Lb[lb]
     int64_t saved = 0;
     bool have_data = false, have_state = false;
+    int *nan_dev = nullptr;       // k_finite flag (device) and its pinned host mirror
+    int *nan_host = nullptr;
     std::string err;
     std::vector<void *> allocs;
     double *draws_mem = nullptr;
@@ -181,11 +184,62 @@ static int loop_allgather(dcfm_handle *h, const double *send, double *recv, size
     return DCFM_OK;
 }
 
+// Gather to one rank: rank k's cnt[k] doubles land at recv + base[k] on root (recv is
+// only read on root; root's own part is already in place when send == recv + base[root]).
+static int loop_gather(dcfm_handle *h, const double *send, double *recv, const std::vector<long long> &base,
+                       const std::vector<long long> &cnt, int root, hipStream_t s) {
+    LoopGroup &G = *h->loop;
+    const int r = h->d.rank;
+    HIPC(h, hipEventRecord(h->lp_ready, s));
+    {
+        std::unique_lock<std::mutex> lk(G.mu);
+        G.send[r] = send;
+        G.ready[r] = h->lp_ready;
+        if (!G.barrier(lk)) return fail(h, DCFM_ERR_RCCL, "loopback gather: ranks did not meet");
+    }
+    if (r == root)
+        for (int k = 0; k < G.n; ++k) {
+            if (cnt[k] == 0 || G.send[k] == recv + base[k]) continue;
+            if (k != r) HIPC(h, hipStreamWaitEvent(s, G.ready[k], 0));
+            HIPC(h, hipMemcpyAsync(recv + base[k], G.send[k], cnt[k] * sizeof(double), hipMemcpyDeviceToDevice, s));
+        }
+    HIPC(h, hipEventRecord(h->lp_done, s));
+    {
+        std::unique_lock<std::mutex> lk(G.mu);
+        G.done[r] = h->lp_done;
+        if (!G.barrier(lk)) return fail(h, DCFM_ERR_RCCL, "loopback gather: ranks did not meet");
+    }
+    if (r != root) HIPC(h, hipStreamWaitEvent(s, G.done[root], 0));   // root has read my buffer
+    {
+        std::unique_lock<std::mutex> lk(G.mu);
+        if (!G.barrier(lk)) return fail(h, DCFM_ERR_RCCL, "loopback gather: ranks did not meet");
+    }
+    return DCFM_OK;
+}
+
 // recv = concatenation over ranks of count doubles (send may be recv + rank * count)
 static int coll_allgather(dcfm_handle *h, int ch, const double *send, double *recv, size_t count, hipStream_t s) {
     if (h->loop) return loop_allgather(h, send, recv, count, s);
     ncclComm_t c = ch == CH_MAIN ? h->comm : (ch == CH_SIDE ? h->comm_side : h->comm_asm);
     NCCLC(h, ncclAllGather(send, recv, count, ncclDouble, c, s));
+    return DCFM_OK;
+}
+
+// Point-to-point gather of variable-size parts to `root` (no all-reduce of the data): RCCL
+// send / recv in one group on the assembly communicator, or the loopback group.
+static int coll_gather(dcfm_handle *h, const double *send, double *recv, const std::vector<long long> &base,
+                       const std::vector<long long> &cnt, int root, hipStream_t s) {
+    if (h->loop) return loop_gather(h, send, recv, base, cnt, root, s);
+    const int r = h->d.rank;
+    NCCLC(h, ncclGroupStart());
+    if (r == root) {
+        for (int k = 0; k < h->d.nranks; ++k)
+            if (k != root && cnt[k] > 0)
+                NCCLC(h, ncclRecv(recv + base[k], (size_t)cnt[k], ncclDouble, k, h->comm_asm, s));
+    } else if (cnt[r] > 0) {
+        NCCLC(h, ncclSend(send, (size_t)cnt[r], ncclDouble, root, h->comm_asm, s));
+    }
+    NCCLC(h, ncclGroupEnd());
     return DCFM_OK;
 }
 
@@ -252,6 +306,20 @@ static void sync_all(dcfm_handle *h) {
     if (h->sasm) (void)hipStreamSynchronize(h->sasm);
 }
 
+// DCFM_ERR_NUMERIC once the sentinel of a finished dcfm_run has seen a non-finite state
+// (call after the streams are synchronised)
+static int numeric_status(dcfm_handle *h) {
+    if (h->nan_host && *h->nan_host)
+        return fail(h, DCFM_ERR_NUMERIC, "non-finite sampler state (NaN / Inf in Lambda, ps, omega, X or tau) "
+                                         "after dcfm_run; set_state / init_state to restart");
+    return DCFM_OK;
+}
+static int reset_numeric(dcfm_handle *h) {
+    HIPC(h, hipMemset(h->nan_dev, 0, sizeof(int)));
+    *h->nan_host = 0;
+    return DCFM_OK;
+}
+
 static void collect_prof(dcfm_handle *h) {
     if (h->recs.empty()) return;
     sync_all(h);
@@ -265,6 +333,23 @@ static void collect_prof(dcfm_handle *h) {
         h->evpool.push_back(r.b);
     }
     h->recs.clear();
+}
+
+// Sigma block-sharding: tile rows [Tb[k], Tb[k+1]) to rank k, contiguous, each rank's
+// share of the nt(nt+1)/2 lower tiles as near total/nranks as row granularity allows
+// (rank k's tiles: tri(Tb[k+1]) - tri(Tb[k])).  Ranks may own no rows when nt < nranks.
+static std::vector<int> sigma_split(int nt, int nranks) {
+    std::vector<int> Tb(nranks + 1, nt);
+    Tb[0] = 0;
+    const double total = (double)tri(nt);
+    for (int k = 1; k < nranks; ++k) {
+        const double target = total * k / nranks;
+        int t = Tb[k - 1];
+        while (t < nt && (double)tri(t) < target) ++t;                 // first t with tri(t) >= target
+        if (t > Tb[k - 1] && target - (double)tri(t - 1) < (double)tri(t) - target) --t;   // the nearer
+        Tb[k] = t;
+    }
+    return Tb;
 }
 
 // ---------------------------------------------------------------------------
@@ -293,6 +378,14 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     if (!(c.rho >= 0.0 && c.rho <= 1.0)) return fail(nullptr, DCFM_ERR_INVALID, "rho must be in [0,1]");
     if (c.thin < 1 || c.mcmc < 0 || c.burnin < 0)
         return fail(nullptr, DCFM_ERR_INVALID, "thin >= 1, mcmc >= 0, burnin >= 0 required");
+    if (!(c.bs > 0 && c.bd1 > 0 && c.bd2 > 0 && c.df > 0))
+        return fail(nullptr, DCFM_ERR_INVALID, "bs, bd1, bd2, df must be > 0 (dc:62-65)");
+    // on-device gammas are Marsaglia-Tsang for shape >= 1 (philox.h); the smallest shapes the
+    // stream draws are as, df/2 (init, dc:69,73), ad1, ad2 (dc:83) and df/2 + 0.5 (dc:150)
+    if (!(c.flags & DCFM_FLAG_INJECT_DRAWS) && !(c.as_ >= 1.0 && c.df >= 2.0 && c.ad1 >= 1.0 && c.ad2 >= 1.0))
+        return fail(nullptr, DCFM_ERR_UNSUPPORTED,
+                    "on-device gamma draws need shapes >= 1: as >= 1, df >= 2, ad1 >= 1, ad2 >= 1 "
+                    "(got %g, %g, %g, %g); inject the draws for other hyper-parameters", c.as_, c.df, c.ad1, c.ad2);
     const int nranks = c.nranks < 1 ? 1 : c.nranks;
     if (c.rank < 0 || c.rank >= nranks) return fail(nullptr, DCFM_ERR_INVALID, "bad rank");
     if (c.g % nranks)
@@ -337,6 +430,16 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         HIPC(h, hipEventCreateWithFlags(&h->e_used[sl], hipEventDisableTiming));
     }
 
+    {
+        void *q = nullptr;
+        HIPC(h, hipMalloc(&q, sizeof(int)));
+        h->allocs.push_back(q);
+        h->nan_dev = static_cast<int *>(q);
+        HIPC(h, hipMemset(h->nan_dev, 0, sizeof(int)));
+        HIPC(h, hipHostMalloc(&q, sizeof(int), hipHostMallocDefault));
+        h->nan_host = static_cast<int *>(q);
+        *h->nan_host = 0;
+    }
     Dims &d = h->d;
     d.n = c.n; d.P = c.P; d.g = c.g; d.K = c.K;
     d.nranks = nranks; d.rank = c.rank;
@@ -408,7 +511,14 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     ALLOC(b.Lb[1], p * (size_t)b.LDB);
     ALLOC(b.wsum[0], p);
     ALLOC(b.wsum[1], p);
-    ALLOC(b.Sigma, p * p);
+    // Sigmaout block-sharded over ranks: contiguous tile rows balanced by tile count
+    {
+        const int nt = (d.p + ASM_TILE - 1) / ASM_TILE;
+        h->Tb = sigma_split(nt, nranks);
+        b.T0 = h->Tb[c.rank];
+        b.T1 = h->Tb[c.rank + 1];
+    }
+    ALLOC(b.Sigma, (size_t)(tri(b.T1) - tri(b.T0)) * ASM_TILE * ASM_TILE);
     if (!d.inject) {
         const size_t K = c.K, n = c.n, P = c.P;
         const size_t nz = K * n * g, nx = K * n, nl = K * P * g, gpsi = P * K * g, gdel = K * g, gps = P * g;
@@ -432,14 +542,11 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         }
     }
 #undef ALLOC
-    // lower-triangle assembly tiles, dealt round-robin over ranks
+    // this rank's lower-triangle assembly tiles, in the storage order of its Sigma block
     {
-        const int nt = (d.p + ASM_TILE - 1) / ASM_TILE;
         std::vector<int2> tl;
-        int64_t idx = 0;
-        for (int ti = 0; ti < nt; ++ti)
-            for (int tj = 0; tj <= ti; ++tj, ++idx)
-                if (idx % nranks == c.rank) tl.push_back(make_int2(ti, tj));
+        for (int ti = b.T0; ti < b.T1; ++ti)
+            for (int tj = 0; tj <= ti; ++tj) tl.push_back(make_int2(ti, tj));
         b.ntiles = (int)tl.size();
         void *q = nullptr;
         HIPC(h, hipMalloc(&q, std::max<size_t>(1, tl.size()) * sizeof(int2)));
@@ -472,6 +579,7 @@ void dcfm_destroy(dcfm_handle *h) {
     if (h->comm_side) ncclCommDestroy(h->comm_side);
     if (h->comm) ncclCommDestroy(h->comm);
     for (void *q : h->allocs) (void)hipFree(q);
+    if (h->nan_host) (void)hipHostFree(h->nan_host);
     if (h->draws_mem) (void)hipFree(h->draws_mem);
     if (h->trace) (void)hipFree(h->trace);
     if (h->sasm && h->sasm != h->stream) (void)hipStreamDestroy(h->sasm);
@@ -623,7 +731,7 @@ int dcfm_init_state(dcfm_handle *h) {
     h->plam_valid = true;      // Plam = psi o tau' was formed (dc:86), as set_state's caller Plam
     h->prep_valid = false;
     h->have_state = true;
-    return DCFM_OK;
+    return reset_numeric(h);
 }
 
 int dcfm_get_data(dcfm_handle *h, double *Yd_local) {
@@ -760,7 +868,7 @@ int dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s) {
     h->plam_valid = true;
     h->prep_valid = false;
     h->have_state = true;
-    return DCFM_OK;
+    return reset_numeric(h);
 }
 
 int dcfm_get_state(dcfm_handle *h, dcfm_state_view *o) {
@@ -768,6 +876,7 @@ int dcfm_get_state(dcfm_handle *h, dcfm_state_view *o) {
     const Dims &d = h->d;
     HIPC(h, hipSetDevice(h->cfg.device));
     sync_all(h);
+    if (int rc = numeric_status(h)) return rc;
     std::vector<double> v;
     int rc;
     const size_t KP = d.kp;
@@ -1074,6 +1183,9 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     }
     int rc = flush_batch(h);
     if (rc) return rc;
+    launch_finite(d, b, b.tau + h->cur * nkg, h->nan_dev, s);   // sentinel, read at the next sync point
+    HIPC(h, hipGetLastError());
+    HIPC(h, hipMemcpyAsync(h->nan_host, h->nan_dev, sizeof(int), hipMemcpyDeviceToHost, s));
     if (h->prof) collect_prof(h);
     return DCFM_OK;
 }
@@ -1118,45 +1230,98 @@ int dcfm_synchronize(dcfm_handle *h) {
     HIPC(h, hipStreamSynchronize(h->side));
     HIPC(h, hipStreamSynchronize(h->sdraw));
     HIPC(h, hipStreamSynchronize(h->sasm));
-    return DCFM_OK;
+    return numeric_status(h);
 }
 
 int64_t dcfm_saved_samples(const dcfm_handle *h) { return h ? h->saved : -1; }
 
 int dcfm_get_sigma_cols(dcfm_handle *h, int64_t col0, int64_t ncols, double *out) {
-    if (!h || !out) return fail(h, DCFM_ERR_INVALID, "null argument");
+    if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
     Dims &d = h->d;
+    const int root = 0;
+    if (!out && d.rank == root) return fail(h, DCFM_ERR_INVALID, "null output on the root rank");
     if (col0 < 0 || ncols < 0 || col0 + ncols > d.p)
         return fail(h, DCFM_ERR_INVALID, "columns [%lld, %lld) outside 0..p = %d", (long long)col0,
                     (long long)(col0 + ncols), d.p);
     if (ncols == 0) return DCFM_OK;
     HIPC(h, hipSetDevice(h->cfg.device));
     sync_all(h);
-    const size_t n = (size_t)ncols * d.p;
+    if (int rc = numeric_status(h)) return rc;
+    const int nr = d.nranks;
+    const long long p = d.p, c0 = col0, c1 = col0 + ncols;
+    // every rank's packed-window count for this stripe (known to all ranks: no size exchange)
+    std::vector<long long> cnt(nr), base(nr);
+    long long tot = 0;
+    for (int k = 0; k < nr; ++k) {
+        const long long R0 = std::min<long long>(p, (long long)h->Tb[k] * ASM_TILE);
+        const long long R1 = std::min<long long>(p, (long long)h->Tb[k + 1] * ASM_TILE);
+        cnt[k] = win_off(c1, c0, R0, R1);
+        base[k] = tot;
+        tot += cnt[k];
+    }
+    if (tot != p * ncols) return fail(h, DCFM_ERR_INVALID, "sigma_cols: windows cover %lld of %lld", tot, p * ncols);
+    const bool is_root = d.rank == root;
+    // root: [recv (all ranks' windows, own part packed in place) | dense stripe]; others: own windows
+    const size_t ndev = is_root ? (nr > 1 ? 2 * (size_t)tot : (size_t)tot) : (size_t)std::max<long long>(cnt[d.rank], 1);
     void *q = nullptr;
-    HIPC(h, hipMalloc(&q, n * sizeof(double)));
-    double *tmp = static_cast<double *>(q);
+    HIPC(h, hipMalloc(&q, ndev * sizeof(double)));
+    double *buf = static_cast<double *>(q);
+    double *mine = is_root ? buf + base[d.rank] : buf;
     int rc = DCFM_OK;
-    launch_sigma_cols(h->b.Sigma, d.p, (int)col0, (int)ncols, tmp, h->stream);
+    launch_sigma_pack(h->b.Sigma, d.p, h->b.T0, h->b.T1, (int)col0, (int)ncols, mine, h->stream);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "sigma_cols: %s", hipGetErrorString(e));
-    if (rc == DCFM_OK && d.nranks > 1)   // each element is owned by exactly one rank: the sum is exact
-        rc = coll_allreduce_sum(h, CH_ASM, tmp, n, h->stream);
-    if (rc == DCFM_OK) {
-        e = hipMemcpyAsync(out, tmp, n * sizeof(double), hipMemcpyDeviceToHost, h->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "sigma_pack: %s", hipGetErrorString(e));
+    double *dense = buf;   // one rank: its windows are the dense stripe
+    if (rc == DCFM_OK && nr > 1) {
+        rc = coll_gather(h, mine, buf, base, cnt, root, h->stream);
+        if (rc == DCFM_OK && is_root) {
+            dense = buf + tot;
+            void *qt = nullptr;
+            e = hipMalloc(&qt, (size_t)nr * sizeof(long long) + (size_t)(nr + 1) * sizeof(int));
+            if (e == hipSuccess) {
+                long long *dbase = static_cast<long long *>(qt);
+                int *dTb = reinterpret_cast<int *>(dbase + nr);
+                e = hipMemcpyAsync(dbase, base.data(), nr * sizeof(long long), hipMemcpyHostToDevice, h->stream);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(dTb, h->Tb.data(), (nr + 1) * sizeof(int), hipMemcpyHostToDevice, h->stream);
+                if (e == hipSuccess) {
+                    launch_sigma_unpack(buf, d.p, (int)col0, (int)ncols, dTb, dbase, nr, dense, h->stream);
+                    e = hipGetLastError();
+                }
+                if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+                (void)hipFree(qt);
+            }
+            if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "sigma_unpack: %s", hipGetErrorString(e));
+        }
+    }
+    if (rc == DCFM_OK && is_root) {
+        e = hipMemcpyAsync(out, dense, (size_t)tot * sizeof(double), hipMemcpyDeviceToHost, h->stream);
         if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "get_sigma_cols: %s", hipGetErrorString(e));
     }
-    (void)hipFree(tmp);
+    if (rc == DCFM_OK) {
+        e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) rc = fail(h, DCFM_ERR_HIP, "get_sigma_cols: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(buf);
     return rc;
 }
 
-int dcfm_get_sigma(dcfm_handle *h, double *out) {
-    if (!h || !out) return fail(h, DCFM_ERR_INVALID, "null argument");
+int dcfm_sigma_block(const dcfm_handle *h, int64_t out[3]) {
+    if (!h || !out) return fail(nullptr, DCFM_ERR_INVALID, "null argument");
     const int64_t p = h->d.p;
-    const int64_t chunk = std::max<int64_t>(32, std::min<int64_t>(p, ((int64_t)1 << 29) / p));   // <= 4 GiB stripes
+    out[0] = std::min<int64_t>(p, (int64_t)h->b.T0 * ASM_TILE);
+    out[1] = std::min<int64_t>(p, (int64_t)h->b.T1 * ASM_TILE);
+    out[2] = (int64_t)(tri(h->b.T1) - tri(h->b.T0)) * ASM_TILE * ASM_TILE * (int64_t)sizeof(double);
+    return DCFM_OK;
+}
+
+int dcfm_get_sigma(dcfm_handle *h, double *out) {
+    if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
+    if (!out && h->d.rank == 0) return fail(h, DCFM_ERR_INVALID, "null output on the root rank");
+    const int64_t p = h->d.p;
+    const int64_t chunk = std::max<int64_t>(32, std::min<int64_t>(p, ((int64_t)1 << 28) / p));   // <= 2 GiB stripes
     for (int64_t c = 0; c < p; c += chunk) {
-        const int rc = dcfm_get_sigma_cols(h, c, std::min(chunk, p - c), out + (size_t)c * p);
+        const int rc = dcfm_get_sigma_cols(h, c, std::min(chunk, p - c), out ? out + (size_t)c * p : nullptr);
         if (rc) return rc;
     }
     return DCFM_OK;
@@ -1237,7 +1402,7 @@ int dcfm_sigma_error(dcfm_handle *h, const double *U, int32_t r, const double *s
         if (rc) return false;
         if (vh && !hip_ok(hipMemcpyAsync(dv, vh, P * sizeof(double), hipMemcpyHostToDevice, h->stream), "upload v"))
             return false;
-        launch_sigma_err(h->b.Sigma, p, dU, r, ds, vh ? dv : nullptr, d.rank, d.nranks, first, vh ? py : nullptr,
+        launch_sigma_err(h->b.Sigma, p, dU, r, ds, vh ? dv : nullptr, h->b.T0, h->b.T1, first, vh ? py : nullptr,
                          pfro, ptru, dy, h->stream);
         if (!hip_ok(hipGetLastError(), "launch")) return false;
         if (d.nranks > 1) {

@@ -21,7 +21,10 @@
 //   sloc   [G][KW], sall [g][KW]  column sums (all-gathered)
 //   Lb     [2][p][LDB]   saved Lambda rows of an assembly batch (double-buffered), sample s at cols s*K..
 //   wsum   [2][p]        sum of saved omega of the batch
-//   Sigma  [p][p]        lower triangle accumulated (each rank: its tiles), mirrored on get
+//   Sigma  [ntiles][128][128]  this rank's block of the lower triangle of Sigmaout, tile-packed:
+//                        rank r owns the contiguous tile rows [T0, T1) (balanced by tile count,
+//                        sigma_split), tile (ti, tj), tj <= ti, at index tri(ti) - tri(T0) + tj,
+//                        row-major inside (a % 128, b % 128); ~p^2 / (2 nranks) doubles per rank
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -66,7 +69,28 @@ struct Bufs {
     double *msg_all;                   // packed gather target (fused, nranks > 1), else null
     int2 *tiles;
     int ntiles, LDB;
+    int T0, T1;                        // owned tile rows of Sigma (block-sharded, see above)
 };
+
+// Sigma block-sharding helpers (host + device)
+__host__ __device__ inline long long tri(long long t) { return t * (t + 1) / 2; }
+// offset of the stored element (a, b), a >= b, in a rank's tile-packed Sigma (owner of tile row a/128)
+__host__ __device__ inline size_t sig_off(int a, int b, int T0) {
+    const int ta = a / ASM_TILE, tb = b / ASM_TILE;
+    return ((size_t)(tri(ta) - tri(T0) + tb) * ASM_TILE + (a % ASM_TILE)) * ASM_TILE + (b % ASM_TILE);
+}
+// Packed window of a rank owning rows [R0, R1) in a column stripe: column c holds the rows
+// [lo(c), R1) of Sigmaout(:, c) it owns (lo = 0 for c in [R0, R1): the upper part mirrored from
+// its own rows; lo = R0 for c < R0; nothing for c >= R1).  off(c) = start of column c in the
+// rank's packed stripe [c0, ...).
+__host__ __device__ inline long long win_lo(long long c, long long R0, long long R1) {
+    return (c >= R0 && c < R1) ? 0 : (c < R0 ? R0 : R1);
+}
+__host__ __device__ inline long long win_off(long long c, long long c0, long long R0, long long R1) {
+    const long long na = (c < R0 ? c : R0) - c0;                 // columns of [c0, c) below R0
+    const long long b0 = c0 > R0 ? c0 : R0, b1 = c < R1 ? c : R1;  // columns of [c0, c) in [R0, R1)
+    return (na > 0 ? na : 0) * (R1 - R0) + (b1 > b0 ? b1 - b0 : 0) * R1;
+}
 
 // launchers (kernels.hip)
 void launch_prep(const Dims &d, const Bufs &b, hipStream_t s);
@@ -94,13 +118,19 @@ void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
 void launch_save(const Dims &d, const Bufs &b, double *Lb, double *wsum, int slot, hipStream_t s);
 void launch_assemble(const Dims &d, const Bufs &b, const double *Lb, const double *wsum, int kext,
                      double inv_eff, hipStream_t s);
-void launch_sigma_cols(const double *S, int p, int c0, int nc, double *out, hipStream_t s);
+// column stripe [c0, c0 + nc) of Sigmaout from a rank's tile-packed block (tile rows [T0, T1)):
+// the rank's packed windows (win_lo / win_off; with one rank = the dense p x nc stripe)
+void launch_sigma_pack(const double *S, int p, int T0, int T1, int c0, int nc, double *out, hipStream_t s);
+// root of the gather: the dense p x nc stripe from every rank's packed windows, rank k's at
+// recv + base[k]; Tb[0..nranks] are the ranks' tile-row boundaries (device arrays)
+void launch_sigma_unpack(const double *recv, int p, int c0, int nc, const int *Tb, const long long *base,
+                         int nranks, double *out, hipStream_t s);
 void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s);
 // sigma_err.hip: rows' sums of (Sigmaout - U U' - diag s) v, squares and truth squares
 // (partials [splits][p] in y / fro / tru; summed into out[0..p), out[p..2p), out[2p..3p))
 int sigma_err_splits(int p);
 void launch_sigma_err(const double *S, int p, const double *U, int R, const double *sdiag, const double *v,
-                      int rank, int nranks, bool first, double *y, double *fro, double *tru, double *out,
+                      int T0, int T1, bool first, double *y, double *fro, double *tru, double *out,
                       hipStream_t s);
 // ingest.hip: dc:31-34 column nnz counts; dc:50-59 partition + standardise into Y / yy
 void launch_nnz_cols(const double *Y, int n, long long p, int *nnz, hipStream_t s);
@@ -111,6 +141,8 @@ void launch_trace(const Dims &d, const Bufs &b, const double *tau_cur, double *p
 // init.hip: dc:68-87 initial state from Philox (iteration-0 counters), delta/tau buffer 0
 void launch_init_state(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s);
+// NaN / Inf sentinel over the state (sets *flag = 1 if any value is non-finite)
+void launch_finite(const Dims &d, const Bufs &b, const double *tau_cur, int *flag, hipStream_t s);
 // dst[i] = sum_k src[k * count + i] in slice order (loopback all-reduce)
 void launch_sum_slices(const double *src, int ns, size_t count, double *dst, hipStream_t s);
 void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,

@@ -1138,7 +1138,9 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
                                                      double *__restrict__ Sig) {
     __shared__ double As[2][AKC][ALD], Bs[2][AKC][ALD];
     __shared__ int shard_of[2][ASM_TILE];      // shard of the tile's rows / columns (epilogue coef)
-    const int2 T = tiles[xcd_remap(blockIdx.x, gridDim.x)];
+    const int tix = xcd_remap(blockIdx.x, gridDim.x);   // = the tile's index in the packed block
+    const int2 T = tiles[tix];
+    double *__restrict__ St = Sig + (size_t)tix * ASM_TILE * ASM_TILE;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     shard_of[t >> 7][t & 127] = ((t < ASM_TILE ? T.x : T.y) * ASM_TILE + (t & 127)) / d.P;
     const int r = lane & 15, q = lane >> 4;
@@ -1195,8 +1197,8 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
         if (more) lstore(buf ^ 1);
         __syncthreads();
     }
-    // epilogue: lower-triangle read-modify-write of the tile, loads issued together
-    // (predicated, no branches around them), shard test from the LDS table
+    // epilogue: lower-triangle read-modify-write of the tile (tile-packed, row-major inside),
+    // loads issued together (predicated, no branches around them), shard test from the LDS table
     const int a0 = T.x * ASM_TILE + wa, b0 = T.y * ASM_TILE + wb;
     int sb[4];
 #pragma unroll
@@ -1211,7 +1213,7 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
             for (int v = 0; v < 4; ++v) {
                 const int b = b0 + 16 * v + r;
                 const bool live = a < p && b <= a;
-                old[g][v] = live ? Sig[(size_t)a * p + b] : 0.0;
+                old[g][v] = live ? St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r] : 0.0;
             }
         }
 #pragma unroll
@@ -1226,21 +1228,23 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
                     const double coef = (sb[v] == sa) ? 1.0 : d.rho;
                     double val = coef * acc[u][v][g] * inv_eff;
                     if (a == b) val += dg;
-                    Sig[(size_t)a * p + b] = old[g][v] + val;
+                    St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r] = old[g][v] + val;
                 }
             }
         }
     }
 }
 
-// Column stripe of the symmetric Sigmaout from the lower-triangle accumulator:
-// out[(c - c0) * p + r] = Sigma(r, c) for c in [c0, c0 + nc) — i.e. columns c0.. of
-// the MATLAB column-major p x p array, contiguous (dc:194-195 output, Q9: the
-// symmetrisation is this mirror).  32x32 tiles: Sigma(r, c) = S[r][c] for r >= c
-// (read along c, transposed through LDS), S[c][r] for r < c (read along r).
-__global__ __launch_bounds__(256) void k_sigma_cols(const double *__restrict__ S, int p, int c0, int nc,
-                                                    double *__restrict__ out) {
+// Column stripe [c0, c0 + nc) of the symmetric Sigmaout from this rank's tile-packed block
+// of the lower triangle (tile rows [T0, T1), rows [R0, R1)), written as the rank's packed
+// windows: column c holds rows [win_lo(c), R1) at out + win_off(c) (dc:194-195 output, Q9:
+// the symmetrisation is this mirror).  One rank owns everything: the windows are then the
+// dense p x nc column-major stripe.  32x32 tiles: Sigma(r, c) = S(r, c) for r >= c (read
+// along c, transposed through LDS), S(c, r) for r < c (read along r).
+__global__ __launch_bounds__(256) void k_sigma_pack(const double *__restrict__ S, int p, int T0, int T1, int c0,
+                                                    int nc, double *__restrict__ out) {
     __shared__ double lo[32][33];
+    const int R0 = min(p, T0 * ASM_TILE), R1 = min(p, T1 * ASM_TILE);
     const int r0 = blockIdx.x * 32, cb = c0 + blockIdx.y * 32;
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
     const bool need_lo = r0 + 31 >= cb;            // some r >= c in the tile
@@ -1248,15 +1252,33 @@ __global__ __launch_bounds__(256) void k_sigma_cols(const double *__restrict__ S
     if (need_lo) {
         for (int yy = ty; yy < 32; yy += 8) {      // rows r = r0 + yy, columns c = cb + tx
             const int r = r0 + yy, c = cb + tx;
-            lo[yy][tx] = (r < p && c < c0 + nc && r >= c) ? S[(size_t)r * p + c] : 0.0;
+            lo[yy][tx] = (r >= R0 && r < R1 && c < c0 + nc && r >= c) ? S[sig_off(r, c, T0)] : 0.0;
         }
     }
     __syncthreads();
     for (int yy = ty; yy < 32; yy += 8) {          // output column c = cb + yy, rows r = r0 + tx
         const int c = cb + yy, r = r0 + tx;
-        if (c >= c0 + nc || r >= p) continue;
-        const double v = (r >= c) ? lo[tx][yy] : (need_up ? S[(size_t)c * p + r] : 0.0);
-        out[(size_t)(c - c0) * p + r] = v;
+        if (c >= c0 + nc || r >= R1) continue;
+        const long long wl = win_lo(c, R0, R1);
+        if (r < wl) continue;
+        const double v = (r >= c) ? lo[tx][yy] : (need_up ? S[sig_off(c, r, T0)] : 0.0);
+        out[win_off(c, c0, R0, R1) + (r - wl)] = v;
+    }
+}
+
+// Root of the striped gather: out (dense p x nc, column-major) from the ranks' packed
+// windows.  Element (r, c) lives on the owner of tile row max(r, c) / 128.
+__global__ __launch_bounds__(256) void k_sigma_unpack(const double *__restrict__ recv, int p, int c0, int cbeg,
+                                                      const int *__restrict__ Tb,
+                                                      const long long *__restrict__ base, int nranks,
+                                                      double *__restrict__ out) {
+    const int c = cbeg + blockIdx.y;
+    for (int r = blockIdx.x * 256 + threadIdx.x; r < p; r += gridDim.x * 256) {
+        const int t = max(r, c) / ASM_TILE;
+        int k = 0;
+        while (k + 1 < nranks && Tb[k + 1] <= t) ++k;
+        const long long R0 = min(p, Tb[k] * ASM_TILE), R1 = min(p, Tb[k + 1] * ASM_TILE);
+        out[(size_t)(c - c0) * p + r] = recv[base[k] + win_off(c, c0, R0, R1) + (r - win_lo(c, R0, R1))];
     }
 }
 
@@ -1501,9 +1523,18 @@ void launch_assemble(const Dims &d, const Bufs &b, const double *Lb, const doubl
     hipLaunchKernelGGL(k_assemble, dim3(b.ntiles), dim3(256), 0, s, d, Lb, b.LDB, kext, wsum, inv_eff,
                        b.tiles, b.Sigma);
 }
-void launch_sigma_cols(const double *S, int p, int c0, int nc, double *out, hipStream_t s) {
-    if (nc <= 0) return;
-    hipLaunchKernelGGL(k_sigma_cols, dim3(cdiv(p, 32), cdiv(nc, 32)), dim3(256), 0, s, S, p, c0, nc, out);
+void launch_sigma_pack(const double *S, int p, int T0, int T1, int c0, int nc, double *out, hipStream_t s) {
+    const int R1 = std::min(p, T1 * ASM_TILE);
+    if (nc <= 0 || R1 <= 0 || T1 <= T0) return;
+    hipLaunchKernelGGL(k_sigma_pack, dim3(cdiv(R1, 32), cdiv(nc, 32)), dim3(256), 0, s, S, p, T0, T1, c0, nc, out);
+}
+void launch_sigma_unpack(const double *recv, int p, int c0, int nc, const int *Tb, const long long *base,
+                         int nranks, double *out, hipStream_t s) {
+    for (int j = 0; j < nc; j += 32768) {   // grid.y <= 32768 columns per launch
+        const int w = std::min(32768, nc - j);
+        hipLaunchKernelGGL(k_sigma_unpack, dim3(std::min(cdiv(p, 256), 16), w), dim3(256), 0, s, recv, p, c0, c0 + j,
+                           Tb, base, nranks, out);
+    }
 }
 void launch_eta(const Dims &d, const Bufs &b, double *eta_out, hipStream_t s) {
     const size_t total = (size_t)d.G * d.NP * d.kp;
@@ -1515,6 +1546,29 @@ void launch_draws(const Dims &d, const DrawsDev &dr, int64_t iter, hipStream_t s
     hipLaunchKernelGGL(k_draws<true>, dim3(pl.b_gpsi), dim3(256), 0, s, d, dr, iter);
     hipLaunchKernelGGL(k_draws<false>, dim3(pl.total - pl.b_gpsi), dim3(256), 0, s, d, dr, iter);
 }
+// NaN / Inf sentinel (DCFM_ERR_NUMERIC): after a dcfm_run, every non-finite value of the
+// state a later iteration reads (Lambda, ps, omega, X, tau) sets *flag (sticky until the
+// next set_state / init_state).  A NaN anywhere in a sweep reaches these within one
+// iteration (SS_j -> ps_j -> omega_j; X -> eta -> Lambda).  One pass over ~6 MB at c3.
+__device__ __forceinline__ bool bad(double v) { return !(fabs(v) <= 1.7976931348623157e308); }
+__global__ __launch_bounds__(256) void k_finite(Dims d, const double *__restrict__ Lam,
+                                                const double *__restrict__ ps, const double *__restrict__ omega,
+                                                const double *__restrict__ X, const double *__restrict__ tau,
+                                                int *__restrict__ flag) {
+    const size_t nL = (size_t)d.G * d.PP * d.kp, nP = (size_t)d.G * d.PP, nX = (size_t)d.NP * d.kp,
+                 nT = (size_t)d.g * d.kp;
+    bool any = false;
+    for (size_t e = blockIdx.x * (size_t)256 + threadIdx.x; e < nL; e += (size_t)gridDim.x * 256) any |= bad(Lam[e]);
+    for (size_t e = blockIdx.x * (size_t)256 + threadIdx.x; e < nP; e += (size_t)gridDim.x * 256)
+        any |= bad(ps[e]) || bad(omega[e]);
+    for (size_t e = blockIdx.x * (size_t)256 + threadIdx.x; e < nX; e += (size_t)gridDim.x * 256) any |= bad(X[e]);
+    for (size_t e = blockIdx.x * (size_t)256 + threadIdx.x; e < nT; e += (size_t)gridDim.x * 256) any |= bad(tau[e]);
+    if (any) *flag = 1;   // benign race: every writer stores 1
+}
+void launch_finite(const Dims &d, const Bufs &b, const double *tau_cur, int *flag, hipStream_t s) {
+    hipLaunchKernelGGL(k_finite, dim3(128), dim3(256), 0, s, d, b.Lam, b.ps, b.omega, b.X, tau_cur, flag);
+}
+
 __global__ __launch_bounds__(256) void k_sum_slices(const double *__restrict__ src, int ns, size_t count,
                                                    double *__restrict__ dst) {
     for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < count; i += (size_t)gridDim.x * 256) {

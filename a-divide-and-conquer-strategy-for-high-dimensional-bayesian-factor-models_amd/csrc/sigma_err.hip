@@ -15,10 +15,10 @@
 // and sum_c Sigma0_rc^2 (Frobenius norms).  Every block writes its rows' sums; the
 // host adds rows in a fixed order, so results are deterministic.
 //
-// Several ranks: each lower-triangle element of the accumulator lives on the rank that
-// owns its 128 x 128 assembly tile (dealt round-robin, dcfm_create), zero elsewhere.  A
-// rank counts only the elements it owns — S minus truth, both — so the per-rank sums
-// and matvecs add up exactly to those of the full matrix.
+// Several ranks: the accumulator is block-sharded (dcfm_internal.h): rank r holds the
+// tile rows [T0, T1) of the lower triangle, tile-packed.  A rank counts only the elements
+// it owns — S minus truth, both — so the per-rank sums and matvecs add up exactly to those
+// of the full matrix.
 //
 // Roofline: HBM-bound, 8 p^2 bytes per pass (the full matrix, both halves of the
 // stored triangle); U / s / v are L2-resident.
@@ -36,18 +36,17 @@ constexpr int ERR_RMAX = 32;
 #endif
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-// stored element (a, b), a >= b: does this rank own it (its 128 x 128 assembly tile)?
-__device__ __forceinline__ bool owns(int a, int b, int rank, int nranks) {
-    if (nranks <= 1) return true;
-    const long long ta = a / ASM_TILE, tb = b / ASM_TILE;
-    return ((ta * (ta + 1) / 2 + tb) % nranks) == rank;
+// stored element (a, b), a >= b: does this rank own it (tile row a / 128 in [T0, T1))?
+__device__ __forceinline__ bool owns(int a, int T0, int T1) {
+    const int ta = a / ASM_TILE;
+    return ta >= T0 && ta < T1;
 }
 
 template <int RM>
 __global__ __launch_bounds__(256) void k_sigma_err(const double *__restrict__ S, int p,
                                                    const double *__restrict__ U, int R,
                                                    const double *__restrict__ sdiag,
-                                                   const double *__restrict__ v, int rank, int nranks,
+                                                   const double *__restrict__ v, int T0, int T1,
                                                    int first, double *__restrict__ y,
                                                    double *__restrict__ fro, double *__restrict__ tru) {
     constexpr int NT = ERR_NT;
@@ -91,9 +90,9 @@ __global__ __launch_bounds__(256) void k_sigma_err(const double *__restrict__ S,
                 if (c0 < r0) { a = r0 + yy; b = c0 + tx; ok = true; }
                 else if (c0 > r0) { a = c0 + yy; b = r0 + tx; ok = true; }
                 else { a = r0 + yy; b = r0 + tx; ok = tx <= yy; }
-                ok = ok && live && a < p && b < p && owns(a, b, rank, nranks);
+                ok = ok && live && a < p && b < p && owns(a, T0, T1);
                 ok_[u][i] = ok;
-                sv_[u][i] = ok ? S[(size_t)a * p + b] : 0.0;
+                sv_[u][i] = ok ? S[sig_off(a, b, T0)] : 0.0;
             }
 #pragma unroll
             for (int i = 0; i < RM / 8; ++i) {
@@ -197,15 +196,15 @@ int sigma_err_splits(int p) {
 }
 // y / fro / tru: [splits][p] partials; work: 3 x p outputs (y, fro, tru summed over splits)
 void launch_sigma_err(const double *S, int p, const double *U, int R, const double *sdiag, const double *v,
-                      int rank, int nranks, bool first, double *y, double *fro, double *tru, double *out,
+                      int T0, int T1, bool first, double *y, double *fro, double *tru, double *out,
                       hipStream_t s) {
     const int ns = sigma_err_splits(p);
     if (R <= 16)
-        hipLaunchKernelGGL(k_sigma_err<16>, dim3(cdiv(p, 32), ns), dim3(256), 0, s, S, p, U, R, sdiag, v, rank,
-                           nranks, first ? 1 : 0, y, fro, tru);
+        hipLaunchKernelGGL(k_sigma_err<16>, dim3(cdiv(p, 32), ns), dim3(256), 0, s, S, p, U, R, sdiag, v, T0,
+                           T1, first ? 1 : 0, y, fro, tru);
     else
         hipLaunchKernelGGL(k_sigma_err<ERR_RMAX>, dim3(cdiv(p, 32), ns), dim3(256), 0, s, S, p, U, R, sdiag, v,
-                           rank, nranks, first ? 1 : 0, y, fro, tru);
+                           T0, T1, first ? 1 : 0, y, fro, tru);
     if (y) hipLaunchKernelGGL(k_sigma_err_sum, dim3(cdiv(p, 256)), dim3(256), 0, s, y, ns, p, out);
     if (first) {
         hipLaunchKernelGGL(k_sigma_err_sum, dim3(cdiv(p, 256)), dim3(256), 0, s, fro, ns, p, out + p);

@@ -181,18 +181,34 @@ class Sampler:
         self._check(self.lib.dcfm_get_state(self.h, C.byref(view)))
         return out
 
-    def get_sigma(self) -> np.ndarray:
+    def get_sigma(self):
+        """Sigmaout (p x p, Fortran order).  Collective when nranks > 1: every rank calls it,
+        rank 0 receives the matrix and the other ranks get None (Sigmaout is block-sharded
+        over the ranks, dcfm_sigma_block; each element moves once, owner -> rank 0)."""
         p = self.P * self.g
+        if self.rank != 0:
+            self._check(self.lib.dcfm_get_sigma(self.h, None))
+            return None
         S = np.zeros((p, p), dtype=np.float64, order="F")
         self._check(self.lib.dcfm_get_sigma(self.h, _ptr(S)))
         return S
 
-    def get_sigma_cols(self, col0: int, ncols: int) -> np.ndarray:
-        """Sigmaout(:, col0 : col0+ncols) as a p x ncols Fortran array (collective if nranks > 1)."""
+    def get_sigma_cols(self, col0: int, ncols: int):
+        """Sigmaout(:, col0 : col0+ncols) as a p x ncols Fortran array (collective if nranks > 1;
+        rank 0 receives it, other ranks get None)."""
         p = self.P * self.g
+        if self.rank != 0:
+            self._check(self.lib.dcfm_get_sigma_cols(self.h, int(col0), int(ncols), None))
+            return None
         S = np.zeros((p, int(ncols)), dtype=np.float64, order="F")
         self._check(self.lib.dcfm_get_sigma_cols(self.h, int(col0), int(ncols), _ptr(S)))
         return S
+
+    def sigma_block(self) -> dict:
+        """This rank's block of Sigmaout: rows [row0, row1) of the lower triangle and its bytes."""
+        out = (C.c_int64 * 3)()
+        self._check(self.lib.dcfm_sigma_block(self.h, out))
+        return {"row0": int(out[0]), "row1": int(out[1]), "bytes": int(out[2])}
 
     def sigma_error(self, U, s, iters: int = 60, seed: int = 1) -> dict:
         """Frobenius / operator-norm error of Sigmaout against U U' + diag(s), on the device

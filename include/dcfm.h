@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DCFM_ABI_VERSION 1
+#define DCFM_ABI_VERSION 2
 
 /* status codes */
 #define DCFM_OK              0
@@ -156,13 +156,22 @@ int  dcfm_synchronize(dcfm_handle *h);
 int  dcfm_get_state(dcfm_handle *h, dcfm_state_view *out);
 /* Sigmaout, p x p (p = P*g), symmetric, in the reference's permuted and
  * standardised coordinates (dc:186-195, quirk Q7).  Collective when
- * nranks > 1: every rank must call it; every rank receives the full matrix. */
+ * nranks > 1: every rank must call it; rank 0 receives the matrix (out may be
+ * NULL on the other ranks and is not written there).  Sigmaout is block-sharded
+ * over the ranks (dcfm_sigma_block): the read-out moves each element once, from
+ * its owner to rank 0 (RCCL send/recv), in column stripes of <= 2 GiB. */
 int  dcfm_get_sigma(dcfm_handle *h, double *out);
 /* Columns col0 .. col0+ncols-1 of Sigmaout: p x ncols column-major, i.e. exactly
  * out = Sigmaout(:, col0+1 : col0+ncols) — a contiguous chunk of the MATLAB array,
  * so a caller can fill a p x p result stripe by stripe (config c5: 80 GB) with
- * device scratch of only p x ncols.  Collective when nranks > 1. */
+ * device scratch of only p x ncols.  Collective when nranks > 1; the stripe goes
+ * to rank 0 only (as dcfm_get_sigma). */
 int  dcfm_get_sigma_cols(dcfm_handle *h, int64_t col0, int64_t ncols, double *out);
+/* This rank's block of Sigmaout (the build's output sharding; the reference holds
+ * the whole p x p, dc:42): out[0], out[1] = the rows [row0, row1) whose lower
+ * triangle it accumulates (contiguous 128-row tiles, balanced by tile count over
+ * the ranks), out[2] = its device bytes for Sigmaout (~p^2 / (2 nranks) * 8). */
+int  dcfm_sigma_block(const dcfm_handle *h, int64_t out[3]);
 int64_t dcfm_saved_samples(const dcfm_handle *h);
 /* Error of Sigmaout against a truth Sigma0 = U U' + diag(s) given in the same permuted,
  * standardised coordinates (U: p x r column-major, r <= 32; s: p), computed on the

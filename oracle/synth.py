@@ -20,8 +20,9 @@ DATA_SEED = 20161209
 
 
 def make_data(n: int, p: int, k0: int = 10, sparsity: float = 0.7, seed: int = DATA_SEED,
-              zero_cols: int = 0, factors: bool = False):
-    """Y (n x p) and Sigma0; with ``factors`` also (Lambda0, sigma0^2) of Sigma0."""
+              zero_cols: int = 0, factors: bool = False, dense_truth: bool = True):
+    """Y (n x p) and Sigma0; with ``factors`` also (Lambda0, sigma0^2) of Sigma0.
+    ``dense_truth=False`` returns None for Sigma0 (p x p: 3.2 GB at p = 20k)."""
     r = np.random.Generator(np.random.PCG64(seed))
     Lam0 = r.standard_normal((p, k0))
     Lam0[r.random((p, k0)) < sparsity] = 0.0
@@ -29,7 +30,7 @@ def make_data(n: int, p: int, k0: int = 10, sparsity: float = 0.7, seed: int = D
     F = r.standard_normal((n, k0))
     E = r.standard_normal((n, p)) * np.sqrt(sig2)[None, :]
     Y = F @ Lam0.T + E
-    Sigma0 = Lam0 @ Lam0.T + np.diag(sig2)
+    Sigma0 = Lam0 @ Lam0.T + np.diag(sig2) if dense_truth else None
     if zero_cols:
         cols = r.choice(p, size=zero_cols, replace=False)
         Y[:, cols] = 0.0

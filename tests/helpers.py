@@ -16,8 +16,8 @@ def rel_err(a, b):
     return float(np.max(np.abs(a - b))) / max(den, 1e-300)
 
 
-def make_case(n, p, g, K, *, rho=0.5, seed=3, k0=4, zero_cols=0):
-    Y, Sigma0 = oracle.synth.make_data(n, p, k0=k0, zero_cols=zero_cols)
+def make_case(n, p, g, K, *, rho=0.5, seed=3, k0=4, zero_cols=0, dense_truth=True):
+    Y, Sigma0 = oracle.synth.make_data(n, p, k0=k0, zero_cols=zero_cols, dense_truth=dense_truth)
     hyper = F.Hyper()
     Yk, n, pk, P, K_, keep = F.preprocess(Y, g, K * g)
     src = oracle.DrawSource(seed, n, pk, g, K, hyper)
@@ -41,3 +41,12 @@ def state_dict(st, s0=0, gl=None):
 def stacked_draws(src, first, n_iter):
     ds = [src.iteration(t) for t in range(first, first + n_iter)]
     return ds[0].stacked(ds[1:])
+
+
+def sigma_stripe_from_lower(SigLower, c0, c1):
+    """Columns [c0, c1) of the symmetric matrix whose lower triangle is SigLower (p x p)."""
+    lo = SigLower[:, c0:c1]
+    up = SigLower[c0:c1, :].T
+    r = np.arange(SigLower.shape[0])[:, None]
+    c = np.arange(c0, c1)[None, :]
+    return np.where(r >= c, lo, up)

@@ -9,8 +9,11 @@ nranks GPUs and exchanges, per iteration (the fused K <= 32 chain):
      -> replicated delta/tau chain over ALL shards (quirks Q4/Q5, dc:155-165) and the
      next iteration's Xprec (dc:117); before the first iteration the A sums alone
 and per assembly flush an all-gather of the saved Lambda rows and omega, after
-which each rank accumulates its round-robin share of lower-triangle tiles;
-dcfm_get_sigma sums the per-rank accumulators (all-reduce) and mirrors.
+which each rank accumulates its block of Sigmaout: the contiguous tile rows
+[Tb[r], Tb[r+1]) of the lower triangle (``sigma_split``, balanced by tile count).
+dcfm_get_sigma gathers to rank 0: each rank packs, per column of the stripe, the
+rows it owns (``win_lo`` / ``win_off``), sends them point to point, and rank 0
+unpacks — every element moves once, nothing is all-reduced.
 
 This module runs the same decomposition with NumPy on CPU ranks connected by
 torch.distributed (gloo), so tests can check that the decomposition reproduces
@@ -30,6 +33,58 @@ def all_gather_np(x: np.ndarray):
     out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [o.numpy() for o in out]
+
+
+def tri(t):
+    return t * (t + 1) // 2
+
+
+def sigma_split(nt, nranks):
+    """Tile-row boundaries Tb[0..nranks] of the block-sharded Sigmaout (dcfm.hip sigma_split)."""
+    Tb = [0] + [nt] * nranks
+    total = float(tri(nt))
+    for k in range(1, nranks):
+        target = total * k / nranks
+        t = Tb[k - 1]
+        while t < nt and tri(t) < target:
+            t += 1
+        if t > Tb[k - 1] and target - tri(t - 1) < tri(t) - target:
+            t -= 1
+        Tb[k] = t
+    return Tb
+
+
+def win_lo(c, R0, R1):
+    """First owned row of column c for a rank owning rows [R0, R1) (dcfm_internal.h)."""
+    return 0 if R0 <= c < R1 else (R0 if c < R0 else R1)
+
+
+def win_off(c, c0, R0, R1):
+    na = max(min(c, R0) - c0, 0)
+    nb = max(min(c, R1) - max(c0, R0), 0)
+    return na * (R1 - R0) + nb * R1
+
+
+def pack_stripe(SigLower, R0, R1, c0, c1):
+    """This rank's packed windows of the columns [c0, c1) of Sigmaout (k_sigma_pack)."""
+    out = np.zeros(win_off(c1, c0, R0, R1))
+    for c in range(c0, c1):
+        lo = win_lo(c, R0, R1)
+        for r in range(lo, R1):
+            out[win_off(c, c0, R0, R1) + r - lo] = SigLower[r, c] if r >= c else SigLower[c, r]
+    return out
+
+
+def unpack_stripe(parts, Tb, tile, p, c0, c1):
+    """Rank 0: the dense p x (c1 - c0) stripe from every rank's packed windows (k_sigma_unpack)."""
+    out = np.zeros((p, c1 - c0))
+    for c in range(c0, c1):
+        for r in range(p):
+            t = max(r, c) // tile
+            k = max(i for i in range(len(Tb) - 1) if Tb[i] <= t)
+            R0, R1 = min(p, Tb[k] * tile), min(p, Tb[k + 1] * tile)
+            out[r, c - c0] = parts[k][win_off(c, c0, R0, R1) + r - win_lo(c, R0, R1)]
+    return out
 
 
 def chol_upper(A):
@@ -119,18 +174,18 @@ class RankChain:
                 tauh[:, :, m] = np.cumprod(delta[:, :, m], axis=0)
 
     def save_and_assemble(self, SigLower, effsamp, tile=8):
-        """Flush of one saved sample: all-gather Lambda/omega, this rank's tiles (round-robin)."""
+        """Flush of one saved sample: all-gather Lambda/omega, this rank's block of tile rows."""
         st = self.st
         Lloc = np.moveaxis(st["Lambda"], 2, 0).reshape(self.G * self.P, self.K)
         L = np.concatenate(all_gather_np(Lloc), axis=0)                  # exchange 3
         w = np.concatenate(all_gather_np(st["omega"].T.reshape(-1)))
         p = L.shape[0]
         nt = -(-p // tile)
-        idx = 0
         rank, world = dist.get_rank(), dist.get_world_size()
-        for ti in range(nt):
+        Tb = sigma_split(nt, world)
+        for ti in range(Tb[rank], Tb[rank + 1]):
             for tj in range(ti + 1):
-                if idx % world == rank:
+                if True:
                     a = slice(ti * tile, min(p, (ti + 1) * tile))
                     b = slice(tj * tile, min(p, (tj + 1) * tile))
                     blk = L[a] @ L[b].T
@@ -140,5 +195,27 @@ class RankChain:
                     if ti == tj:
                         blk = np.tril(blk) + np.diag(w[a] / effsamp)
                     SigLower[a, b] += blk
-                idx += 1
         return SigLower
+
+    @staticmethod
+    def gather_sigma(SigLower, tile=8, stripe=16):
+        """dcfm_get_sigma: stripes of packed windows, point to point to rank 0 (gloo gather)."""
+        p = SigLower.shape[0]
+        rank, world = dist.get_rank(), dist.get_world_size()
+        Tb = sigma_split(-(-p // tile), world)
+        R0, R1 = min(p, Tb[rank] * tile), min(p, Tb[rank + 1] * tile)
+        full = np.zeros((p, p)) if rank == 0 else None
+        for c0 in range(0, p, stripe):
+            c1 = min(p, c0 + stripe)
+            mine = torch.from_numpy(pack_stripe(SigLower, R0, R1, c0, c1))
+            cnts = [win_off(c1, c0, min(p, Tb[k] * tile), min(p, Tb[k + 1] * tile)) for k in range(world)]
+            if rank == 0:
+                bufs = [torch.empty(n_, dtype=torch.float64) for n_ in cnts]
+                bufs[0] = mine
+                for k in range(1, world):
+                    if cnts[k]:
+                        dist.recv(bufs[k], src=k)
+                full[:, c0:c1] = unpack_stripe([b_.numpy() for b_ in bufs], Tb, tile, p, c0, c1)
+            elif cnts[rank]:
+                dist.send(mine, dst=0)
+        return full

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(dcfm):
     assert declared == set(dcfm.EXPORTS), declared ^ set(dcfm.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.dcfm_abi_version() == 1
+    assert lib.dcfm_abi_version() == 2
 
 
 def test_struct_layout_matches_c(dcfm, tmp_path):
@@ -56,7 +56,8 @@ def _create(dcfm, **kw):
     from dcfm_amd import _abi
     lib = dcfm.load_library()
     cfg = _abi.DcfmConfig()
-    base = dict(n=10, P=4, g=2, K=2, rho=0.5, burnin=0, mcmc=2, thin=1, nranks=1, rank=0, device=0)
+    base = dict(n=10, P=4, g=2, K=2, rho=0.5, burnin=0, mcmc=2, thin=1, nranks=1, rank=0, device=0,
+                as_=1.0, bs=0.3, df=3.0, ad1=2.0, bd1=1.0, ad2=2.0, bd2=1.0)
     base.update(kw)
     for k, v in base.items():
         setattr(cfg, k, v)
@@ -75,6 +76,12 @@ def test_create_validates_before_touching_a_device(dcfm):
     assert _create(dcfm, rho=1.5)[0] == _abi.DCFM_ERR_INVALID
     assert _create(dcfm, thin=0)[0] == _abi.DCFM_ERR_INVALID
     assert _create(dcfm, n=0)[0] == _abi.DCFM_ERR_INVALID
+    assert _create(dcfm, bs=0.0)[0] == _abi.DCFM_ERR_INVALID
+    # on-device gamma needs shape >= 1 (no shape < 1 boost): rejected unless draws are injected
+    assert _create(dcfm, df=1.5)[0] == _abi.DCFM_ERR_UNSUPPORTED
+    assert _create(dcfm, as_=0.5)[0] == _abi.DCFM_ERR_UNSUPPORTED
+    assert _create(dcfm, ad2=0.9)[0] == _abi.DCFM_ERR_UNSUPPORTED
+    assert _create(dcfm, ad1=0.5, flags=_abi.DCFM_FLAG_INJECT_DRAWS)[0] != _abi.DCFM_ERR_UNSUPPORTED
 
 
 def test_create_without_gpu_reports_hip_error(dcfm, gpu_available):

@@ -55,13 +55,10 @@ def _worker(rank, world, port, outdir):
             rc.iteration(c["src"].iteration(it))
             if it % CASE["thin"] == 0 and it > CASE["burnin"]:
                 rc.save_and_assemble(Sig, effsamp)
-        import torch
-        t = torch.from_numpy(Sig)
-        dist.all_reduce(t)
-        Sig = t.numpy()
-        Sig = np.tril(Sig) + np.tril(Sig, -1).T
-        np.savez(Path(outdir) / f"rank{rank}.npz", Sig=Sig, X=rc.st["X"], delta=rc.st["delta"],
-                 tauh=rc.st["tauh"], Lambda=rc.st["Lambda"], ps=rc.st["ps"])
+        full = RankChain.gather_sigma(Sig)                  # rank 0 only (block-sharded output)
+        extra = {"Sig": full} if rank == 0 else {}
+        np.savez(Path(outdir) / f"rank{rank}.npz", X=rc.st["X"], delta=rc.st["delta"],
+                 tauh=rc.st["tauh"], Lambda=rc.st["Lambda"], ps=rc.st["ps"], Sig_local=Sig, **extra)
     finally:
         dist.destroy_process_group()
 
@@ -80,8 +77,17 @@ def test_two_rank_protocol_matches_single_process(tmp_path):
     r1 = np.load(tmp_path / "rank1.npz")
     rel = lambda a, b: np.max(np.abs(a - b)) / np.max(np.abs(b))
     # replicated quantities identical on both ranks, bit for bit
-    for f in ("Sig", "X", "delta", "tauh"):
+    for f in ("X", "delta", "tauh"):
         assert np.array_equal(r0[f], r1[f]), f
+    # each rank holds only its block of tile rows; the blocks are disjoint and cover Sigmaout
+    from sharded_protocol import sigma_split
+    p = S_ref.shape[0]
+    Tb = sigma_split(-(-p // 8), world)
+    for k, r in enumerate((r0, r1)):
+        rows = np.zeros(p, bool)
+        rows[min(p, Tb[k] * 8):min(p, Tb[k + 1] * 8)] = True
+        assert not np.any(r["Sig_local"][~rows]), f"rank {k} wrote rows it does not own"
+    assert "Sig" not in r1.files
     assert rel(r0["Sig"], S_ref) < 1e-12
     assert rel(r0["X"], st.X) < 1e-12
     assert rel(r0["delta"], st.delta) < 1e-12

@@ -1,11 +1,12 @@
 """The multi-rank sweep on ONE GPU: n handles (ranks 0..n-1) joined by the in-process
 loopback communicator (dcfm_comm_init_loopback), each driven by its own host thread.
 Every collective of the RCCL path (X message and shard sums of A all-gathers, column
-sums for delta, the assembly batch all-gather, the Sigma all-reduce) runs with the same
-call order and semantics, so this is the parity test of the decomposition itself: with
-injected draws the n-rank chain must match the single-process oracle to the 1e-10 bar
-of tests/test_gpu_parity.py, and the replicated quantities (X, delta, tau, Sigmaout)
-must be bitwise identical on all ranks.
+sums for delta, the assembly batch all-gather, the striped gather of the block-sharded
+Sigmaout to rank 0) runs with the same call order and semantics, so this is the parity
+test of the decomposition itself: with injected draws the n-rank chain must match the
+single-process oracle to the 1e-10 bar of tests/test_gpu_parity.py, the replicated
+quantities (X, delta, tau) must be bitwise identical on all ranks, and rank 0's gathered
+Sigmaout must be bitwise the one-rank Sigmaout (same tiles, same arithmetic).
 """
 import threading
 
@@ -14,16 +15,17 @@ import pytest
 
 from helpers import make_case, rel_err, stacked_draws, state_dict
 from oracle import dc_oracle as F
+from oracle import vectorised as V
 
 pytestmark = pytest.mark.gpu
 
 
-def _run_ranks(dcfm, c, g, K, burnin, mcmc, thin, n):
+def _run_ranks(dcfm, c, g, K, burnin, mcmc, thin, n, asm_batch=0):
     N = burnin + mcmc
     G = g // n
     draws = stacked_draws(c["src"], 1, N)
     smps = [dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], burnin, mcmc, thin, inject_draws=True,
-                         nranks=n, rank=r, device=0) for r in range(n)]
+                         nranks=n, rank=r, device=0, asm_batch=asm_batch) for r in range(n)]
     try:
         dcfm.Sampler.comm_loopback(smps)
         for r, smp in enumerate(smps):
@@ -37,7 +39,8 @@ def _run_ranks(dcfm, c, g, K, burnin, mcmc, thin, n):
             try:
                 smps[r].run(1, N)
                 got = smps[r].get_state()
-                got["Sig"] = smps[r].get_sigma()          # collective
+                got["Sig"] = smps[r].get_sigma()          # collective: rank 0 receives
+                got["block"] = smps[r].sigma_block()
                 out[r] = got
             except Exception as e:                        # surfaced below
                 errs.append(e)
@@ -55,6 +58,34 @@ def _run_ranks(dcfm, c, g, K, burnin, mcmc, thin, n):
             smp.close()
 
 
+def _one_rank_sigma(dcfm, c, g, K, burnin, mcmc, thin, asm_batch=0):
+    N = burnin + mcmc
+    smp = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], burnin, mcmc, thin, inject_draws=True,
+                       asm_batch=asm_batch)
+    try:
+        smp.set_data(c["Yd"])
+        smp.set_state({f: v for f, v in state_dict(c["st"]).items() if f != "eta"})
+        smp.set_draws(stacked_draws(c["src"], 1, N), 1, N)
+        smp.run(1, N)
+        return smp.get_sigma()
+    finally:
+        smp.close()
+
+
+def _check_blocks(out, p, n):
+    """Each rank holds only its rows of Sigmaout: disjoint, covering, ~p^2/(2n) doubles."""
+    rows = sorted((o["block"]["row0"], o["block"]["row1"]) for o in out)
+    assert rows[0][0] == 0 and rows[-1][1] == p
+    assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
+    total = sum(o["block"]["bytes"] for o in out)
+    nt = -(-p // 128)
+    assert total == nt * (nt + 1) // 2 * 128 * 128 * 8
+    if nt >= 4 * n:   # enough tile rows to balance
+        assert max(o["block"]["bytes"] for o in out) < 1.5 * total / n
+    for r in range(1, n):
+        assert out[r]["Sig"] is None
+
+
 @pytest.mark.parametrize("n,g,K,nobs,p", [(2, 4, 5, 40, 60), (4, 8, 6, 50, 96), (2, 4, 40, 60, 120)])
 def test_loopback_ranks_match_oracle(dcfm, n, g, K, nobs, p):
     burnin, mcmc, thin = 1, 4, 2
@@ -62,9 +93,41 @@ def test_loopback_ranks_match_oracle(dcfm, n, g, K, nobs, p):
     out, N = _run_ranks(dcfm, c, g, K, burnin, mcmc, thin, n)
     ref = c["st"].copy()
     S_ref = F.run_chain(c["Yd"], ref, c["rho"], c["hyper"], c["src"].iteration, 1, N, burnin, mcmc, thin)
-    for f in ("Sig", "X", "delta", "tauh"):
+    for f in ("X", "delta", "tauh"):
         for r in range(1, n):
             assert np.array_equal(out[0][f], out[r][f]), f"{f} differs between ranks 0 and {r}"
+    _check_blocks(out, c["p"], n)
+    assert np.array_equal(out[0]["Sig"], _one_rank_sigma(dcfm, c, g, K, burnin, mcmc, thin))
+    assert rel_err(out[0]["Sig"], S_ref) < 1e-10
+    for f in ("X", "delta", "tauh"):
+        assert rel_err(out[0][f], getattr(ref, f)) < 1e-10, f
+    for f in ("Lambda", "ps", "omega", "psi", "Plam", "Z", "eta"):
+        both = np.concatenate([out[r][f] for r in range(n)], axis=-1)
+        assert rel_err(both, getattr(ref, f)) < 1e-10, f
+
+
+# c3's shard layout (g = 64, K = 30, 8 shards per rank, as on an 8-GPU node) at a reduced
+# n and P; K = 1 with g >= 3 split over ranks (quirk Q5: cumprod over shards held by
+# different ranks, dc:158); a Sigmaout of several tile rows per rank (p = 2,560: 20 tile
+# rows over 8 ranks) with batched flushes.
+@pytest.mark.parametrize("n,g,K,nobs,P,asm_batch", [
+    (8, 64, 30, 96, 6, 0),          # c3 layout, 8 ranks
+    (4, 8, 1, 40, 9, 0),            # K = 1, g = 8 over 4 ranks (Q5 across ranks)
+    (8, 8, 1, 30, 5, 0),            # K = 1, one shard per rank
+    (8, 64, 4, 40, 40, 3),          # p = 2,560 over 8 ranks, 3-sample flushes
+])
+def test_loopback_eight_ranks(dcfm, n, g, K, nobs, P, asm_batch):
+    burnin, mcmc, thin = 1, 5, 2
+    c = make_case(nobs, P * g, g, K, seed=17)
+    out, N = _run_ranks(dcfm, c, g, K, burnin, mcmc, thin, n, asm_batch=asm_batch)
+    ref = c["st"].copy()
+    S_ref = V.full(V.run_chain(c["Yd"], ref, c["rho"], c["hyper"], c["src"].iteration, 1, N, burnin, mcmc,
+                               thin))
+    for f in ("X", "delta", "tauh"):
+        for r in range(1, n):
+            assert np.array_equal(out[0][f], out[r][f]), f"{f} differs between ranks 0 and {r}"
+    _check_blocks(out, c["p"], n)
+    assert np.array_equal(out[0]["Sig"], _one_rank_sigma(dcfm, c, g, K, burnin, mcmc, thin, asm_batch))
     assert rel_err(out[0]["Sig"], S_ref) < 1e-10
     for f in ("X", "delta", "tauh"):
         assert rel_err(out[0][f], getattr(ref, f)) < 1e-10, f

@@ -127,6 +127,19 @@ def test_faithful_vs_vectorised(n, p, g, K):
     assert rel_err(S2, S1) < 1e-12
 
 
+def test_faithful_vs_vectorised_at_c1_shape():
+    """The vectorised oracle that the BASELINE-shape GPU parity tests use
+    (tests/test_gpu_parity_configs.py) agrees with the faithful per-row loop at c1's shape
+    (p = 1,000, n = 100, g = 4, K = 5), the largest the faithful loop runs in seconds."""
+    c = make_case(100, 1000, 4, 5, seed=29, k0=10)
+    s1, s2 = c["st"].copy(), c["st"].copy()
+    S1 = F.run_chain(c["Yd"], s1, c["rho"], c["hyper"], c["src"].iteration, 1, 2, 1, 1, 1)
+    S2 = V.full(V.run_chain(c["Yd"], s2, c["rho"], c["hyper"], c["src"].iteration, 1, 2, 1, 1, 1))
+    for f, a in s1.as_dict().items():
+        assert rel_err(getattr(s2, f), a) < 1e-12, f
+    assert rel_err(S2, S1) < 1e-12
+
+
 def test_posterior_mean_recovers_truth():
     """End-to-end statistical sanity of the oracle chain's Sigmaout against the synthetic truth.
 
