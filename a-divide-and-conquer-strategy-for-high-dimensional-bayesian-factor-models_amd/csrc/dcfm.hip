@@ -494,7 +494,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         ALLOC(b.xa_all, (size_t)nranks * KP * KP);
     }
     ALLOC(b.XM, 2 * KP * KP);
-    ALLOC(b.xpart, 8 * KP * KP);          // k_deltaops: min(8, G) chunk sums
+    ALLOC(b.xpart, (size_t)G * KP * KP);  // k_deltaops: xsum_blocks(G) <= G chunk sums
     {
         double *tk = nullptr;
         ALLOC(tk, 1);

@@ -368,36 +368,30 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
 }
 
 // ============================================================================
-// k_xred: xin[i][k] = sum_m Sp[m][i][k]  (local shards, fixed order)     dc:120-124
+// k_xred: xin[i][k] = sum_m Sp[m][i][k]  (local shards, canonical tree)  dc:120-124
 // ============================================================================
 __global__ __launch_bounds__(256) void k_xred(Dims d, const double *__restrict__ Sp,
                                               double *__restrict__ xin) {
     const size_t total = (size_t)d.NP * d.kp;
     const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (e >= total) return;
-    double acc = 0.0;
-#pragma unroll 8
-    for (int m = 0; m < d.G; ++m) acc += Sp[(size_t)m * total + e];
-    xin[e] = acc;
+    xin[e] = tree_sum(Sp + e, d.G, total);
 }
 
 // ============================================================================
-// k_asum: xa = sum_m A_m over local shards (fixed order), one thread per element.   dc:113-116
+// k_asum: xa = sum_m A_m over local shards (canonical tree), one thread per element.  dc:113-116
 // ============================================================================
 __global__ __launch_bounds__(256) void k_asum(Dims d, const double *__restrict__ A,
                                               double *__restrict__ xa) {
     const int e = blockIdx.x * 256 + threadIdx.x;
     const int kk = d.kp * d.kp;
     if (e >= kk) return;
-    double v = 0.0;
-#pragma unroll 8
-    for (int m = 0; m < d.G; ++m) v += A[(size_t)m * kk + e];
-    xa[e] = v;
+    xa[e] = tree_sum(A + e, d.G, (size_t)kk);
 }
 
 // ============================================================================
 // k_xchol: Xprec = g*I + rho*sum A (dc:117) and Rx = cholcov(Xprec) (dc:118), on the
-// side stream.  Sums the per-rank sums xa_all (k_asum, all-gathered) in rank order
+// side stream.  Sums the per-rank sums xa_all (k_asum, all-gathered) in the canonical tree
 // and writes the X-draw operators XM = {Tx = sqrt(rho) Ux Ux', Ux = Rx^{-T}} (Tx by MFMA).
 // ============================================================================
 constexpr int XCHOL_SMEM = 2 * KP * (KP + 1) + TS16 * (KP + 1) + 3 * TS16 + 2;
@@ -440,9 +434,7 @@ __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict_
                                                double *__restrict__ XM) {
     __shared__ double smem[XCHOL_SMEM];
     for (int e = threadIdx.x; e < KP * KP; e += 256) {
-        double v = xa_all[e];
-        for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * d.xstride + e];
-        xprec_store(d, smem, e, v);
+        xprec_store(d, smem, e, tree_sum(xa_all + e, d.nranks, (size_t)d.xstride));
     }
     __syncthreads();
     xchol_factor(d, XM, smem);
@@ -450,16 +442,17 @@ __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict_
 
 // ============================================================================
 // k_xdraw: X' = Tx S' + Ux eps' as fp64 MFMA (operators from k_xchol).  S is the sum of
-// nsrc [NP][KP] slices: the ranks' gathered sums (xall, rank order), or — one rank, fused
-// chain — the G shard messages Sp themselves, which makes k_xred's launch unnecessary.
-// 16 rows per block: the 4 waves sum slices w, w+4, ... (fixed order), wave 0 adds the
-// partials in wave order and runs the MFMAs.                                  dc:119-128
+// nsrc [NP][KP] slices in the canonical tree order (TreeSum): the ranks' gathered sums
+// (xall), or — one rank, fused chain — the G shard messages Sp themselves, which makes
+// k_xred's launch unnecessary.  16 rows per block: wave w sums the slices of columns
+// 8w .. 8w+7 (lane (c, q): row i0 + c, columns 8w + 2q, +1), wave 0 collects the four
+// column groups and runs the MFMAs.                                       dc:119-128
 // ============================================================================
 __global__ __launch_bounds__(256) void k_xdraw(Dims d, const double *__restrict__ src, int nsrc,
                                                const double *__restrict__ XM,
                                                double *__restrict__ X, DrawsDev dr, int64_t iter) {
     __shared__ double Ms[2][KP][KP + 1];
-    __shared__ d2 part[3][4][64];
+    __shared__ d2 part[3][64];
     for (int e = threadIdx.x; e < 2 * KP * KP; e += 256) {
         const int mat = e / (KP * KP), rem = e % (KP * KP);
         Ms[mat][rem / KP][rem % KP] = XM[e];
@@ -469,8 +462,6 @@ __global__ __launch_bounds__(256) void k_xdraw(Dims d, const double *__restrict_
     const bool live = i < d.n;
     const size_t stride = (size_t)d.NP * KP;
     d2 sv[4], ev[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) sv[t] = d2{0.0, 0.0};
     if (w == 0) {   // eps of dc:126 (draw buffer), in flight during the sum
         const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K;
 #pragma unroll
@@ -480,22 +471,26 @@ __global__ __launch_bounds__(256) void k_xdraw(Dims d, const double *__restrict_
             ev[t].y = (live && kk + 1 < d.K) ? nx[kk + 1] : 0.0;
         }
     }
-    const double *base = src + (size_t)i * KP + 2 * q;
-#pragma unroll 4
-    for (int rk = w; rk < nsrc; rk += 4) {
-        const double *p = base + rk * stride;
+    {
+        const double *p = src + (size_t)i * KP + 8 * w + 2 * q;
+        TreeSum<d2> ts;
+        int rk = 0;
+        for (; rk + 4 <= nsrc; rk += 4) {   // 4 loads in flight, pushed in order
+            d2 v[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) sv[t] += *reinterpret_cast<const d2 *>(p + 8 * t);
-    }
-    if (w > 0) {
+            for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const d2 *>(p + (size_t)(rk + u) * stride);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) part[w - 1][t][lane] = sv[t];
+            for (int u = 0; u < 4; ++u) ts.push(v[u]);
+        }
+        for (; rk < nsrc; ++rk) ts.push(*reinterpret_cast<const d2 *>(p + (size_t)rk * stride));
+        const d2 tot = ts.total();
+        if (w > 0) part[w - 1][lane] = tot;
+        else sv[0] = tot;
     }
     __syncthreads();
     if (w > 0) return;
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-        for (int r = 0; r < 3; ++r) sv[t] += part[r][t][lane];
+    for (int t = 1; t < 4; ++t) sv[t] = part[t - 1][lane];
     d4 ax[2];
     ax[0] = ax[1] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1005,6 +1000,14 @@ __global__ __launch_bounds__(256) void k_colgram(Dims d, const double *__restric
 // completion before the ticket — __threadfence's buffer_wbl2 / buffer_inv flush the XCD's
 // whole L2 and drop what co-resident blocks cache (measured +20 us next to a Y pass).
 constexpr int XSUM_BLOCKS = 8;
+// blocks of the A sum: G / chunk, chunk = a power of two dividing G, grown while more than
+// XSUM_BLOCKS chunks remain — so each chunk is a subtree of the canonical tree (TreeSum) and
+// the tree over the chunk sums is T(0, G)
+__host__ __device__ inline int xsum_blocks(int G) {
+    int chunk = 1;
+    while (G / chunk > XSUM_BLOCKS && (G / chunk) % 2 == 0) chunk *= 2;
+    return G / chunk;
+}
 __device__ __forceinline__ void st_agent(double *p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1033,14 +1036,12 @@ __device__ __forceinline__ void xsum_tree(const Dims &d, const double *__restric
                                           unsigned *__restrict__ ticket, double *__restrict__ xa, int j, int nxs,
                                           double *smem) {
     const int t = threadIdx.x;
-    const int chunk = (d.G + nxs - 1) / nxs, m0 = j * chunk, m1 = min(d.G, m0 + chunk);
+    const int chunk = d.G / nxs, m0 = j * chunk;   // a canonical subtree (xsum_blocks)
     double v[KP * KP / 256];
 #pragma unroll
     for (int u = 0; u < KP * KP / 256; ++u) {
         const int e = t + 256 * u;
-        double acc = 0.0;
-#pragma unroll 8
-        for (int m = m0; m < m1; ++m) acc += A[(size_t)m * KP * KP + e];
+        const double acc = tree_sum(A + (size_t)m0 * KP * KP + e, chunk, (size_t)KP * KP);
         v[u] = acc;
         st_agent(xpart + (size_t)j * KP * KP + e, acc);
     }
@@ -1048,9 +1049,9 @@ __device__ __forceinline__ void xsum_tree(const Dims &d, const double *__restric
 #pragma unroll
     for (int u = 0; u < KP * KP / 256; ++u) {
         const int e = t + 256 * u;
-        double acc = 0.0;
-        for (int jj = 0; jj < nxs; ++jj) acc += (jj == j) ? v[u] : ld_agent(xpart + (size_t)jj * KP * KP + e);
-        xa[e] = acc;
+        TreeSum<double> ts;
+        for (int jj = 0; jj < nxs; ++jj) ts.push((jj == j) ? v[u] : ld_agent(xpart + (size_t)jj * KP * KP + e));
+        xa[e] = ts.total();
     }
 }
 
@@ -1063,7 +1064,7 @@ __global__ __launch_bounds__(256) void k_deltaops(Dims d, const double *__restri
                                                   unsigned *__restrict__ ticket, double *__restrict__ xa,
                                                   int ops) {
     __shared__ double smem[PREP_SMEM];
-    const int nxs = d.G < XSUM_BLOCKS ? d.G : XSUM_BLOCKS;
+    const int nxs = xsum_blocks(d.G);
     int b = blockIdx.x + (ops ? 0 : nxs + d.G);   // !ops: the delta blocks alone
     if (b < nxs) {
         xsum_tree(d, A, xpart, ticket, xa, b, nxs, smem);
@@ -1090,10 +1091,8 @@ __global__ __launch_bounds__(256) void k_zxchol(Dims d, const double *__restrict
         zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blockIdx.x - 1, gridDim.x - 1), smem);
         return;
     }
-    for (int e = threadIdx.x; e < KP * KP; e += 256) {   // the ranks' shard sums, in rank order
-        double v = xa_all[e];
-        for (int rk = 1; rk < d.nranks; ++rk) v += xa_all[(size_t)rk * d.xstride + e];
-        xprec_store(d, smem, e, v);
+    for (int e = threadIdx.x; e < KP * KP; e += 256) {   // the ranks' shard sums, canonical tree
+        xprec_store(d, smem, e, tree_sum(xa_all + e, d.nranks, (size_t)d.xstride));
     }
     __syncthreads();
     xchol_factor(d, XM, smem);
@@ -1452,7 +1451,7 @@ void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
                      const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
                      hipStream_t s, bool ops) {
     if (d.kp != KP) return;
-    const int nxs = d.G < XSUM_BLOCKS ? d.G : XSUM_BLOCKS;
+    const int nxs = xsum_blocks(d.G);
     const int nb = (ops ? nxs + d.G : 0) + (delta ? (d.g + 3) / 4 : 0);
     if (nb == 0) return;
     hipLaunchKernelGGL(k_deltaops, dim3(nb), dim3(256), 0, s, d, b.sall, delta_in, tau_in, delta_out, tau_out, dr,

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 }
 
 // ============================================================================
-// k_xchol: Xprec = g I + rho sum_m A_m (dc:117, summed over ranks in rank order),
+// k_xchol: Xprec = g I + rho sum_m A_m (dc:117, summed over ranks in the canonical tree),
 // Rx = cholcov(Xprec) (dc:118); XM = {Tx = sqrt(rho) Ux Ux', Ux = Rx^{-T}}.
 // ============================================================================
 template <int KW>
@@ -120,8 +120,7 @@ __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict_
         double v = (R == Cc) ? 1.0 : 0.0;
         if (R < N && Cc < N) {
             const size_t o = (size_t)Cc * KW + R;   // upper triangle: Xprec[c][r]
-            double sa = xa_all[o];
-            for (int rk = 1; rk < d.nranks; ++rk) sa += xa_all[(size_t)rk * KW * KW + o];
+            const double sa = tree_sum(xa_all + o, d.nranks, (size_t)KW * KW);   // ranks' sums, canonical tree
             v = (R == Cc ? (double)d.g : 0.0) + d.rho * sa;
         }
         Ts[tile::tix(I, J) * tile::TSZ + c * tile::TLD + r] = v;
@@ -234,7 +233,7 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
 }
 
 // ============================================================================
-// k_xdraw: X' = Tx S' + Ux eps' (S summed over ranks in rank order), one wave per
+// k_xdraw: X' = Tx S' + Ux eps' (S summed over ranks, canonical tree), one wave per
 // 16 rows.                                                                   dc:119-128
 // ============================================================================
 template <int KW>
@@ -252,9 +251,9 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
     for (int mt = 0; mt < MT; ++mt) ax[mt] = d4{0.0, 0.0, 0.0, 0.0};
     for (int t = 0; t < KW / 8; ++t) {
         const int kk = 8 * t + 2 * q;
-        d2 sv = *reinterpret_cast<const d2 *>(xall + (size_t)i * KW + kk);
-        for (int rk = 1; rk < d.nranks; ++rk)
-            sv += *reinterpret_cast<const d2 *>(xall + rk * stride + (size_t)i * KW + kk);
+        TreeSum<d2> ts;                                  // the ranks' message sums, canonical tree
+        for (int rk = 0; rk < d.nranks; ++rk) ts.push(*reinterpret_cast<const d2 *>(xall + rk * stride + (size_t)i * KW + kk));
+        const d2 sv = ts.total();
         const d2 ev = row_normals(d, nx, live, SITE_X, 0, i, kk, iter);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {

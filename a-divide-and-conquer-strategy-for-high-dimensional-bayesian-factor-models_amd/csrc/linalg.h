@@ -53,6 +53,54 @@ __device__ __forceinline__ double bcast16(double v) {
     return __hiloint2double(hi, lo);
 }
 
+// Canonical shard sum, independent of the rank count: sum_{m < n} x_m evaluated as the
+// left-complete binary tree T(0, n) = T(0, h) + T(h, n - h), h = the largest power of two
+// below n.  A rank's G consecutive shards (G a power of two, offset a multiple of G) are
+// one subtree, and the tree over the ranks' subtotals has the same shape, so the per-rank
+// sums combined over ranks reproduce T(0, g) bit for bit: the sweep gives the same numbers
+// on 1, 2, 4 or 8 GPUs (the X message sum dc:120-124 and the A sum dc:117).  Evaluated as
+// a binary counter: after i pushes, level l holds a finished 2^l-subtree iff bit l of i is
+// set.  Levels stay in registers (unrolled, constant indices); n < 2^TREE_LEVELS.
+constexpr int TREE_LEVELS = 16;
+template <class T>
+struct TreeSum {
+    T s[TREE_LEVELS];
+    int i = 0;
+    // static_for: the level indices are constants from the start, so s[] is promoted to registers
+    __device__ __forceinline__ void push(T v) {
+        bool open = true;   // still carrying
+        static_for<TREE_LEVELS>([&](auto L) {
+            if (open) {
+                if ((i >> L) & 1) {
+                    v = s[L] + v;
+                } else {
+                    s[L] = v;
+                    open = false;
+                }
+            }
+        });
+        ++i;
+    }
+    // right to left: the smallest finished subtree is the rightmost
+    __device__ __forceinline__ T total() const {
+        T acc{};
+        bool have = false;
+        static_for<TREE_LEVELS>([&](auto L) {
+            if ((i >> L) & 1) {
+                acc = have ? s[L] + acc : s[L];
+                have = true;
+            }
+        });
+        return acc;
+    }
+};
+// sum_{k < n} src[k * stride] in the canonical tree order
+__device__ __forceinline__ double tree_sum(const double *__restrict__ src, int n, size_t stride) {
+    TreeSum<double> t;
+    for (int k = 0; k < n; ++k) t.push(src[(size_t)k * stride]);
+    return t.total();
+}
+
 // 1/sqrt(x) to full fp64 precision: hardware estimate + 2 Newton steps
 __device__ __forceinline__ double rsqrt_f64(double x) {
     double y = __builtin_amdgcn_rsq(x);
