@@ -68,29 +68,63 @@ def binding_roof(flops, nbytes):
     return "hbm" if nbytes / (HBM_PEAK_GBS * 1e9) >= flops / (FP64_MFMA_PEAK_TFLOPS * 1e12) else "mfma"
 
 
-def pmc_traffic(kernel, workload_tag):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the
-    same workload (profiles/r01_<tag>_pmc.json, written by tools/pmc_summary.py from
-    separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 note of
-    the MI355X microarchitecture guide).  None when no summary matches."""
-    f = ROOT / "profiles" / f"r01_{workload_tag}_pmc.json"
-    if not f.exists():
-        return None, None
-    ks = json.load(open(f))["kernels"]
-    k = ks.get(kernel) or next((v for name, v in ks.items() if name.startswith(kernel + "_")), {})   # k_lambda_t
-    return k.get("hbm_bytes_per_dispatch"), str(f.relative_to(ROOT))
+def build_id():
+    """Identity of the product build: sha256 over the sources libdcfm.so is compiled from
+    (csrc/*.hip, csrc/*.h, the Makefile, include/dcfm.h).  PMC summaries carry it, so
+    roofline.traffic is only ever taken from a profile of this exact build."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = ROOT / "a-divide-and-conquer-strategy-for-high-dimensional-bayesian-factor-models_amd" / "csrc"
+    files = sorted(list(csrc.glob("*.hip")) + list(csrc.glob("*.h")) + [csrc / "Makefile", ROOT / "include" / "dcfm.h"])
+    for p in files:
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()[:16]
 
 
-def cpu_baseline_run(n, p, g, K, rho, steps=5, thin=5):
-    """Vectorised NumPy restatement (oracle, 'port') on a bounded c3 sample."""
-    import oracle
-    from oracle import dc_oracle as F
-    from oracle import vectorised as V
+def config_key(args, world):
+    """The bench invocation a PMC summary must match (workload, flush sizes, step counts)."""
+    return (f"g{args.g}_P{args.P}_n{args.n}_K{args.K}_thin{args.thin}_asm{args.asm_batch}_"
+            f"steps{args.steps}_warmup{args.warmup}_gpus{world}{'_chains' if args.chains else ''}")
+
+
+def pmc_traffic(kernel, build, key, launches):
+    """HBM bytes per launch of `kernel` in the timed region, from a committed rocprofv3 PMC
+    summary (profiles/*_pmc.json, tools/pmc_summary.py over separate FETCH_SIZE /
+    WRITE_SIZE passes of this same bench command, FETCH_SIZE doubled per the gfx950 note
+    of the MI355X microarchitecture guide) whose build id AND bench configuration equal
+    this run's; the mean over the kernel's last `launches` dispatches (the timed region is
+    the last part of the run).  (None, None) when no summary matches."""
+    for f in sorted((ROOT / "profiles").glob("*_pmc.json")):
+        try:
+            doc = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if doc.get("build") != build or doc.get("config") != key:
+            continue
+        ks = doc.get("kernels", {})
+        k = ks.get(kernel) or next((v for name, v in ks.items() if name.startswith(kernel + "_")), None)
+        if not k:
+            continue
+        fe, wr = k.get("fetch_bytes_each"), k.get("write_bytes_each")
+        if fe and wr and len(fe) >= launches and len(wr) >= launches:
+            return sum(fe[-launches:]) / launches + sum(wr[-launches:]) / launches, str(f.relative_to(ROOT))
+        if k.get("hbm_bytes_per_dispatch") is not None:
+            return k["hbm_bytes_per_dispatch"], str(f.relative_to(ROOT))
+    return None, None
+
+
+def _threads():
     try:
         from threadpoolctl import threadpool_info
-        cores = max((i.get("num_threads", 1) for i in threadpool_info()), default=1)
+        return max((i.get("num_threads", 1) for i in threadpool_info()), default=1)
     except Exception:
-        cores = os.cpu_count() or 1
+        return os.cpu_count() or 1
+
+
+def _cpu_case(n, p, g, K, rho):
+    import oracle
+    from oracle import dc_oracle as F
     Y = synth_data(n, p)
     hyper = F.Hyper()
     Yk, n, pk, P, K_, keep = F.preprocess(Y, g, K * g)
@@ -98,14 +132,37 @@ def cpu_baseline_run(n, p, g, K, rho, steps=5, thin=5):
     init = src.init()
     Yd = F.standardize(F.partition(Yk, g, init.varind))
     st = F.initialise(n, P, K, g, rho, hyper, init)
-    draws = [src.iteration(t) for t in range(1, steps + 1)]
+    return Yd, st, src, hyper
+
+
+def cpu_baseline_run(n, p, g, K, rho, steps=5, thin=5):
+    """Vectorised NumPy restatement (oracle, 'port') on a bounded c3 sample.  The timed
+    region includes the draw generation (the GPU leg draws its own numbers too)."""
+    from oracle import vectorised as V
+    Yd, st, src, hyper = _cpu_case(n, p, g, K, rho)
     D = V.Data(Yd)
     t0 = time.perf_counter()
-    V.run_chain(D, st, rho, hyper, lambda it: draws[it - 1], 1, steps, 0, steps, thin)
+    V.run_chain(D, st, rho, hyper, src.iteration, 1, steps, 0, steps, thin)
     dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "iter/s", "cores": int(cores), "kind": "port",
-            "sample": f"{steps} Gibbs iterations of c3 (incl. {steps // thin} covariance assembly at thin={thin}), "
-                      f"vectorised NumPy/OpenBLAS restatement of divideconquer.m:90-196 (not MATLAB), {dt:.1f} s"}
+    return {"value": steps / dt, "unit": "iter/s", "cores": int(_threads()), "kind": "port",
+            "sample": f"{steps} Gibbs iterations of c3 (incl. {steps // thin} covariance assembly at thin={thin} "
+                      f"and the draw generation), vectorised NumPy/OpenBLAS restatement of divideconquer.m:90-196 "
+                      f"(not MATLAB), {dt:.1f} s"}
+
+
+def cpu_faithful_run(n, p, g, K, rho):
+    """The MATLAB-structure CPU proxy: the faithful restatement
+    (oracle/dc_oracle.py, the reference's per-shard, per-row loops of dc:97-177 kept as
+    loops) for ONE Gibbs iteration of c3, draws generated inside the timed region.  A
+    restatement, not MATLAB (no MATLAB on the box)."""
+    from oracle import dc_oracle as F
+    Yd, st, src, hyper = _cpu_case(n, p, g, K, rho)
+    t0 = time.perf_counter()
+    F.gibbs_iteration(st, Yd, rho, hyper, src.iteration(1))
+    dt = time.perf_counter() - t0
+    return {"value": 1.0 / dt, "unit": "iter/s", "cores": int(_threads()), "kind": "port",
+            "sample": f"1 Gibbs iteration of c3 (no assembly), faithful per-row-loop NumPy restatement of "
+                      f"divideconquer.m:97-177 (restatement, not MATLAB), {dt:.1f} s"}
 
 
 def main():
@@ -121,6 +178,7 @@ def main():
     ap.add_argument("--K", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=10)
+    ap.add_argument("--no-faithful", action="store_true", help="skip the faithful-loop CPU leg (~30 s)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--chains", action="store_true",
                     help="one independent chain per rank (config c4: parallel chains, seed 1 + rank, no "
@@ -169,6 +227,8 @@ def main():
     nnz, ms_nnz = dcfm.count_nonzero_columns(Y, device=device, return_ms=True)
     keep = np.flatnonzero(nnz != 0)
     pk = keep.size
+    if pk % g:   # the reference errors here too (dc:41: p must split into g equal shards)
+        raise SystemExit(f"{pk} non-zero columns do not split into g = {g} equal shards")
     P = pk // g
     init = dcfm.driver._HostVarind(1, pk)     # dc:50 on the host; dc:68-87 on the device below
     chains = args.chains
@@ -288,6 +348,7 @@ def main():
         dt = float(tt.item())
 
     value = args.steps / dt * (world if chains else 1)     # chains: iterations of all chains
+    bid, ckey = build_id(), config_key(args, world)
     d = {"n": n, "P": P, "K": K, "G": gl, "p": p, "nranks": shard_ranks}
     kern = {}
     roof = None
@@ -319,12 +380,11 @@ def main():
             ach, peak, unit = fl / avg_s / 1e12, FP64_MFMA_PEAK_TFLOPS, "TFLOP/s"
         else:
             ach, peak, unit = by / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
-        tag = {(64, 312, 1000, 30): "c3", (8, 1250, 2000, 100): "c4"}.get((g, P, n, K))
-        traffic, tsrc = pmc_traffic(dominant, tag) if tag else (None, None)
+        traffic, tsrc = pmc_traffic(dominant, bid, ckey, int(cnt))
         roof = {"kernel": dominant, "bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": unit,
                 "frac": round(ach / peak, 4),
                 "traffic": round(traffic) if traffic is not None else None,
-                "traffic_unit": "bytes/launch", "traffic_source": tsrc,
+                "traffic_unit": "bytes/launch", "traffic_source": tsrc, "build": bid, "config_key": ckey,
                 "algorithmic_bytes": round(by), "avg_us": round(avg_s * 1e6, 2),
                 "launches": int(cnt),
                 "note": "achieved = algorithmic work per launch / mean HIP-event duration of this kernel, "
@@ -342,6 +402,8 @@ def main():
                    "global_batch": n,
                    "parallelism": f"chains{world} (1 per GPU)" if chains else f"shards{g}/gpus{world}"},
         "roofline": roof,
+        "build": bid,
+        "config_key": ckey,
     }
     if "k_assemble" in kern:
         out["assembly_mfma_util"] = round(kern["k_assemble"]["tflops"] / FP64_MFMA_PEAK_TFLOPS, 4)
@@ -353,6 +415,8 @@ def main():
         out["diagnostics"] = diag
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_run(n, p, g, K, rho, steps=args.cpu_steps, thin=thin)
+        if not args.no_faithful:
+            out["cpu_baseline_faithful"] = cpu_faithful_run(n, p, g, K, rho)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
