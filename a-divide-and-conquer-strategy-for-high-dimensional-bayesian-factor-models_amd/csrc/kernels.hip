@@ -34,17 +34,6 @@
 
 namespace dcfm {
 
-#ifdef DCFM_PHASE_TIMING
-__device__ unsigned long long g_phase[32];
-}  // namespace dcfm
-// development build only: read and clear the per-phase shader-clock sums
-extern "C" int dcfm_debug_phases(unsigned long long out[32]) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dcfm::g_phase), 32 * sizeof(unsigned long long)) != hipSuccess) return 1;
-    unsigned long long z[32] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(dcfm::g_phase), z, sizeof z) == hipSuccess ? 0 : 1;
-}
-namespace dcfm {
-#endif
 
 // device helpers (MFMA, lane broadcast, rsqrt, register Cholesky): linalg.h
 
@@ -133,14 +122,10 @@ __device__ __forceinline__ void prep_ops(const Dims &d, double *__restrict__ ZM,
     double *lds_l = smem + 4 * KP * (KP + 1), *lds_u = lds_l + 2 * TS16;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     double *Zm = ZM + (size_t)m * 4 * KP * KP;
-    PHASE_T0();
     if (wave == 0) {                                                // U = L^{-1} -> part[1]
-        PHASE(2);
         chol_inv32(part[2], part[1], part[3], lds_l, lds_u, lane);
-        PHASE(3);
     }
     __syncthreads();
-    PHASE(4);
     {   // T = U U' (fp64 MFMA, one 16x16 tile per wave) -> part[2]; M1 = s1r T; U
         const int ti = wave >> 1, tj = wave & 1, j = lane & 15, q = lane >> 4;
         const d4 T = mfma_tile32<true>(part[1], part[1], ti, tj, lane);
@@ -160,8 +145,6 @@ __device__ __forceinline__ void prep_ops(const Dims &d, double *__restrict__ ZM,
 #pragma unroll
         for (int g = 0; g < 4; ++g) Zm[KP * KP + (16 * ti + q + 4 * g) * KP + 16 * tj + j] = s2 * M[g];
     }
-    PHASE(5);
-    PHASE_END_AT(8);
 }
 
 __device__ __forceinline__ void prep_shard(const Dims &d, const double *__restrict__ Lam,
@@ -401,15 +384,11 @@ __device__ __forceinline__ void xchol_factor(const Dims &d, double *__restrict__
     double (*Us)[KP + 1] = Sm + KP;
     double (*Wk)[KP + 1] = Us + KP;
     double *lds_l = smem + 2 * KP * (KP + 1) + TS16 * (KP + 1), *lds_u = lds_l + 2 * TS16;
-    PHASE_T0();
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (wave == 0) {                       // Ux = Lx^{-1} = Rx^{-T}
-        PHASE(1);
         chol_inv32(Sm, Us, Wk, lds_l, lds_u, lane);
-        PHASE(2);
     }
     __syncthreads();
-    PHASE(3);
     // X = Rx^{-T}(Rx^{-1} sqrt(rho) S + eps) = Tx S + Ux eps,  Tx = sqrt(rho) Ux Ux'
     const int ti = wave >> 1, tj = wave & 1, j = lane & 15, q = lane >> 4;
     const d4 T = mfma_tile32<true>(Us, Us, ti, tj, lane);
@@ -419,8 +398,6 @@ __device__ __forceinline__ void xchol_factor(const Dims &d, double *__restrict__
         XM[a * KP + c] = d.sr * T[g];
         XM[KP * KP + a * KP + c] = Us[a][c];
     }
-    PHASE(4);
-    PHASE_END_AT(16);
 }
 
 // Xprec's upper triangle, transposed into the lower triangle of Sm: g I + rho sum A   dc:117
@@ -645,10 +622,7 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
 // psi o lambda^2 of the row -> cpart[m][j][:] (k_colsum sums the rows).
 // ============================================================================
 
-#ifndef DCFM_LAMBDA_MINWAVES
-#define DCFM_LAMBDA_MINWAVES 1
-#endif
-__global__ __launch_bounds__(64, DCFM_LAMBDA_MINWAVES) void k_lambda(Dims d, const double *__restrict__ C,
+__global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict__ C,
                                                const double *__restrict__ E,
                                                const double *__restrict__ yy,
                                                const double *__restrict__ tau_cur,
@@ -772,9 +746,6 @@ __global__ __launch_bounds__(64, DCFM_LAMBDA_MINWAVES) void k_lambda(Dims d, con
                 if (c < KH) qa[c < KH ? c : 0] = fma(-la1, lc.y, fma(-la0, lc.x, qa[c < KH ? c : 0]));
             }
             qb[c] = fma(-lb1, lc.y, fma(-lb0, lc.x, qb[c]));
-#ifdef DCFM_LAMBDA_CHUNK
-            if ((c - k - 2) % DCFM_LAMBDA_CHUNK == DCFM_LAMBDA_CHUNK - 1) __builtin_amdgcn_sched_barrier(0);   // bound the hoisted reads
-#endif
         }
 #pragma unroll
         for (int c = k + 2; c < KP; ++c) {
@@ -1347,9 +1318,6 @@ __device__ __forceinline__ void draw_normal_row(const Rng &rng, uint32_t site, u
 // and the normal segments (high occupancy); b_off = first block of the launch
 template <bool GAMMAS>
 __global__ __launch_bounds__(256) void k_draws(Dims d, DrawsDev dr, int64_t iter) {
-#ifdef DCFM_VARIANT_NODRAWS
-    if (iter >= 0) return;   // development A/B only: the chain without RNG cost
-#endif
     const DrawPlan pl = draw_plan(d);
     const Rng rng(d.seed);
     const uint32_t it = (uint32_t)iter;

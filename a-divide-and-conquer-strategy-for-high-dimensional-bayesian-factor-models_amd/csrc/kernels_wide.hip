@@ -362,11 +362,7 @@ __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
     }
     __syncthreads();
     // ---- factorisation with fused forward solve (dc:142 chol, dc:143 Llam \ blam)
-#ifdef DCFM_VARIANT_NOFACTOR
-    for (int Jk = 0; Jk < 0; ++Jk) {
-#else
     for (int Jk = 0; Jk < nb; ++Jk) {
-#endif
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
             const int k = 8 * Jk + kk;
@@ -391,11 +387,7 @@ __global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
                 }
             }
             __syncthreads();
-#ifndef DCFM_VARIANT_NOUPDATE
             if (role != 3 && J >= Jk) {
-#else
-            if (role != 3 && J >= Jk && d.n < 0) {
-#endif
                 const bool same = (J == Jk);
                 double lc[8];
 #pragma unroll

@@ -144,38 +144,6 @@ __device__ inline double delta_G(const Dims &d, const DrawsDev &dr, int64_t iter
     return dr.Gdelta[((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + h];
 }
 
-// Development-only phase timer (build with -DDCFM_PHASE_TIMING): lane 0 of every
-// wave adds shader-clock deltas per phase into g_phase (read by dcfm_debug_phases).
-#ifdef DCFM_PHASE_TIMING
-extern __device__ unsigned long long g_phase[32];
-#define PHASE_T0()                                                                          \
-    unsigned long long ph_t_ = __builtin_amdgcn_s_memtime(), ph_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
-#define PHASE(k)                                                                            \
-    do {                                                                                    \
-        const unsigned long long ph_n_ = __builtin_amdgcn_s_memtime();                      \
-        ph_acc_[(k)] += ph_n_ - ph_t_;                                                      \
-        ph_t_ = ph_n_;                                                                      \
-    } while (0)
-#define PHASE_END_AT(b)                                                                     \
-    do {                                                                                    \
-        if ((threadIdx.x & 63) == 0)                                                        \
-            for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&g_phase[(b) + k_], ph_acc_[k_]);      \
-    } while (0)
-#define PHASE_END() PHASE_END_AT(0)
-// block-role completion stamps of one launch: slot 24 = ~(earliest block start), slot s = latest end
-#define STAMP_START() do { if (threadIdx.x == 0) atomicMax(&g_phase[24], ~(unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
-#define STAMP_END(s) do { if (threadIdx.x == 0) atomicMax(&g_phase[(s)], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
-#define STAMP_START2() do { if (threadIdx.x == 0) atomicMax(&g_phase[28], ~(unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
-#else
-#define STAMP_START2() (void)0
-#define STAMP_START() (void)0
-#define STAMP_END(s) (void)0
-#define PHASE_END_AT(b) (void)0
-#define PHASE_T0() (void)0
-#define PHASE(k) (void)0
-#define PHASE_END() (void)0
-#endif
-
 // eta = sqrt(rho) X + sqrt(1-rho) Z    (dc:81,133) — one definition for every use
 __device__ __forceinline__ double eta_of(double sr, double s1r, double x, double z) {
     return sr * x + s1r * z;
