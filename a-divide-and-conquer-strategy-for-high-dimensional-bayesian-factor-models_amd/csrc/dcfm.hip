@@ -542,11 +542,21 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         }
     }
 #undef ALLOC
-    // this rank's lower-triangle assembly tiles, in the storage order of its Sigma block
+    // this rank's lower-triangle assembly tiles in k_assemble's processing order: 8 x 8-tile
+    // supertiles (row bands of the rank's block, then column bands), row-major inside — the
+    // tiles an XCD runs together share their Lb panels in L2.  (Storage is by (ti, tj).)
     {
+        constexpr int SB = 8;
         std::vector<int2> tl;
-        for (int ti = b.T0; ti < b.T1; ++ti)
-            for (int tj = 0; tj <= ti; ++tj) tl.push_back(make_int2(ti, tj));
+        for (int rb0 = b.T0; rb0 < b.T1; rb0 += SB) {
+            const int rb1 = std::min(b.T1, rb0 + SB);
+            for (int cb0 = 0; cb0 < rb1; cb0 += SB)
+                for (int ti = rb0; ti < rb1; ++ti)
+                    for (int tj = cb0; tj < std::min(cb0 + SB, ti + 1); ++tj) tl.push_back(make_int2(ti, tj));
+        }
+        if ((int64_t)tl.size() != tri(b.T1) - tri(b.T0))
+            return fail(h, DCFM_ERR_INVALID, "assembly tile list: %zu tiles for %lld", tl.size(),
+                        (long long)(tri(b.T1) - tri(b.T0)));
         b.ntiles = (int)tl.size();
         void *q = nullptr;
         HIPC(h, hipMalloc(&q, std::max<size_t>(1, tl.size()) * sizeof(int2)));

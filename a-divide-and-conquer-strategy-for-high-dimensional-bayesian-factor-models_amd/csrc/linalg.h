@@ -94,11 +94,21 @@ struct TreeSum {
         return acc;
     }
 };
+// sum_{k < n} load(k) in the canonical tree order; the loads go out in batches of B
+// (predicated, all in flight together) before the batch is pushed
+template <class T, int B = 8, class F>
+__device__ __forceinline__ T tree_sum_f(int n, F &&load) {
+    TreeSum<T> ts;
+    for (int k = 0; k < n; k += B) {
+        T v[B];
+        static_for<B>([&](auto U) { if (k + U < n) v[U] = load(k + U); });
+        static_for<B>([&](auto U) { if (k + U < n) ts.push(v[U]); });
+    }
+    return ts.total();
+}
 // sum_{k < n} src[k * stride] in the canonical tree order
 __device__ __forceinline__ double tree_sum(const double *__restrict__ src, int n, size_t stride) {
-    TreeSum<double> t;
-    for (int k = 0; k < n; ++k) t.push(src[(size_t)k * stride]);
-    return t.total();
+    return tree_sum_f<double>(n, [&](int k) { return src[(size_t)k * stride]; });
 }
 
 // 1/sqrt(x) to full fp64 precision: hardware estimate + 2 Newton steps
