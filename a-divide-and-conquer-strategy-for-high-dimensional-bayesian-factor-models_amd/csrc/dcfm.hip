@@ -462,7 +462,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
 
     Bufs &b = h->b;
     const size_t G = d.G, NP = d.NP, PP = d.PP, g = d.g, p = d.p, KP = d.kp;
-    b.LDB = round_up(h->B * d.K, 16);
+    b.LDB = round_up(h->B * d.K, ASM_KC);
     int rc = DCFM_OK;
 #define ALLOC(ptr, n) if ((rc = dalloc(h, &(ptr), (n))) != DCFM_OK) { int r2 = rc; std::string m = h->err; dcfm_destroy(h); g_err = m; return r2; }
     ALLOC(b.Y, G * NP * PP);
@@ -983,15 +983,19 @@ static int flush_batch(dcfm_handle *h) {
         if (!h->loop) NCCLC(h, ncclGroupEnd());
         if (rc) return rc;
     }
-    const int kext = round_up(h->batch * d.K, 16);   // k_assemble chunk
+    const int used = h->batch * d.K, kext = round_up(used, ASM_KC);   // k_assemble chunk
     const double effsamp = (double)h->cfg.mcmc / (double)h->cfg.thin;   // dc:45 (Q8)
+    // k_save wrote columns [0, used) of every row; only the chunk's tail [used, kext) can
+    // hold an earlier batch's samples: zero just that (not the p x LDB buffer)
+    if (kext > used)
+        HIPC(h, hipMemset2DAsync(b.Lb[lb] + used, (size_t)b.LDB * sizeof(double), 0, (size_t)(kext - used) * sizeof(double),
+                                 (size_t)d.p, h->sasm));
     {
         KTimer t(h, DCFM_K_ASSEMBLE, h->sasm);
         launch_assemble(d, b, b.Lb[lb], b.wsum[lb], kext, 1.0 / effsamp, h->sasm);
     }
     HIPC(h, hipGetLastError());
-    HIPC(h, hipMemsetAsync(b.Lb[lb], 0, (size_t)d.p * b.LDB * sizeof(double), h->sasm));
-    HIPC(h, hipMemsetAsync(b.wsum[lb], 0, (size_t)d.p * sizeof(double), h->sasm));
+    HIPC(h, hipMemsetAsync(b.wsum[lb], 0, (size_t)d.p * sizeof(double), h->sasm));   // k_save adds into it
     HIPC(h, hipEventRecord(h->e_free[lb], h->sasm));
     h->asm_pending[lb] = true;
     h->lb ^= 1;

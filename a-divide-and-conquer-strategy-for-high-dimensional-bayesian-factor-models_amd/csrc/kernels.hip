@@ -1087,7 +1087,7 @@ __global__ __launch_bounds__(256) void k_save(Dims d, const double *__restrict__
 //    its L2 instead of streaming a new column panel per tile from the Infinity Cache.
 //    The tile's place in the rank's packed Sigma block comes from (ti, tj).
 //  * 8 waves in 2 x 4, each 64 x 32 = 4 x 2 tiles of v_mfma_f64_16x16x4.  The k extent
-//    (batch x K) runs in chunks of 16 through double-buffered LDS, stored k-major with a
+//    (batch x K) runs in chunks of 32 through double-buffered LDS (147 KB), stored k-major with a
 //    144-double pitch (an operand read, 16 consecutive rows x 4 k, is a conflict-free
 //    ds_read_b64); the next chunk's global loads are in flight during the current
 //    chunk's MFMAs.  One barrier per chunk.
@@ -1095,7 +1095,7 @@ __global__ __launch_bounds__(256) void k_save(Dims d, const double *__restrict__
 //    into registers before the k loop, so their HBM latency hides behind the MFMAs;
 //    the epilogue is adds and stores only (stores drain while the next block runs).
 // ============================================================================
-constexpr int AKC = 16, ALD = ASM_TILE + 16, ASM_THREADS = 512;
+constexpr int AKC = ASM_KC, ALD = ASM_TILE + 16, ASM_THREADS = 512;
 
 __global__ __launch_bounds__(ASM_THREADS, 1) void k_assemble(Dims d, const double *__restrict__ Lb, int LDB,
                                                              int kext, const double *__restrict__ wsum,
@@ -1124,25 +1124,25 @@ __global__ __launch_bounds__(ASM_THREADS, 1) void k_assemble(Dims d, const doubl
                 old[u][v][g] = (a < p && b <= a) ? St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r] : 0.0;
             }
         }
-    // global -> LDS: thread t stages row (t >> 2) of both panels, k = 4 (t & 3) .. +3
+    // global -> LDS: thread t stages row (t >> 2) of both panels, k = 8 (t & 3) .. +7
     const int srow = t >> 2, sq = t & 3;
     const int ga = T.x * ASM_TILE + srow, gb = T.y * ASM_TILE + srow;
     const bool va = ga < p, vb = gb < p;
-    const double *pa = Lb + (size_t)(va ? ga : 0) * LDB + 4 * sq;
-    const double *pb = Lb + (size_t)(vb ? gb : 0) * LDB + 4 * sq;
+    const double *pa = Lb + (size_t)(va ? ga : 0) * LDB + 8 * sq;
+    const double *pb = Lb + (size_t)(vb ? gb : 0) * LDB + 8 * sq;
     const d2 zero2 = {0.0, 0.0};
-    d2 ra[2], rb[2];
+    d2 ra[4], rb[4];
     auto gload = [&](int kc) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 4; ++i) {
             ra[i] = va ? *reinterpret_cast<const d2 *>(pa + kc + 2 * i) : zero2;
             rb[i] = vb ? *reinterpret_cast<const d2 *>(pb + kc + 2 * i) : zero2;
         }
     };
     auto lstore = [&](int buf) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int k = 4 * sq + 2 * i;
+        for (int i = 0; i < 4; ++i) {
+            const int k = 8 * sq + 2 * i;
             As[buf][k][srow] = ra[i].x;
             As[buf][k + 1][srow] = ra[i].y;
             Bs[buf][k][srow] = rb[i].x;
