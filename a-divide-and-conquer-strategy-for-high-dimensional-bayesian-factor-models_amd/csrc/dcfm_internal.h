@@ -34,7 +34,7 @@ namespace dcfm {
 constexpr int KP = 32;         // padded factor width of the narrow (K <= 32) kernels
 constexpr int KP_MAX = 128;    // widest supported padding (K <= 128, config c4 has K = 100)
 constexpr int ASM_TILE = 128;  // covariance-assembly output tile
-constexpr int ASM_KC = 32;            // k_assemble's k chunk (kext, LDB are multiples)
+constexpr int ASM_KC = 16;            // k_assemble's k chunk (kext, LDB are multiples)
 
 struct Dims {
     int n, P, g, K, G;          // G = local shards

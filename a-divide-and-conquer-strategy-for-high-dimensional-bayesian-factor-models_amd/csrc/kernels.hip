@@ -1080,56 +1080,37 @@ __global__ __launch_bounds__(256) void k_save(Dims d, const double *__restrict__
 // k_assemble: Sigma[a][b] += (coef(a,b)/effsamp) sum_kk Lb[a][kk] Lb[b][kk]
 //                            + [a==b] wsum[a]/effsamp                       dc:184-195
 // coef = 1 inside a diagonal shard block (Lambda_r Lambda_r' + Omega_r), rho
-// across blocks (rho Lambda_r Lambda_c').  Lower-triangle 128x128 tiles only, one
-// tile per 512-thread block, one block per CU (2 waves per SIMD).
-//  * Tile order (dcfm_create): 8 x 8-tile supertiles, XCD-contiguous (xcd_remap), so the
-//    ~32 tiles an XCD has in flight share 8 row panels and 8 column panels of Lb in
-//    its L2 instead of streaming a new column panel per tile from the Infinity Cache.
-//    The tile's place in the rank's packed Sigma block comes from (ti, tj).
-//  * 8 waves in 2 x 4, each 64 x 32 = 4 x 2 tiles of v_mfma_f64_16x16x4.  The k extent
-//    (batch x K) runs in chunks of 32 through double-buffered LDS (147 KB), stored k-major with a
-//    144-double pitch (an operand read, 16 consecutive rows x 4 k, is a conflict-free
-//    ds_read_b64); the next chunk's global loads are in flight during the current
-//    chunk's MFMAs.  One barrier per chunk.
-//  * The tile's old Sigma values (the read half of the read-modify-write) are loaded
-//    into registers before the k loop, so their HBM latency hides behind the MFMAs;
-//    the epilogue is adds and stores only (stores drain while the next block runs).
+// across blocks (rho Lambda_r Lambda_c').  Lower-triangle 128x128 tiles only, in
+// 8 x 8-tile supertiles (dcfm_create), XCD-contiguous (xcd_remap): the tiles an XCD
+// has in flight share 8 row and 8 column panels of Lb in its L2.  The tile's place
+// in the rank's packed Sigma block comes from (ti, tj).
+// 4 waves in 2x2, each 64x64 = 4x4 tiles of v_mfma_f64_16x16x4.  The k extent
+// (batch x K) runs in chunks of 16 through double-buffered LDS, stored k-major
+// with a 144-double pitch: an MFMA operand read (16 consecutive rows x 4 k) is a
+// conflict-free ds_read_b64, and the next chunk's global loads are in flight
+// during the current chunk's 64 MFMAs per wave.  One barrier per chunk.
 // ============================================================================
-constexpr int AKC = ASM_KC, ALD = ASM_TILE + 16, ASM_THREADS = 512;
+constexpr int AKC = ASM_KC, ALD = ASM_TILE + 16, ASM_THREADS = 256;
 
-__global__ __launch_bounds__(ASM_THREADS, 1) void k_assemble(Dims d, const double *__restrict__ Lb, int LDB,
-                                                             int kext, const double *__restrict__ wsum,
-                                                             double inv_eff, const int2 *__restrict__ tiles,
-                                                             int T0, double *__restrict__ Sig) {
+__global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__restrict__ Lb, int LDB,
+                                                     int kext, const double *__restrict__ wsum,
+                                                     double inv_eff, const int2 *__restrict__ tiles, int T0,
+                                                     double *__restrict__ Sig) {
     __shared__ double As[2][AKC][ALD], Bs[2][AKC][ALD];
     __shared__ int shard_of[2][ASM_TILE];      // shard of the tile's rows / columns (epilogue coef)
     const int2 T = tiles[xcd_remap(blockIdx.x, gridDim.x)];
     double *__restrict__ St = Sig + (size_t)(tri(T.x) - tri(T0) + T.y) * ASM_TILE * ASM_TILE;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-    if (t < 2 * ASM_TILE) shard_of[t >> 7][t & 127] = ((t < ASM_TILE ? T.x : T.y) * ASM_TILE + (t & 127)) / d.P;
+    shard_of[t >> 7][t & 127] = ((t < ASM_TILE ? T.x : T.y) * ASM_TILE + (t & 127)) / d.P;
     const int r = lane & 15, q = lane >> 4;
     const int p = d.p;
-    const int wa = (wave >> 2) * 64, wb = (wave & 3) * 32;
-    const int a0 = T.x * ASM_TILE + wa, b0 = T.y * ASM_TILE + wb;
-    // ---- the old values of this thread's 32 tile elements: in flight during the k loop
-    double old[4][2][4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int a = a0 + 16 * u + q + 4 * g;
-#pragma unroll
-            for (int v = 0; v < 2; ++v) {
-                const int b = b0 + 16 * v + r;
-                old[u][v][g] = (a < p && b <= a) ? St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r] : 0.0;
-            }
-        }
-    // global -> LDS: thread t stages row (t >> 2) of both panels, k = 8 (t & 3) .. +7
-    const int srow = t >> 2, sq = t & 3;
+    const int wa = (wave >> 1) * 64, wb = (wave & 1) * 64;
+    // global -> LDS: thread t stages row (t >> 1) of both panels, k = 8 (t & 1) .. +7
+    const int srow = t >> 1, shalf = t & 1;
     const int ga = T.x * ASM_TILE + srow, gb = T.y * ASM_TILE + srow;
     const bool va = ga < p, vb = gb < p;
-    const double *pa = Lb + (size_t)(va ? ga : 0) * LDB + 8 * sq;
-    const double *pb = Lb + (size_t)(vb ? gb : 0) * LDB + 8 * sq;
+    const double *pa = Lb + (size_t)(va ? ga : 0) * LDB + 8 * shalf;
+    const double *pb = Lb + (size_t)(vb ? gb : 0) * LDB + 8 * shalf;
     const d2 zero2 = {0.0, 0.0};
     d2 ra[4], rb[4];
     auto gload = [&](int kc) {
@@ -1142,18 +1123,18 @@ __global__ __launch_bounds__(ASM_THREADS, 1) void k_assemble(Dims d, const doubl
     auto lstore = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int k = 8 * sq + 2 * i;
+            const int k = 8 * shalf + 2 * i;
             As[buf][k][srow] = ra[i].x;
             As[buf][k + 1][srow] = ra[i].y;
             Bs[buf][k][srow] = rb[i].x;
             Bs[buf][k + 1][srow] = rb[i].y;
         }
     };
-    d4 acc[4][2];
+    d4 acc[4][4];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int v = 0; v < 2; ++v) acc[u][v] = d4{0.0, 0.0, 0.0, 0.0};
+        for (int v = 0; v < 4; ++v) acc[u][v] = d4{0.0, 0.0, 0.0, 0.0};
     gload(0);
     lstore(0);
     __syncthreads();
@@ -1162,41 +1143,55 @@ __global__ __launch_bounds__(ASM_THREADS, 1) void k_assemble(Dims d, const doubl
         if (more) gload(kc + AKC);
 #pragma unroll
         for (int s4 = 0; s4 < AKC / 4; ++s4) {
-            double av[4], bv[2];
+            double a[4], b[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) av[u] = As[buf][4 * s4 + q][wa + 16 * u + r];
+            for (int u = 0; u < 4; ++u) a[u] = As[buf][4 * s4 + q][wa + 16 * u + r];
 #pragma unroll
-            for (int v = 0; v < 2; ++v) bv[v] = Bs[buf][4 * s4 + q][wb + 16 * v + r];
+            for (int v = 0; v < 4; ++v) b[v] = Bs[buf][4 * s4 + q][wb + 16 * v + r];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
 #pragma unroll
-                for (int v = 0; v < 2; ++v) acc[u][v] = mfma16x16x4(av[u], bv[v], acc[u][v]);
+                for (int v = 0; v < 4; ++v) acc[u][v] = mfma16x16x4(a[u], b[v], acc[u][v]);
         }
         if (more) lstore(buf ^ 1);
         __syncthreads();
     }
-    // ---- epilogue: lower-triangle update of the tile (tile-packed, row-major inside)
-    int sb[2];
+    // epilogue: lower-triangle read-modify-write of the tile (tile-packed, row-major inside),
+    // loads issued together (predicated, no branches around them), shard test from the LDS table
+    const int a0 = T.x * ASM_TILE + wa, b0 = T.y * ASM_TILE + wb;
+    int sb[4];
 #pragma unroll
-    for (int v = 0; v < 2; ++v) sb[v] = shard_of[1][wb + 16 * v + r];
+    for (int v = 0; v < 4; ++v) sb[v] = shard_of[1][wb + 16 * v + r];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < 4; ++u) {
+        double old[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int a = a0 + 16 * u + q + 4 * g;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int b = b0 + 16 * v + r;
+                const bool live = a < p && b <= a;
+                old[g][v] = live ? St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r] : 0.0;
+            }
+        }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int a = a0 + 16 * u + q + 4 * g;
             const int sa = shard_of[0][wa + 16 * u + q + 4 * g];
             const double dg = (a < p) ? wsum[a] * inv_eff : 0.0;
 #pragma unroll
-            for (int v = 0; v < 2; ++v) {
+            for (int v = 0; v < 4; ++v) {
                 const int b = b0 + 16 * v + r;
                 if (a < p && b <= a) {
                     const double coef = (sb[v] == sa) ? 1.0 : d.rho;
                     double val = coef * acc[u][v][g] * inv_eff;
                     if (a == b) val += dg;
-                    St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r] = old[u][v][g] + val;
+                    St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r] = old[g][v] + val;
                 }
             }
         }
+    }
 }
 
 // Column stripe [c0, c0 + nc) of the symmetric Sigmaout from this rank's tile-packed block
