@@ -73,6 +73,7 @@ struct dcfm_handle {
     hipEvent_t e_lam = nullptr, e_prep = nullptr, e_xchol = nullptr, e_batch = nullptr,
                e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
+    unsigned long long wc_ops = 0, wc_cs = 0;   // k_wcol launches with the ops / delta roles so far
     bool prep_valid = false;      // fused path: A / ZM hold the next iteration's Z operators
     bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
@@ -499,6 +500,9 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         double *tk = nullptr;
         ALLOC(tk, 1);
         b.ticket = reinterpret_cast<unsigned *>(tk);
+        double *sy = nullptr;
+        ALLOC(sy, 2);                     // zeroed: the k_wcol counters start at 0
+        b.sync = reinterpret_cast<unsigned long long *>(sy);
     }
     ALLOC(b.C, G * PP * KP);
     ALLOC(b.E, G * KP * KP);
@@ -1026,6 +1030,28 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     // operators run on the side stream
     static const bool nofuse = [] { const char *e = std::getenv("DCFM_NOFUSE"); return e && e[0] == '1'; }();
     const bool fused = d.kp == KP && !nofuse;
+    // one rank, fused: the operators, the previous iteration's delta chain and the Y pass
+    // share one launch per iteration (k_wcol); iteration t's delta chain runs in t+1's launch
+    // (or the trailing one at the end of this call)
+    const bool wc = fused && d.nranks == 1;
+    bool delta_pending = false;           // k_lambda of it - 1 ran, its delta chain not yet queued
+    auto wcol = [&](bool ops, bool delta, bool wpass, int64_t it) -> int {
+        const unsigned long long ot = (h->wc_ops + (ops ? 1 : 0)) * (unsigned long long)d.G;
+        const unsigned long long ct = (h->wc_cs + (delta ? 1 : 0)) * (unsigned long long)d.G;
+        launch_wcol(d, b, h->d.inject ? h->dr : h->gen[0], ops, delta, wpass, ot, ct, b.delta + h->cur * nkg,
+                    b.tau + h->cur * nkg, b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, s);
+        HIPC(h, hipGetLastError());
+        h->wc_ops += ops ? 1 : 0;
+        h->wc_cs += delta ? 1 : 0;
+        if (delta) {                                                      // iteration it - 1 is complete
+            h->cur ^= 1;
+            if (h->trace_n < h->trace_cap) {                              // dcfm_set_trace
+                launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4, s);
+                h->trace_n += 1;
+            }
+        }
+        return DCFM_OK;
+    };
     // generated draws: batches [b0, b0 + DB) aligned to this call's first iteration,
     // queued on sdraw into a slot whose previous batch the sweep has finished with
     int rc_gen = DCFM_OK;
@@ -1068,6 +1094,8 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     if (!fused) {
         HIPC(h, hipEventRecord(h->e_lam, s));      // Lambda/omega of the previous iteration are final
         h->prep_valid = false;
+    } else if (wc) {
+        h->prep_valid = false;                     // k_wcol forms every iteration's operators itself
     } else if (!h->prep_valid) {                   // operators of first_iter from the state as set
         KTimer t(h, DCFM_K_PREP, s);
         launch_colgram(d, b, false, s);
@@ -1087,7 +1115,14 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             if (it + batch_n < end_iter && gen_batch(it + batch_n, slot) < 0) return rc_gen;   // next batch
         }
         const DrawsDev &dr = d.inject ? h->dr : h->gen[slot];
-        if (fused) {
+        if (wc) {
+            {
+                KTimer t(h, DCFM_K_WPASS, s);
+                if (int rc = wcol(true, delta_pending, true, it)) return rc;
+            }
+            delta_pending = false;
+            { KTimer t(h, DCFM_K_ZDRAW, s); launch_zdraw(d, b, dr, it, s); }
+        } else if (fused) {
             { KTimer t(h, DCFM_K_WPASS, s); launch_wpass(d, b, s); }
             { KTimer t(h, DCFM_K_ZDRAW, s); launch_zxchol(d, b, dr, it, s); }
             if (d.nranks > 1) {   // one rank: k_xdraw sums the shard messages itself
@@ -1125,7 +1160,9 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s);
         }
         h->plam_valid = false;
-        if (fused && d.sgap) {   // several ranks: ONE all-gather of [column sums | A sum]
+        if (wc) {
+            delta_pending = true;     // column sums + delta chain ride in the next k_wcol
+        } else if (fused && d.sgap) {   // several ranks: ONE all-gather of [column sums | A sum]
             { KTimer t(h, DCFM_K_COLSUM, s); launch_colgram(d, b, true, s); }
             {   // Z operators + the local A sum (independent of delta), then the message
                 KTimer t(h, DCFM_K_DELTA, s);
@@ -1174,10 +1211,12 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             HIPC(h, hipEventRecord(h->e_used[slot], s));
             h->used_pending[slot] = true;
         }
-        h->cur ^= 1;
-        if (h->trace_n < h->trace_cap) {                                  // dcfm_set_trace
-            launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4, s);
-            h->trace_n += 1;
+        if (!wc) {
+            h->cur ^= 1;
+            if (h->trace_n < h->trace_cap) {                              // dcfm_set_trace
+                launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4, s);
+                h->trace_n += 1;
+            }
         }
         HIPC(h, hipGetLastError());
         if (it % h->cfg.thin == 0 && it > h->cfg.burnin) {                // dc:180
@@ -1194,6 +1233,10 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
                 if (rc) return rc;
             }
         }
+    }
+    if (delta_pending) {   // the last iteration's column sums + delta chain (trailing k_wcol)
+        KTimer t(h, DCFM_K_DELTA, s);
+        if (int rc = wcol(false, true, false, end_iter)) return rc;
     }
     int rc = flush_batch(h);
     if (rc) return rc;

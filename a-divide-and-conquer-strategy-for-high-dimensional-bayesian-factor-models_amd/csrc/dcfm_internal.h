@@ -67,6 +67,7 @@ struct Bufs {
     double *xa, *xa_all, *XM;          // per-rank sum of A, gathered sums, X-draw operators
     double *xpart;                     // k_deltaops chunk sums of A (8 x KP x KP)
     unsigned *ticket;                  // k_deltaops last-arrival ticket (0 between launches)
+    unsigned long long *sync;          // k_wcol hand-off counters [A_m out, column sums out] (monotonic)
     double *msg_all;                   // packed gather target (fused, nranks > 1), else null
     int2 *tiles;
     int ntiles, LDB;
@@ -104,6 +105,11 @@ void launch_colgram(const Dims &d, const Bufs &b, bool colsum, hipStream_t s);
 void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool delta,
                      const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
                      hipStream_t s, bool ops = true);
+// one rank, K <= 32: Z / X operators (ops), the previous iteration's column sums + delta
+// chain (delta) and the Y pass W (wpass) in one launch (k_wcol); returns the block count
+int launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, bool ops, bool delta, bool wpass,
+                unsigned long long ops_target, unsigned long long cs_target, const double *delta_in,
+                const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s);
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_asum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);

@@ -49,6 +49,8 @@ namespace dcfm {
 constexpr int PREP_SMEM = 4 * KP * (KP + 1) + 3 * TS16;
 // prep_gram: A_m (to HBM and LDS part[0]), NA, and Zprec's upper triangle into the
 // lower triangle of part[2]; prep_ops: the Z-draw operators from the LDS image.
+// PUB: A_m is published with agent-scope stores (read by other blocks of the same launch, k_wcol)
+template <bool PUB = false>
 __device__ __forceinline__ void prep_gram(const Dims &d, const double *__restrict__ Lam,
                                           const double *__restrict__ omega, double *__restrict__ A,
                                           double *__restrict__ ZM, int m, double *smem) {
@@ -87,7 +89,8 @@ __device__ __forceinline__ void prep_gram(const Dims &d, const double *__restric
     for (int u = 0; u < 4; ++u) {
         const int e = t + 256 * u, a = e / KP, b = e % KP;
         av[u] = (part[0][a][b] + part[1][a][b]) + (part[2][a][b] + part[3][a][b]);
-        Am[e] = av[u];
+        if (PUB) st_agent(Am + e, av[u]);
+        else Am[e] = av[u];
         Zm[3 * KP * KP + e] = -d.s1r * av[u];                       // NA
     }
     __syncthreads();
@@ -806,7 +809,7 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
 // k_colsum: sloc[m][k] = sum_{j<P} cpart[m][j][k], fixed order            dc:156 sum(mat)
 // block = (shard m, 32 columns); 8 row groups x 4 independent accumulators each.
 // ============================================================================
-template <int KW>
+template <int KW, bool PUB = false>
 __device__ __forceinline__ void colsum_tile(const Dims &d, const double *__restrict__ cpart,
                                             double *__restrict__ sloc, int m, int kt, double *smem) {
     double (*part)[32] = reinterpret_cast<double (*)[32]>(smem);
@@ -825,7 +828,8 @@ __device__ __forceinline__ void colsum_tile(const Dims &d, const double *__restr
         double tt = 0.0;
 #pragma unroll
         for (int g2 = 0; g2 < 8; ++g2) tt += part[g2][threadIdx.x];
-        sloc[(size_t)m * KW + k] = tt;
+        if (PUB) st_agent(sloc + (size_t)m * KW + k, tt);
+        else sloc[(size_t)m * KW + k] = tt;
     }
 }
 template <int KW>
@@ -866,7 +870,9 @@ __device__ __forceinline__ size_t sall_off(const Dims &d, int mg) {
     return (size_t)mg * KP + (d.sgap ? (size_t)(mg / d.G) * d.sgap : 0);
 }
 
-// one wave = one global shard m, lane l
+// one wave = one global shard m, lane l.  COH: sall was published by other blocks of the
+// same launch (k_wcol) and is read with agent-scope loads
+template <bool COH = false>
 __device__ __forceinline__ void delta_shard(const Dims &d, const double *__restrict__ sall,
                                             const double *__restrict__ delta_in, const double *__restrict__ tau_in,
                                             double *__restrict__ delta_out, double *__restrict__ tau_out,
@@ -878,7 +884,8 @@ __device__ __forceinline__ void delta_shard(const Dims &d, const double *__restr
         if (d.K >= 2) {
             // shard 1 (index 0) with its own pre-update delta_h
             const double d0 = act ? delta_in[lk] : 1.0;
-            const double T0 = wave_suffix_sum(act ? tau_in[lk] * sall[sall_off(d, 0) + lk] : 0.0, l);
+            const double s0 = act ? (COH ? ld_agent(sall + sall_off(d, 0) + lk) : sall[sall_off(d, 0) + lk]) : 0.0;
+            const double T0 = wave_suffix_sum(act ? tau_in[lk] * s0 : 0.0, l);
             const double G0 = act ? delta_G(d, dr, iter, 0, l) : 1.0;
             const double id0 = 1.0 / d0;
             const double d0new = delta_chain(d, l, T0, G0, id0, id0);
@@ -886,7 +893,8 @@ __device__ __forceinline__ void delta_shard(const Dims &d, const double *__restr
             if (m != 0) {
                 const size_t o = (size_t)m * KP + lk;
                 const double dold = act ? delta_in[o] : 1.0;
-                const double Tm = wave_suffix_sum(act ? tau_in[o] * sall[sall_off(d, m) + lk] : 0.0, l);
+                const double sm = act ? (COH ? ld_agent(sall + sall_off(d, m) + lk) : sall[sall_off(d, m) + lk]) : 0.0;
+                const double Tm = wave_suffix_sum(act ? tau_in[o] * sm : 0.0, l);
                 const double Gm = act ? delta_G(d, dr, iter, m, l) : 1.0;
                 const double idold = 1.0 / dold;
                 const double idref = (l == 0) ? idold : 1.0 / d0new;   // delta(1,:,m) | delta(h) (Q4)
@@ -903,7 +911,8 @@ __device__ __forceinline__ void delta_shard(const Dims &d, const double *__restr
                 for (int mm = 0; mm <= m; ++mm) {
                     const double dold = delta_in[(size_t)mm * KP];
                     const double tused = prefix * dold;
-                    const double bd = d.bd1 + (0.5 * (1.0 / dold)) * (tused * sall[sall_off(d, mm)]);
+                    const double smm = COH ? ld_agent(sall + sall_off(d, mm)) : sall[sall_off(d, mm)];
+                    const double bd = d.bd1 + (0.5 * (1.0 / dold)) * (tused * smm);
                     dnew = (1.0 / bd) * delta_G(d, dr, iter, mm, 0);
                     prefix = prefix * dnew;
                 }
@@ -968,12 +977,6 @@ __host__ __device__ inline int xsum_blocks(int G) {
     int chunk = 1;
     while (G / chunk > XSUM_BLOCKS && (G / chunk) % 2 == 0) chunk *= 2;
     return G / chunk;
-}
-__device__ __forceinline__ void st_agent(double *p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_agent(const double *p) {
-    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ bool last_arrival(unsigned *ticket, unsigned count, double *smem) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this thread's agent-scope stores are done
@@ -1055,6 +1058,124 @@ __global__ __launch_bounds__(256) void k_zxchol(Dims d, const double *__restrict
     }
     __syncthreads();
     xchol_factor(d, XM, smem);
+}
+
+// ============================================================================
+// k_wcol (one rank, K <= 32): the small per-iteration chains ride in the Y pass's launch.
+// Every block role below the Y-pass tiles is latency-bound (K x K factorisations, the
+// scalar delta chain, shard sums); as separate launches they cost ~30 us per iteration on
+// the critical path, inside k_wpass's launch they run on the CUs the pass leaves to them.
+// Roles, in block order (a consumer's producers always have lower block ids, so they are
+// dispatched first and a spinning consumer can never hold back its producer):
+//   OPS    [0, G)          prep_shard(m): A_m (published agent-coherent) and the Z
+//                          operators ZM_m of THIS iteration (from the incoming Lambda, omega)
+//   DELTA  [.., +G)        colsum tile m of the PREVIOUS iteration's psi o Lambda^2 (published)
+//   OPS    [.., +nxs)      wait for every A_m; chunk j's tree sum (a canonical subtree) ->
+//                          xpart; the last arrival sums the chunks (canonical tree), forms
+//                          Xprec = g I + rho sum A (dc:117) and the X operators XM (dc:118)
+//   DELTA  [.., +g/4)      wait for every column sum; the delta / tau chain of the previous
+//                          iteration (dc:155-165), 4 shards per block
+//   WPASS  [.., +nw)       W_m = Y_m (w o Lambda_m) tiles (dc:102-103,122-123)
+// Hand-offs: payload by agent-scope stores, s_waitcnt vmcnt(0), then a relaxed fetch-add on
+// a monotonic 64-bit counter; consumers poll the counter (s_sleep) up to the launch's target
+// and read the payload with agent-scope loads.
+// ============================================================================
+__device__ __forceinline__ void signal_count(unsigned long long *ctr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this thread's agent-scope stores are done
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_count(unsigned long long *ctr, unsigned long long target) {
+    if (threadIdx.x == 0)
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
+    __syncthreads();
+}
+
+struct WcolArgs {
+    int ops, delta, wpass;                 // roles present in this launch
+    unsigned long long ops_target;         // counter value once every A_m of this launch is out
+    unsigned long long cs_target;          // ... every column sum
+    const double *delta_in, *tau_in;       // the delta chain's buffers (previous iteration)
+    double *delta_out, *tau_out;
+    int64_t delta_iter;                    // iteration whose delta / tau the chain updates
+};
+
+__global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, DrawsDev dr, WcolArgs w) {
+    __shared__ double smem[PREP_SMEM];
+    const int G = d.G, nxs = xsum_blocks(G), ndel = (d.g + 3) / 4;
+    unsigned long long *ops_ctr = b.sync, *cs_ctr = b.sync + 1;
+    int blk = blockIdx.x;
+    if (w.ops) {
+        if (blk < G) {
+            prep_gram<true>(d, b.Lam, b.omega, b.A, b.ZM, blk, smem);
+            signal_count(ops_ctr);             // A_m is out; the operators follow
+            prep_ops(d, b.ZM, blk, smem);
+            return;
+        }
+        blk -= G;
+    }
+    if (w.delta) {
+        if (blk < G) {
+            colsum_tile<KP, true>(d, b.cpart, b.sloc, blk, 0, smem);
+            signal_count(cs_ctr);
+            return;
+        }
+        blk -= G;
+    }
+    if (w.ops) {
+        if (blk < nxs) {
+            wait_count(ops_ctr, w.ops_target);
+            const int t = threadIdx.x, j = blk;
+            const int chunk = G / nxs, m0 = j * chunk;   // a canonical subtree (xsum_blocks)
+            constexpr int NU = KP * KP / 256, NH = 2;    // elements per thread, per pass
+            // tree sums of NH elements at a time over 8 shards in flight (bounded registers)
+            auto sums = [&](int n, auto &&load, double *out) {
+                for (int u0 = 0; u0 < NU; u0 += NH) {
+                    TreeSum<double, 8> ts[NH];
+                    for (int k = 0; k < n; k += 8) {
+                        double v[NH][8];
+                        static_for<8>([&](auto U) {
+                            if (k + U < n)
+                                for (int u = 0; u < NH; ++u) v[u][U] = load(k + U, u0 + u);
+                        });
+                        static_for<8>([&](auto U) {
+                            if (k + U < n)
+                                for (int u = 0; u < NH; ++u) ts[u].push(v[u][U]);
+                        });
+                    }
+                    for (int u = 0; u < NH; ++u) out[u0 + u] = ts[u].total();
+                }
+            };
+            double vs[NU], xs[NU];
+            sums(chunk, [&](int k, int u) { return ld_agent(b.A + (size_t)(m0 + k) * KP * KP + t + 256 * u); }, vs);
+            for (int u = 0; u < NU; ++u) st_agent(b.xpart + (size_t)j * KP * KP + t + 256 * u, vs[u]);
+            if (!last_arrival(b.ticket, (unsigned)nxs, smem)) return;
+            sums(nxs, [&](int k, int u) { return k == j ? vs[u] : ld_agent(b.xpart + (size_t)k * KP * KP + t + 256 * u); },
+                 xs);
+            __syncthreads();                          // smem (last_arrival's flag) is reused below
+            for (int u = 0; u < NU; ++u) xprec_store(d, smem, t + 256 * u, xs[u]);
+            __syncthreads();
+            xchol_factor(d, b.XM, smem);
+            return;
+        }
+        blk -= nxs;
+    }
+    if (w.delta) {
+        if (blk < ndel) {
+            wait_count(cs_ctr, w.cs_target);
+            const int m = blk * 4 + (threadIdx.x >> 6);
+            if (m < d.g)
+                delta_shard<true>(d, b.sloc, w.delta_in, w.tau_in, w.delta_out, w.tau_out, dr, w.delta_iter, m,
+                                  threadIdx.x & 63);
+            return;
+        }
+        blk -= ndel;
+    }
+    if (w.wpass) {
+        const int nw = gridDim.x - (int)(blockIdx.x - blk);
+        const int q = xcd_remap(blk, nw);
+        wpass_tile<KP>(d, b.Y, b.Lam, b.omega, b.W, q, 0);
+    }
 }
 
 // ============================================================================
@@ -1413,6 +1534,21 @@ void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
     if (nb == 0) return;
     hipLaunchKernelGGL(k_deltaops, dim3(nb), dim3(256), 0, s, d, b.sall, delta_in, tau_in, delta_out, tau_out, dr,
                        iter, b.A, b.ZM, b.xpart, b.ticket, b.xa, ops ? 1 : 0);
+}
+// k_wcol launch: returns the blocks launched (0 when no role is requested)
+int launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, bool ops, bool delta, bool wpass,
+                unsigned long long ops_target, unsigned long long cs_target, const double *delta_in,
+                const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s) {
+    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (delta ? d.G + (d.g + 3) / 4 : 0) +
+                   (wpass ? (d.NP / 128) * d.G : 0);
+    if (nb == 0) return 0;
+    WcolArgs w;
+    w.ops = ops; w.delta = delta; w.wpass = wpass;
+    w.ops_target = ops_target; w.cs_target = cs_target;
+    w.delta_in = delta_in; w.tau_in = tau_in; w.delta_out = delta_out; w.tau_out = tau_out;
+    w.delta_iter = delta_iter;
+    hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, dr, w);
+    return nb;
 }
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return;

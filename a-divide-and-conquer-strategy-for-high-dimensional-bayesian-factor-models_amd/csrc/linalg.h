@@ -62,19 +62,19 @@ __device__ __forceinline__ double bcast16(double v) {
 // a binary counter: after i pushes, level l holds a finished 2^l-subtree iff bit l of i is
 // set.  Levels stay in registers (unrolled, constant indices); n < 2^TREE_LEVELS.
 constexpr int TREE_LEVELS = 16;
-template <class T>
+template <class T, int L = TREE_LEVELS>
 struct TreeSum {
-    T s[TREE_LEVELS];
+    T s[L];
     int i = 0;
     // static_for: the level indices are constants from the start, so s[] is promoted to registers
     __device__ __forceinline__ void push(T v) {
         bool open = true;   // still carrying
-        static_for<TREE_LEVELS>([&](auto L) {
+        static_for<L>([&](auto Q) {
             if (open) {
-                if ((i >> L) & 1) {
-                    v = s[L] + v;
+                if ((i >> Q) & 1) {
+                    v = s[Q] + v;
                 } else {
-                    s[L] = v;
+                    s[Q] = v;
                     open = false;
                 }
             }
@@ -85,9 +85,9 @@ struct TreeSum {
     __device__ __forceinline__ T total() const {
         T acc{};
         bool have = false;
-        static_for<TREE_LEVELS>([&](auto L) {
-            if ((i >> L) & 1) {
-                acc = have ? s[L] + acc : s[L];
+        static_for<L>([&](auto Q) {
+            if ((i >> Q) & 1) {
+                acc = have ? s[Q] + acc : s[Q];
                 have = true;
             }
         });
@@ -109,6 +109,15 @@ __device__ __forceinline__ T tree_sum_f(int n, F &&load) {
 // sum_{k < n} src[k * stride] in the canonical tree order
 __device__ __forceinline__ double tree_sum(const double *__restrict__ src, int n, size_t stride) {
     return tree_sum_f<double>(n, [&](int k) { return src[(size_t)k * stride]; });
+}
+
+// Agent-scope (all XCDs) coherent access for data handed between blocks of one launch:
+// relaxed atomics bypass the non-coherent per-XCD L2 copies (sc1), no L2 flush needed.
+__device__ __forceinline__ void st_agent(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double *p) {
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // 1/sqrt(x) to full fp64 precision: hardware estimate + 2 Newton steps
@@ -149,9 +158,14 @@ __device__ __forceinline__ double wave_suffix_sum(double v, int l) {
     return v;
 }
 
-// standard gamma of the delta site, h = 0-based factor index (dc:158,163), from the draw buffer
+// standard gamma of the delta site, h = 0-based factor index (dc:158,163): the injected
+// buffer, or — generated draws — the counter-addressed Philox variate itself (the value
+// k_draws writes), so the delta chain never depends on which draw-batch slot holds its
+// iteration (k_wcol runs iteration t's chain during iteration t+1)
 __device__ inline double delta_G(const Dims &d, const DrawsDev &dr, int64_t iter, int mg, int h) {
-    return dr.Gdelta[((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + h];
+    if (d.inject) return dr.Gdelta[((size_t)(iter - dr.first_iter) * d.g + mg) * d.K + h];
+    const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - h);
+    return Rng(d.seed).gamma(shape, SITE_DELTA, (uint32_t)mg, 0, (uint32_t)h, (uint32_t)iter);
 }
 
 // eta = sqrt(rho) X + sqrt(1-rho) Z    (dc:81,133) — one definition for every use
