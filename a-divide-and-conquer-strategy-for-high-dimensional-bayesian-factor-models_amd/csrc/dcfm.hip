@@ -73,7 +73,7 @@ struct dcfm_handle {
     hipEvent_t e_lam = nullptr, e_prep = nullptr, e_xchol = nullptr, e_batch = nullptr,
                e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
-    unsigned long long wc_ops = 0, wc_cs = 0;   // k_wcol launches with the ops / delta roles so far
+    unsigned long long wc_ops = 0;   // k_wcol launches with the operator roles so far (hand-off counter epoch)
     bool prep_valid = false;      // fused path: A / ZM hold the next iteration's Z operators
     bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
@@ -1030,27 +1030,17 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     // operators run on the side stream
     static const bool nofuse = [] { const char *e = std::getenv("DCFM_NOFUSE"); return e && e[0] == '1'; }();
     const bool fused = d.kp == KP && !nofuse;
-    // one rank, fused: the operators, the previous iteration's delta chain and the Y pass
-    // share one launch per iteration (k_wcol); iteration t's delta chain runs in t+1's launch
-    // (or the trailing one at the end of this call)
+    // one rank, fused: per iteration t, k_wcol = [Z operators + shard sum of A of t, column
+    // sums of t-1] beside the W pass of t; k_zxchol = [X operators, delta chain of t-1] beside
+    // the Z draw of t.  The last iteration's chain runs after the loop (k_delta).
     const bool wc = fused && d.nranks == 1;
     bool delta_pending = false;           // k_lambda of it - 1 ran, its delta chain not yet queued
-    auto wcol = [&](bool ops, bool delta, bool wpass, int64_t it) -> int {
-        const unsigned long long ot = (h->wc_ops + (ops ? 1 : 0)) * (unsigned long long)d.G;
-        const unsigned long long ct = (h->wc_cs + (delta ? 1 : 0)) * (unsigned long long)d.G;
-        launch_wcol(d, b, h->d.inject ? h->dr : h->gen[0], ops, delta, wpass, ot, ct, b.delta + h->cur * nkg,
-                    b.tau + h->cur * nkg, b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, s);
-        HIPC(h, hipGetLastError());
-        h->wc_ops += ops ? 1 : 0;
-        h->wc_cs += delta ? 1 : 0;
-        if (delta) {                                                      // iteration it - 1 is complete
-            h->cur ^= 1;
-            if (h->trace_n < h->trace_cap) {                              // dcfm_set_trace
-                launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4, s);
-                h->trace_n += 1;
-            }
+    auto after_delta = [&]() {            // iteration it - 1 is complete
+        h->cur ^= 1;
+        if (h->trace_n < h->trace_cap) {                                  // dcfm_set_trace
+            launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4, s);
+            h->trace_n += 1;
         }
-        return DCFM_OK;
     };
     // generated draws: batches [b0, b0 + DB) aligned to this call's first iteration,
     // queued on sdraw into a slot whose previous batch the sweep has finished with
@@ -1118,10 +1108,20 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         if (wc) {
             {
                 KTimer t(h, DCFM_K_WPASS, s);
-                if (int rc = wcol(true, delta_pending, true, it)) return rc;
+                h->wc_ops += 1;
+                launch_wcol(d, b, true, delta_pending, true, h->wc_ops * (unsigned long long)d.G, s);
             }
+            {
+                KTimer t(h, DCFM_K_ZDRAW, s);
+                if (delta_pending)
+                    launch_zxchol(d, b, dr, it, s, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+                                  b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1);
+                else
+                    launch_zxchol(d, b, dr, it, s);
+            }
+            HIPC(h, hipGetLastError());
+            if (delta_pending) after_delta();
             delta_pending = false;
-            { KTimer t(h, DCFM_K_ZDRAW, s); launch_zdraw(d, b, dr, it, s); }
         } else if (fused) {
             { KTimer t(h, DCFM_K_WPASS, s); launch_wpass(d, b, s); }
             { KTimer t(h, DCFM_K_ZDRAW, s); launch_zxchol(d, b, dr, it, s); }
@@ -1234,9 +1234,14 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             }
         }
     }
-    if (delta_pending) {   // the last iteration's column sums + delta chain (trailing k_wcol)
+    if (delta_pending) {   // the last iteration's column sums + delta chain
         KTimer t(h, DCFM_K_DELTA, s);
-        if (int rc = wcol(false, true, false, end_iter)) return rc;
+        launch_wcol(d, b, false, true, false, 0, s);
+        const DrawsDev &dr = d.inject ? h->dr : h->gen[0];   // gammas drawn in place unless injected
+        launch_delta(d, b, dr, end_iter - 1, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+                     b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);
+        HIPC(h, hipGetLastError());
+        after_delta();
     }
     int rc = flush_batch(h);
     if (rc) return rc;

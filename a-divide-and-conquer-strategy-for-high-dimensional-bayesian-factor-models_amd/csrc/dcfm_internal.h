@@ -105,12 +105,15 @@ void launch_colgram(const Dims &d, const Bufs &b, bool colsum, hipStream_t s);
 void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool delta,
                      const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
                      hipStream_t s, bool ops = true);
-// one rank, K <= 32: Z / X operators (ops), the previous iteration's column sums + delta
-// chain (delta) and the Y pass W (wpass) in one launch (k_wcol); returns the block count
-int launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, bool ops, bool delta, bool wpass,
-                unsigned long long ops_target, unsigned long long cs_target, const double *delta_in,
-                const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s);
-void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
+// one rank, K <= 32: the Z operators + shard sum of A (ops), the previous iteration's column
+// sums (colsum) and the Y pass W (wpass) in one launch (k_wcol)
+void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_target,
+                 hipStream_t s);
+// k_zxchol: X operators (block 0), optionally the delta chain of delta_iter (delta_in != null),
+// and the Z draw tiles
+void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
+                   const double *delta_in = nullptr, const double *tau_in = nullptr, double *delta_out = nullptr,
+                   double *tau_out = nullptr, int64_t delta_iter = 0);
 void launch_asum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,

@@ -61,17 +61,35 @@ __device__ __forceinline__ void prep_gram(const Dims &d, const double *__restric
     const double *L = Lam + (size_t)m * d.PP * KP;
     const double *w = omega + (size_t)m * d.PP;
     d4 a00 = {0, 0, 0, 0}, a01 = a00, a10 = a00, a11 = a00;
-    for (int tt = wave; tt < (d.PP >> 3); tt += 4) {
+    // rows j, j+1 of chunk tt: (w_j Lambda_ja) is the A operand [Zmsg, dc:98], Lambda_jb the B operand
+    auto ld = [&](int tt, d2 &wj, double (&l)[4]) {
         const int j = 8 * tt + 2 * q;
-        const d2 wj = *reinterpret_cast<const d2 *>(w + j);
-        const double lo0 = L[j * KP + r], hi0 = L[j * KP + 16 + r];
-        const double lo1 = L[(j + 1) * KP + r], hi1 = L[(j + 1) * KP + 16 + r];
-        // A operand (w_j Lambda_ja) [Zmsg, dc:98], B operand Lambda_jb
-        const double wl0 = lo0 * wj.x, wh0 = hi0 * wj.x, wl1 = lo1 * wj.y, wh1 = hi1 * wj.y;
-        a00 = mfma16x16x4(wl0, lo0, a00); a01 = mfma16x16x4(wl0, hi0, a01);
-        a10 = mfma16x16x4(wh0, lo0, a10); a11 = mfma16x16x4(wh0, hi0, a11);
-        a00 = mfma16x16x4(wl1, lo1, a00); a01 = mfma16x16x4(wl1, hi1, a01);
-        a10 = mfma16x16x4(wh1, lo1, a10); a11 = mfma16x16x4(wh1, hi1, a11);
+        wj = *reinterpret_cast<const d2 *>(w + j);
+        l[0] = L[j * KP + r]; l[1] = L[j * KP + 16 + r];
+        l[2] = L[(j + 1) * KP + r]; l[3] = L[(j + 1) * KP + 16 + r];
+    };
+    auto mm = [&](const d2 &wj, const double (&l)[4]) {
+        const double wl0 = l[0] * wj.x, wh0 = l[1] * wj.x, wl1 = l[2] * wj.y, wh1 = l[3] * wj.y;
+        a00 = mfma16x16x4(wl0, l[0], a00); a01 = mfma16x16x4(wl0, l[1], a01);
+        a10 = mfma16x16x4(wh0, l[0], a10); a11 = mfma16x16x4(wh0, l[1], a11);
+        a00 = mfma16x16x4(wl1, l[2], a00); a01 = mfma16x16x4(wl1, l[3], a01);
+        a10 = mfma16x16x4(wh1, l[2], a10); a11 = mfma16x16x4(wh1, l[3], a11);
+    };
+    const int nt = d.PP >> 3;
+    int tt = wave;
+    for (; tt + 12 < nt; tt += 16) {       // 4 chunks' loads in flight (latency-bound otherwise)
+        d2 wj[4];
+        double l[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ld(tt + 4 * u, wj[u], l[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) mm(wj[u], l[u]);
+    }
+    for (; tt < nt; tt += 4) {
+        d2 wj;
+        double l[4];
+        ld(tt, wj, l);
+        mm(wj, l);
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -816,12 +834,19 @@ __device__ __forceinline__ void colsum_tile(const Dims &d, const double *__restr
     const int k = 32 * kt + (threadIdx.x & 31), grp = threadIdx.x >> 5;
     const double *cp = cpart + (size_t)m * d.PP * KW + k;
     double s4[4] = {0.0, 0.0, 0.0, 0.0};
-    int j = grp;
-    for (; j + 24 < d.P; j += 32) {
+    // rows j = grp + 8 i: every load of a 320-row band in flight at once (one latency round
+    // per band instead of one per few rows), summed into 4 accumulators in row order
+    constexpr int RB = 40;
+    for (int j0 = 0; j0 < d.P; j0 += 8 * RB) {
+        double v[RB];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) s4[u] += cp[(size_t)(j + 8 * u) * KW];
+        for (int i = 0; i < RB; ++i) {
+            const int j = j0 + grp + 8 * i;
+            v[i] = j < d.P ? cp[(size_t)j * KW] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < RB; ++i) s4[i & 3] += v[i];
     }
-    for (; j < d.P; j += 8) s4[0] += cp[(size_t)j * KW];
     part[grp][threadIdx.x & 31] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     __syncthreads();
     if (threadIdx.x < 32) {
@@ -851,18 +876,31 @@ __global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict
 // (formerly) refresh Plam — now formed lazily in k_lambda.
 // ============================================================================
 
-// lane l < K holds delta_old_l, T_l, G_l, 1/delta_old_l and 1/dref_l; returns delta_new_l
+// lane l < K holds T_l, G_l, 1/delta_old_l and 1/dref_l; returns delta_new_l.
+// The chain  bd_h = b_h + (0.5 / dref_h) F_h T_h,  dn_h = G_h / bd_h,  F_{h+1} = F_h dn_h / dold_h
+// (F_0 = 1, b_0 = bd1, b_h = bd2) is a linear recurrence in y_h = 1 / F_h:
+//   y_{h+1} = alpha_h y_h + beta_h,  alpha_h = b_h dold_h / G_h,  beta_h = (0.5 / dref_h) T_h dold_h / G_h,
+// and dn_h = G_h y_h / (b_h y_h + c_h), c_h = (0.5 / dref_h) T_h.  The affine maps compose by a
+// wave scan (log2 steps) instead of K dependent steps; every term is positive, so the
+// reassociation moves the result by a few ulps only (dc:157-163).
 __device__ __forceinline__ double delta_chain(const Dims &d, int l, double T, double G, double idold, double idref) {
-    double F = 1.0, dnew = 1.0;
-    for (int h = 0; h < d.K; ++h) {
-        const double Th = readlane_d(T, h), ih = readlane_d(idref, h);
-        const double ioh = readlane_d(idold, h), Gh = readlane_d(G, h);
-        const double bd = (h == 0 ? d.bd1 : d.bd2) + (0.5 * ih) * (F * Th);   // dc:157,161
-        const double dn = (1.0 / bd) * Gh;                                      // dc:158,163
-        if (l == h) dnew = dn;
-        F = F * (dn * ioh);
+    const bool act = l < d.K;
+    const double bh = (l == 0) ? d.bd1 : d.bd2;
+    const double c = (0.5 * idref) * T;
+    const double inv = 1.0 / (idold * G);            // dold_h / G_h
+    double A = act ? bh * inv : 1.0, B = act ? c * inv : 0.0;   // identity map on idle lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {                // inclusive scan: (A,B)_l o ... o (A,B)_0
+        const double Ap = __shfl_up(A, o, 64), Bp = __shfl_up(B, o, 64);
+        if (l >= o) {
+            B = fma(A, Bp, B);
+            A = A * Ap;
+        }
     }
-    return dnew;
+    const double yin = A + B;                         // y_{l+1} (y_0 = 1)
+    const double yprev = __shfl_up(yin, 1, 64);
+    const double y = (l == 0) ? 1.0 : yprev;          // y_l
+    return act ? G * y / fma(bh, y, c) : 1.0;
 }
 
 // column sums of global shard mg in the gathered buffer (rank blocks padded by d.sgap)
@@ -1043,14 +1081,30 @@ __global__ __launch_bounds__(256) void k_deltaops(Dims d, const double *__restri
 }
 
 constexpr int ZX_SMEM = ZDRAW_SMEM > XCHOL_SMEM ? ZDRAW_SMEM : XCHOL_SMEM;
+// block 0: the X operators from the ranks' shard sums of A; blocks [1, 1 + ndel): the delta /
+// tau chain of the previous iteration (one rank: its column sums come from k_wcol), 4 shards
+// per block; the rest: k_zdraw tiles.  The chains finish inside the Z pass's time.
+struct DeltaArgs {
+    const double *delta_in, *tau_in;
+    double *delta_out, *tau_out;
+    int64_t iter;                          // iteration whose delta / tau the chain updates
+};
 __global__ __launch_bounds__(256) void k_zxchol(Dims d, const double *__restrict__ W,
                                                 const double *__restrict__ ZM, const double *__restrict__ X,
                                                 double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
                                                 int64_t iter, const double *__restrict__ xa_all,
-                                                double *__restrict__ XM) {
+                                                double *__restrict__ XM, int ndel, const double *__restrict__ sall,
+                                                DeltaArgs da) {
     __shared__ double smem[ZX_SMEM];
-    if (blockIdx.x > 0) {
-        zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blockIdx.x - 1, gridDim.x - 1), smem);
+    const int blk = blockIdx.x;
+    if (blk > ndel) {
+        zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blk - 1 - ndel, gridDim.x - 1 - ndel), smem);
+        return;
+    }
+    if (blk > 0) {
+        const int m = (blk - 1) * 4 + (threadIdx.x >> 6);
+        if (m < d.g)
+            delta_shard(d, sall, da.delta_in, da.tau_in, da.delta_out, da.tau_out, dr, da.iter, m, threadIdx.x & 63);
         return;
     }
     for (int e = threadIdx.x; e < KP * KP; e += 256) {   // the ranks' shard sums, canonical tree
@@ -1061,24 +1115,23 @@ __global__ __launch_bounds__(256) void k_zxchol(Dims d, const double *__restrict
 }
 
 // ============================================================================
-// k_wcol (one rank, K <= 32): the small per-iteration chains ride in the Y pass's launch.
-// Every block role below the Y-pass tiles is latency-bound (K x K factorisations, the
-// scalar delta chain, shard sums); as separate launches they cost ~30 us per iteration on
-// the critical path, inside k_wpass's launch they run on the CUs the pass leaves to them.
-// Roles, in block order (a consumer's producers always have lower block ids, so they are
-// dispatched first and a spinning consumer can never hold back its producer):
-//   OPS    [0, G)          prep_shard(m): A_m (published agent-coherent) and the Z
-//                          operators ZM_m of THIS iteration (from the incoming Lambda, omega)
-//   DELTA  [.., +G)        colsum tile m of the PREVIOUS iteration's psi o Lambda^2 (published)
-//   OPS    [.., +nxs)      wait for every A_m; chunk j's tree sum (a canonical subtree) ->
-//                          xpart; the last arrival sums the chunks (canonical tree), forms
-//                          Xprec = g I + rho sum A (dc:117) and the X operators XM (dc:118)
-//   DELTA  [.., +g/4)      wait for every column sum; the delta / tau chain of the previous
-//                          iteration (dc:155-165), 4 shards per block
-//   WPASS  [.., +nw)       W_m = Y_m (w o Lambda_m) tiles (dc:102-103,122-123)
-// Hand-offs: payload by agent-scope stores, s_waitcnt vmcnt(0), then a relaxed fetch-add on
-// a monotonic 64-bit counter; consumers poll the counter (s_sleep) up to the launch's target
-// and read the payload with agent-scope loads.
+// k_wcol (one rank, K <= 32): the small per-iteration work that feeds the Z / X draws rides
+// in the Y pass's launch.  As separate launches these latency-bound pieces (K x K
+// factorisations, shard sums, column sums) cost ~25 us per iteration on the critical path;
+// inside k_wpass's launch they run beside the pass.  Roles, in block order (a consumer's
+// producers always have lower block ids, so they are dispatched first and a spinning
+// consumer can never hold back its producer):
+//   OPS    [0, G)      prep_shard(m): A_m (published agent-coherent) and the Z operators ZM_m
+//                      of THIS iteration (from the incoming Lambda, omega)           dc:98-107
+//   COLSUM [.., +G)    column sums of the PREVIOUS iteration's psi o Lambda^2 (dc:156) for
+//                      the delta chain, which runs in the next launch (k_zxchol)
+//   OPS    [.., +nxs)  wait for every A_m; chunk j's tree sum (a canonical subtree) -> xpart;
+//                      the last arrival sums the chunks (canonical tree) into xa (dc:117);
+//                      k_zxchol's block 0 factors Xprec                              dc:112-118
+//   WPASS  [.., +nw)   W_m = Y_m (w o Lambda_m) tiles                          dc:102-103,122-123
+// Hand-off: payload by agent-scope stores, s_waitcnt vmcnt(0), then a relaxed fetch-add on a
+// monotonic 64-bit counter; consumers poll it (s_sleep) up to the launch's target and read
+// the payload with agent-scope loads.
 // ============================================================================
 __device__ __forceinline__ void signal_count(unsigned long long *ctr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this thread's agent-scope stores are done
@@ -1091,21 +1144,13 @@ __device__ __forceinline__ void wait_count(unsigned long long *ctr, unsigned lon
     __syncthreads();
 }
 
-struct WcolArgs {
-    int ops, delta, wpass;                 // roles present in this launch
-    unsigned long long ops_target;         // counter value once every A_m of this launch is out
-    unsigned long long cs_target;          // ... every column sum
-    const double *delta_in, *tau_in;       // the delta chain's buffers (previous iteration)
-    double *delta_out, *tau_out;
-    int64_t delta_iter;                    // iteration whose delta / tau the chain updates
-};
-
-__global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, DrawsDev dr, WcolArgs w) {
+__global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsum, int wpass,
+                                              unsigned long long ops_target) {
     __shared__ double smem[PREP_SMEM];
-    const int G = d.G, nxs = xsum_blocks(G), ndel = (d.g + 3) / 4;
-    unsigned long long *ops_ctr = b.sync, *cs_ctr = b.sync + 1;
+    const int G = d.G, nxs = xsum_blocks(G);
+    unsigned long long *ops_ctr = b.sync;
     int blk = blockIdx.x;
-    if (w.ops) {
+    if (ops) {
         if (blk < G) {
             prep_gram<true>(d, b.Lam, b.omega, b.A, b.ZM, blk, smem);
             signal_count(ops_ctr);             // A_m is out; the operators follow
@@ -1114,17 +1159,16 @@ __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, DrawsDev dr, WcolA
         }
         blk -= G;
     }
-    if (w.delta) {
+    if (colsum) {
         if (blk < G) {
-            colsum_tile<KP, true>(d, b.cpart, b.sloc, blk, 0, smem);
-            signal_count(cs_ctr);
+            colsum_tile<KP>(d, b.cpart, b.sloc, blk, 0, smem);
             return;
         }
         blk -= G;
     }
-    if (w.ops) {
+    if (ops) {
         if (blk < nxs) {
-            wait_count(ops_ctr, w.ops_target);
+            wait_count(ops_ctr, ops_target);
             const int t = threadIdx.x, j = blk;
             const int chunk = G / nxs, m0 = j * chunk;   // a canonical subtree (xsum_blocks)
             constexpr int NU = KP * KP / 256, NH = 2;    // elements per thread, per pass
@@ -1152,29 +1196,14 @@ __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, DrawsDev dr, WcolA
             if (!last_arrival(b.ticket, (unsigned)nxs, smem)) return;
             sums(nxs, [&](int k, int u) { return k == j ? vs[u] : ld_agent(b.xpart + (size_t)k * KP * KP + t + 256 * u); },
                  xs);
-            __syncthreads();                          // smem (last_arrival's flag) is reused below
-            for (int u = 0; u < NU; ++u) xprec_store(d, smem, t + 256 * u, xs[u]);
-            __syncthreads();
-            xchol_factor(d, b.XM, smem);
+            for (int u = 0; u < NU; ++u) b.xa[t + 256 * u] = xs[u];
             return;
         }
         blk -= nxs;
     }
-    if (w.delta) {
-        if (blk < ndel) {
-            wait_count(cs_ctr, w.cs_target);
-            const int m = blk * 4 + (threadIdx.x >> 6);
-            if (m < d.g)
-                delta_shard<true>(d, b.sloc, w.delta_in, w.tau_in, w.delta_out, w.tau_out, dr, w.delta_iter, m,
-                                  threadIdx.x & 63);
-            return;
-        }
-        blk -= ndel;
-    }
-    if (w.wpass) {
+    if (wpass) {
         const int nw = gridDim.x - (int)(blockIdx.x - blk);
-        const int q = xcd_remap(blk, nw);
-        wpass_tile<KP>(d, b.Y, b.Lam, b.omega, b.W, q, 0);
+        wpass_tile<KP>(d, b.Y, b.Lam, b.omega, b.W, xcd_remap(blk, nw), 0);
     }
 }
 
@@ -1535,25 +1564,25 @@ void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
     hipLaunchKernelGGL(k_deltaops, dim3(nb), dim3(256), 0, s, d, b.sall, delta_in, tau_in, delta_out, tau_out, dr,
                        iter, b.A, b.ZM, b.xpart, b.ticket, b.xa, ops ? 1 : 0);
 }
-// k_wcol launch: returns the blocks launched (0 when no role is requested)
-int launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, bool ops, bool delta, bool wpass,
-                unsigned long long ops_target, unsigned long long cs_target, const double *delta_in,
-                const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s) {
-    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (delta ? d.G + (d.g + 3) / 4 : 0) +
-                   (wpass ? (d.NP / 128) * d.G : 0);
-    if (nb == 0) return 0;
-    WcolArgs w;
-    w.ops = ops; w.delta = delta; w.wpass = wpass;
-    w.ops_target = ops_target; w.cs_target = cs_target;
-    w.delta_in = delta_in; w.tau_in = tau_in; w.delta_out = delta_out; w.tau_out = tau_out;
-    w.delta_iter = delta_iter;
-    hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, dr, w);
-    return nb;
+// k_wcol launch (one rank, K <= 32)
+void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_target,
+                 hipStream_t s) {
+    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / 128) * d.G : 0);
+    if (nb == 0) return;
+    hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, ops ? 1 : 0, colsum ? 1 : 0, wpass ? 1 : 0,
+                       ops_target);
 }
-void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
+                   const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
+                   int64_t delta_iter) {
     if (d.kp != KP) return;
-    hipLaunchKernelGGL(k_zxchol, dim3(1 + (d.NP / 128) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp, dr,
-                       iter, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
+    // delta blocks padded to keep the zdraw tiles' first block on XCD 0 (xcd_remap)
+    const int ndel = delta_in ? ((d.g + 3) / 4 + 1 + 7) / 8 * 8 - 1 : 0;
+    DeltaArgs da;
+    da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
+    da.iter = delta_iter;
+    hipLaunchKernelGGL(k_zxchol, dim3(1 + ndel + (d.NP / 128) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
+                       dr, iter, d.nranks > 1 ? b.xa_all : b.xa, b.XM, ndel, b.sall, da);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
     const int total = d.NP * d.kp;
