@@ -269,19 +269,54 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
 // k_zdraw: Z draw and per-shard X message as fp64 MFMA chains.   dc:101-107,121-123
 //   Z' = M1 W' + M2 X' + U eps'      (k_prep operators; columns = rows i)
 //   S' = W' + NA Z'                  (S_i = Xmsg'(Y_i - sqrt(1-rho) L Z_i))
-// block = (shard m, 128 rows), 4 waves x 2 tiles of 16 rows.  Operand lane map:
-// lane (c = lane&15, q = lane>>4) holds W[i0+c][8t+2q .. +1] (k-steps 2t+e);
-// the f64 C/D layout of Z' (row = q + 4r) is directly the B operand of the
-// NA Z' product (k-step r), so nothing crosses LDS.
+// block = (shard m, 64 rows), one 16-row tile per wave.  Operand lane map:
+// lane (c = lane&15, q = lane>>4) holds W[i0+c][8t+2q .. +1] (k-steps 2t+e); the three
+// products of Z' accumulate in separate registers (6 independent MFMA chains per wave,
+// 4 waves per SIMD: fp64 MFMA needs many chains in flight) and are added at the end
+// ((M1 W' + M2 X') + U eps').  The f64 C/D layout of Z' (row = q + 4r) is directly the B
+// operand of the NA Z' product (k-step r), so nothing crosses LDS.
 // ============================================================================
 constexpr int ZDRAW_SMEM = 4 * KP * (KP + 1);
+constexpr int ZROWS = 64;                      // rows per k_zdraw block
 __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restrict__ W,
                                            const double *__restrict__ ZM, const double *__restrict__ X,
                                            double *__restrict__ Z, double *__restrict__ Sp, const DrawsDev &dr,
                                            int64_t iter, int w, double *smem) {
     double (*Ms)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);   // M1, M2, U, NA
-    const int nrb = d.NP >> 7;
+    const int nrb = d.NP / ZROWS;
     const int m = w / nrb, rb = w % nrb;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, q = lane >> 4;
+    const int mg = d.shard0 + m;
+    const int i0 = rb * ZROWS + wave * 16;
+    const int i = i0 + c;
+    const bool live = i < d.n;
+    // this wave's operands first (in flight while the block stages the operators)
+    const double *Wi = W + ((size_t)m * d.NP + i) * KP + 2 * q;
+    const double *Xi = X + (size_t)i * KP + 2 * q;
+    d2 wv[4], xv[4], ev[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        wv[t] = *reinterpret_cast<const d2 *>(Wi + 8 * t);
+        xv[t] = *reinterpret_cast<const d2 *>(Xi + 8 * t);
+    }
+    {   // eps[i][kk], kk = 8t + 2q + e   (dc:104 normrnd; draw buffer, k_draws or injected)
+        const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int kk = 8 * t + 2 * q;
+            ev[t].x = (live && kk < d.K) ? nz[kk] : 0.0;
+            ev[t].y = (live && kk + 1 < d.K) ? nz[kk + 1] : 0.0;
+        }
+    }
+    double wr[2][4];   // W in the C/D layout (row = q + 4g of tile mt): the S' accumulator's start
+    {
+        const double *Wr = W + ((size_t)m * d.NP + i) * KP;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) wr[mt][g] = Wr[16 * mt + q + 4 * g];
+    }
     {
         const double *Zm = ZM + (size_t)m * 4 * KP * KP;
         for (int e = threadIdx.x; e < 4 * KP * KP; e += 256) {
@@ -290,76 +325,50 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
         }
     }
     __syncthreads();
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int c = lane & 15, q = lane >> 4;
-    const int mg = d.shard0 + m;
-#pragma unroll 1
-    for (int tile = 0; tile < 2; ++tile) {
-        const int i0 = rb * 128 + wave * 32 + tile * 16;
-        const int i = i0 + c;
-        const bool live = i < d.n;
-        const double *Wi = W + ((size_t)m * d.NP + i) * KP + 2 * q;
-        const double *Xi = X + (size_t)i * KP + 2 * q;
-        d2 wv[4], xv[4], ev[4];
+    d4 zw[2], zx[2], ze[2], as[2];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            wv[t] = *reinterpret_cast<const d2 *>(Wi + 8 * t);
-            xv[t] = *reinterpret_cast<const d2 *>(Xi + 8 * t);
-        }
-        // eps[i][kk], kk = 8t + 2q + e   (dc:104 normrnd; draw buffer, k_draws or injected)
-        {
-            const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K;
+    for (int mt = 0; mt < 2; ++mt) zw[mt] = zx[mt] = ze[mt] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int kk = 8 * t + 2 * q;
-                ev[t].x = (live && kk < d.K) ? nz[kk] : 0.0;
-                ev[t].y = (live && kk + 1 < d.K) ? nz[kk + 1] : 0.0;
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int kk = 8 * t + 2 * q + e;
+            const double we = e ? wv[t].y : wv[t].x, xe = e ? xv[t].y : xv[t].x;
+            const double ee = e ? ev[t].y : ev[t].x;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                zw[mt] = mfma16x16x4(Ms[0][16 * mt + c][kk], we, zw[mt]);
+                zx[mt] = mfma16x16x4(Ms[1][16 * mt + c][kk], xe, zx[mt]);
+                ze[mt] = mfma16x16x4(Ms[2][16 * mt + c][kk], ee, ze[mt]);
             }
         }
-        d4 az[2], as[2];
-        az[0] = az[1] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int kk = 8 * t + 2 * q + e;
-                const double we = e ? wv[t].y : wv[t].x, xe = e ? xv[t].y : xv[t].x;
-                const double ee = e ? ev[t].y : ev[t].x;
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    az[mt] = mfma16x16x4(Ms[0][16 * mt + c][kk], we, az[mt]);
-                    az[mt] = mfma16x16x4(Ms[1][16 * mt + c][kk], xe, az[mt]);
-                    az[mt] = mfma16x16x4(Ms[2][16 * mt + c][kk], ee, az[mt]);
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);   // bound the hoisting of operand reads
-        }
-        // S' = W' + NA Z'; accumulator starts from W in the C/D layout
-        const double *Wr = W + ((size_t)m * d.NP + i) * KP;
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) as[mt][g] = Wr[16 * mt + q + 4 * g];
-#pragma unroll
-        for (int mt2 = 0; mt2 < 2; ++mt2)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int kk = 16 * mt2 + 4 * g + q;
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) as[mt] = mfma16x16x4(Ms[3][16 * mt + c][kk], az[mt2][g], as[mt]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        double *Zr = Z + ((size_t)m * d.NP + i) * KP;
-        double *Sr = Sp + ((size_t)m * d.NP + i) * KP;
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int k = 16 * mt + q + 4 * g;
-                if (live) Zr[k] = (k < d.K) ? az[mt][g] : 0.0;
-                Sr[k] = live ? as[mt][g] : 0.0;
-            }
     }
+    d4 az[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+        az[mt] = (zw[mt] + zx[mt]) + ze[mt];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) as[mt][g] = wr[mt][g];
+    }
+    // S' = W' + NA Z'
+#pragma unroll
+    for (int mt2 = 0; mt2 < 2; ++mt2)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int kk = 16 * mt2 + 4 * g + q;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) as[mt] = mfma16x16x4(Ms[3][16 * mt + c][kk], az[mt2][g], as[mt]);
+        }
+    double *Zr = Z + ((size_t)m * d.NP + i) * KP;
+    double *Sr = Sp + ((size_t)m * d.NP + i) * KP;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int k = 16 * mt + q + 4 * g;
+            if (live) Zr[k] = (k < d.K) ? az[mt][g] : 0.0;
+            Sr[k] = live ? as[mt][g] : 0.0;
+        }
 }
 
 __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W,
@@ -1546,7 +1555,7 @@ void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s) {
 }
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return wide::launch_zdraw(d, b, dr, iter, s);
-    hipLaunchKernelGGL(k_zdraw, dim3((d.NP / 128) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
+    hipLaunchKernelGGL(k_zdraw, dim3((d.NP / ZROWS) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
                        dr, iter);
 }
 void launch_colgram(const Dims &d, const Bufs &b, bool colsum, hipStream_t s) {
@@ -1581,7 +1590,7 @@ void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t ite
     DeltaArgs da;
     da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
     da.iter = delta_iter;
-    hipLaunchKernelGGL(k_zxchol, dim3(1 + ndel + (d.NP / 128) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
+    hipLaunchKernelGGL(k_zxchol, dim3(1 + ndel + (d.NP / ZROWS) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
                        dr, iter, d.nranks > 1 ? b.xa_all : b.xa, b.XM, ndel, b.sall, da);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
