@@ -389,6 +389,12 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
                     "(got %g, %g, %g, %g); inject the draws for other hyper-parameters", c.as_, c.df, c.ad1, c.ad2);
     const int nranks = c.nranks < 1 ? 1 : c.nranks;
     if (c.rank < 0 || c.rank >= nranks) return fail(nullptr, DCFM_ERR_INVALID, "bad rank");
+    {   // the canonical shard-sum trees keep their levels in registers (TreeSum<.., 8 | 10>)
+        const int Gl = c.g / nranks, nxs = xsum_blocks(Gl);
+        if (c.g > 1023 || nxs > 255 || Gl / nxs > 255)
+            return fail(nullptr, DCFM_ERR_UNSUPPORTED, "g = %d shards (%d per rank): at most 1023, and a per-rank "
+                        "count whose odd part is below 256", c.g, Gl);
+    }
     if (c.g % nranks)
         return fail(nullptr, DCFM_ERR_UNSUPPORTED, "g = %d not divisible by nranks = %d", c.g, nranks);
     int ndev = 0;

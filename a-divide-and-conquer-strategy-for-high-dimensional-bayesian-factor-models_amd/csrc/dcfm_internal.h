@@ -74,6 +74,17 @@ struct Bufs {
     int T0, T1;                        // owned tile rows of Sigma (block-sharded, see above)
 };
 
+// k_wcol / k_deltaops shard sum of A
+constexpr int XSUM_BLOCKS = 8;
+// blocks of the A sum: G / chunk, chunk = a power of two dividing G, grown while more than
+// XSUM_BLOCKS chunks remain — so each chunk is a subtree of the canonical tree (TreeSum) and
+// the tree over the chunk sums is T(0, G)
+__host__ __device__ inline int xsum_blocks(int G) {
+    int chunk = 1;
+    while (G / chunk > XSUM_BLOCKS && (G / chunk) % 2 == 0) chunk *= 2;
+    return G / chunk;
+}
+
 // Sigma block-sharding helpers (host + device)
 __host__ __device__ inline long long tri(long long t) { return t * (t + 1) / 2; }
 // offset of the stored element (a, b), a >= b, in a rank's tile-packed Sigma (owner of tile row a/128)

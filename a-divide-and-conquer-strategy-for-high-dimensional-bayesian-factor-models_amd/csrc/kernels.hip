@@ -451,23 +451,35 @@ __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict_
 // k_xdraw: X' = Tx S' + Ux eps' as fp64 MFMA (operators from k_xchol).  S is the sum of
 // nsrc [NP][KP] slices in the canonical tree order (TreeSum): the ranks' gathered sums
 // (xall), or — one rank, fused chain — the G shard messages Sp themselves, which makes
-// k_xred's launch unnecessary.  16 rows per block: wave w sums the slices of columns
-// 8w .. 8w+7 (lane (c, q): row i0 + c, columns 8w + 2q, +1), wave 0 collects the four
-// column groups and runs the MFMAs.                                       dc:119-128
+// k_xred's launch unnecessary.  16 rows per block, 16 waves: wave (t, s) sums source chunk
+// s (a power-of-two run of slices, a canonical subtree; xdraw_chunks) of columns
+// 8t .. 8t+7 (lane (c, q): row i0 + c, columns 8t + 2q, +1) — the sum is latency-bound, so
+// the block keeps 16 waves of loads in flight; wave 0 adds the chunk sums (the tree over the
+// chunks) and runs the MFMAs.                                              dc:119-128
 // ============================================================================
-__global__ __launch_bounds__(256) void k_xdraw(Dims d, const double *__restrict__ src, int nsrc,
-                                               const double *__restrict__ XM,
-                                               double *__restrict__ X, DrawsDev dr, int64_t iter) {
+// source chunks of the X message sum: nch <= 4 runs of `chunk` slices, chunk a power of two
+__device__ __forceinline__ void xdraw_chunks(int nsrc, int &nch, int &chunk) {
+    chunk = 1;
+    while (nsrc / chunk > 4 && (nsrc / chunk) % 2 == 0) chunk *= 2;
+    nch = nsrc / chunk;
+    if (nch > 4) { nch = 1; chunk = nsrc; }
+}
+__global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict__ src, int nsrc,
+                                                const double *__restrict__ XM,
+                                                double *__restrict__ X, DrawsDev dr, int64_t iter) {
     __shared__ double Ms[2][KP][KP + 1];
-    __shared__ d2 part[3][64];
-    for (int e = threadIdx.x; e < 2 * KP * KP; e += 256) {
+    __shared__ d2 part[4][4][64];
+    for (int e = threadIdx.x; e < 2 * KP * KP; e += 1024) {
         const int mat = e / (KP * KP), rem = e % (KP * KP);
         Ms[mat][rem / KP][rem % KP] = XM[e];
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, q = lane >> 4;
+    const int tw = w & 3, sw = w >> 2;                 // column group, source chunk
     const int i0 = blockIdx.x * 16, i = i0 + c;
     const bool live = i < d.n;
     const size_t stride = (size_t)d.NP * KP;
+    int nch, chunk;
+    xdraw_chunks(nsrc, nch, chunk);     // chunk < 1024 (TreeSum levels below); dcfm_create caps g
     d2 sv[4], ev[4];
     if (w == 0) {   // eps of dc:126 (draw buffer), in flight during the sum
         const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K;
@@ -478,16 +490,19 @@ __global__ __launch_bounds__(256) void k_xdraw(Dims d, const double *__restrict_
             ev[t].y = (live && kk + 1 < d.K) ? nx[kk + 1] : 0.0;
         }
     }
-    {
-        const double *p = src + (size_t)i * KP + 8 * w + 2 * q;
-        const d2 tot = tree_sum_f<d2>(nsrc, [&](int rk) { return *reinterpret_cast<const d2 *>(p + (size_t)rk * stride); });
-        if (w > 0) part[w - 1][lane] = tot;
-        else sv[0] = tot;
+    if (sw < nch) {
+        const double *p = src + (size_t)sw * chunk * stride + (size_t)i * KP + 8 * tw + 2 * q;
+        part[sw][tw][lane] =
+            tree_sum_f<d2, 8, 10>(chunk, [&](int rk) { return *reinterpret_cast<const d2 *>(p + (size_t)rk * stride); });
     }
     __syncthreads();
     if (w > 0) return;
 #pragma unroll
-    for (int t = 1; t < 4; ++t) sv[t] = part[t - 1][lane];
+    for (int t = 0; t < 4; ++t) {
+        TreeSum<d2, 3> ts;
+        for (int k = 0; k < nch; ++k) ts.push(part[k][t][lane]);
+        sv[t] = ts.total();
+    }
     d4 ax[2];
     ax[0] = ax[1] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1016,15 +1031,6 @@ __global__ __launch_bounds__(256) void k_colgram(Dims d, const double *__restric
 // coherent across the XCDs' L2s without write-back / invalidate), ordered by the stores'
 // completion before the ticket — __threadfence's buffer_wbl2 / buffer_inv flush the XCD's
 // whole L2 and drop what co-resident blocks cache (measured +20 us next to a Y pass).
-constexpr int XSUM_BLOCKS = 8;
-// blocks of the A sum: G / chunk, chunk = a power of two dividing G, grown while more than
-// XSUM_BLOCKS chunks remain — so each chunk is a subtree of the canonical tree (TreeSum) and
-// the tree over the chunk sums is T(0, G)
-__host__ __device__ inline int xsum_blocks(int G) {
-    int chunk = 1;
-    while (G / chunk > XSUM_BLOCKS && (G / chunk) % 2 == 0) chunk *= 2;
-    return G / chunk;
-}
 __device__ __forceinline__ bool last_arrival(unsigned *ticket, unsigned count, double *smem) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this thread's agent-scope stores are done
     __syncthreads();
@@ -1608,9 +1614,9 @@ void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
                   bool from_shards) {
     if (d.kp != KP) return wide::launch_xdraw(d, b, dr, iter, s);
     if (from_shards)   // one rank: sum the G shard messages here (no k_xred)
-        hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(256), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter);
+        hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter);
     else
-        hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(256), 0, s, d, b.xall, d.nranks, b.XM, b.X, dr,
+        hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(1024), 0, s, d, b.xall, d.nranks, b.XM, b.X, dr,
                            iter);
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {

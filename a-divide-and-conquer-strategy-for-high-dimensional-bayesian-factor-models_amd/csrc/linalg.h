@@ -96,9 +96,9 @@ struct TreeSum {
 };
 // sum_{k < n} load(k) in the canonical tree order; the loads go out in batches of B
 // (predicated, all in flight together) before the batch is pushed
-template <class T, int B = 8, class F>
+template <class T, int B = 8, int L = TREE_LEVELS, class F>
 __device__ __forceinline__ T tree_sum_f(int n, F &&load) {
-    TreeSum<T> ts;
+    TreeSum<T, L> ts;
     for (int k = 0; k < n; k += B) {
         T v[B];
         static_for<B>([&](auto U) { if (k + U < n) v[U] = load(k + U); });
