@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
 // k_zdraw: Z draw and per-shard X message as fp64 MFMA chains.   dc:101-107,121-123
 //   Z' = M1 W' + M2 X' + U eps'      (k_prep operators; columns = rows i)
 //   S' = W' + NA Z'                  (S_i = Xmsg'(Y_i - sqrt(1-rho) L Z_i))
-// block = (shard m, 64 rows), one 16-row tile per wave.  Operand lane map:
+// block = (shard m, 128 rows), 8 waves, one 16-row tile per wave.  Operand lane map:
 // lane (c = lane&15, q = lane>>4) holds W[i0+c][8t+2q .. +1] (k-steps 2t+e); the three
 // products of Z' accumulate in separate registers (6 independent MFMA chains per wave,
 // 4 waves per SIMD: fp64 MFMA needs many chains in flight) and are added at the end
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
 // operand of the NA Z' product (k-step r), so nothing crosses LDS.
 // ============================================================================
 constexpr int ZDRAW_SMEM = 4 * KP * (KP + 1);
-constexpr int ZROWS = 64;                      // rows per k_zdraw block
+constexpr int ZROWS = 128, ZTHREADS = 512;     // rows and threads per k_zdraw block
 __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restrict__ W,
                                            const double *__restrict__ ZM, const double *__restrict__ X,
                                            double *__restrict__ Z, double *__restrict__ Sp, const DrawsDev &dr,
@@ -319,7 +319,9 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
     }
     {
         const double *Zm = ZM + (size_t)m * 4 * KP * KP;
-        for (int e = threadIdx.x; e < 4 * KP * KP; e += 256) {
+#pragma unroll
+        for (int u = 0; u < 4 * KP * KP / ZTHREADS; ++u) {
+            const int e = threadIdx.x + ZTHREADS * u;
             const int mat = e / (KP * KP), rem = e % (KP * KP);
             Ms[mat][rem / KP][rem % KP] = Zm[e];
         }
@@ -371,7 +373,7 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
         }
 }
 
-__global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W,
+__global__ __launch_bounds__(ZTHREADS) void k_zdraw(Dims d, const double *__restrict__ W,
                                                const double *__restrict__ ZM,
                                                const double *__restrict__ X,
                                                double *__restrict__ Z, double *__restrict__ Sp,
@@ -419,6 +421,7 @@ __device__ __forceinline__ void xchol_factor(const Dims &d, double *__restrict__
         chol_inv32(Sm, Us, Wk, lds_l, lds_u, lane);
     }
     __syncthreads();
+    if (wave >= 4) return;                 // blocks of more than 4 waves: the 4 tiles below
     // X = Rx^{-T}(Rx^{-1} sqrt(rho) S + eps) = Tx S + Ux eps,  Tx = sqrt(rho) Ux Ux'
     const int ti = wave >> 1, tj = wave & 1, j = lane & 15, q = lane >> 4;
     const d4 T = mfma_tile32<true>(Us, Us, ti, tj, lane);
@@ -1104,7 +1107,7 @@ struct DeltaArgs {
     double *delta_out, *tau_out;
     int64_t iter;                          // iteration whose delta / tau the chain updates
 };
-__global__ __launch_bounds__(256) void k_zxchol(Dims d, const double *__restrict__ W,
+__global__ __launch_bounds__(ZTHREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_zxchol(Dims d, const double *__restrict__ W,
                                                 const double *__restrict__ ZM, const double *__restrict__ X,
                                                 double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
                                                 int64_t iter, const double *__restrict__ xa_all,
@@ -1116,13 +1119,13 @@ __global__ __launch_bounds__(256) void k_zxchol(Dims d, const double *__restrict
         zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blk - 1 - ndel, gridDim.x - 1 - ndel), smem);
         return;
     }
-    if (blk > 0) {
-        const int m = (blk - 1) * 4 + (threadIdx.x >> 6);
+    if (blk > 0) {   // 8 shards per block, one wave each
+        const int m = (blk - 1) * (ZTHREADS / 64) + (threadIdx.x >> 6);
         if (m < d.g)
             delta_shard(d, sall, da.delta_in, da.tau_in, da.delta_out, da.tau_out, dr, da.iter, m, threadIdx.x & 63);
         return;
     }
-    for (int e = threadIdx.x; e < KP * KP; e += 256) {   // the ranks' shard sums, canonical tree
+    for (int e = threadIdx.x; e < KP * KP; e += ZTHREADS) {   // the ranks' shard sums, canonical tree
         xprec_store(d, smem, e, tree_sum(xa_all + e, d.nranks, (size_t)d.xstride));
     }
     __syncthreads();
@@ -1561,7 +1564,7 @@ void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s) {
 }
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return wide::launch_zdraw(d, b, dr, iter, s);
-    hipLaunchKernelGGL(k_zdraw, dim3((d.NP / ZROWS) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
+    hipLaunchKernelGGL(k_zdraw, dim3((d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
                        dr, iter);
 }
 void launch_colgram(const Dims &d, const Bufs &b, bool colsum, hipStream_t s) {
@@ -1592,11 +1595,11 @@ void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t ite
                    int64_t delta_iter) {
     if (d.kp != KP) return;
     // delta blocks padded to keep the zdraw tiles' first block on XCD 0 (xcd_remap)
-    const int ndel = delta_in ? ((d.g + 3) / 4 + 1 + 7) / 8 * 8 - 1 : 0;
+    const int ndel = delta_in ? ((d.g + 7) / 8 + 1 + 7) / 8 * 8 - 1 : 0;
     DeltaArgs da;
     da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
     da.iter = delta_iter;
-    hipLaunchKernelGGL(k_zxchol, dim3(1 + ndel + (d.NP / ZROWS) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
+    hipLaunchKernelGGL(k_zxchol, dim3(1 + ndel + (d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
                        dr, iter, d.nranks > 1 ? b.xa_all : b.xa, b.XM, ndel, b.sall, da);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
