@@ -73,7 +73,7 @@ struct dcfm_handle {
     hipEvent_t e_lam = nullptr, e_prep = nullptr, e_xchol = nullptr, e_batch = nullptr,
                e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
-    unsigned long long wc_ops = 0;   // k_wcol launches with the operator roles so far (hand-off counter epoch)
+    unsigned long long wc_ops = 0, wc_xm = 0;   // k_wcol / k_xdraw hand-off counter epochs
     bool prep_valid = false;      // fused path: A / ZM hold the next iteration's Z operators
     bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
@@ -1037,8 +1037,8 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     static const bool nofuse = [] { const char *e = std::getenv("DCFM_NOFUSE"); return e && e[0] == '1'; }();
     const bool fused = d.kp == KP && !nofuse;
     // one rank, fused: per iteration t, k_wcol = [Z operators + shard sum of A of t, column
-    // sums of t-1] beside the W pass of t; k_zxchol = [X operators, delta chain of t-1] beside
-    // the Z draw of t.  The last iteration's chain runs after the loop (k_delta).
+    // sums of t-1] beside the W pass of t; k_zdraw; k_xdraw = [X operators, delta chain of
+    // t-1] beside the X draw of t.  The last iteration's chain runs after the loop (k_delta).
     const bool wc = fused && d.nranks == 1;
     bool delta_pending = false;           // k_lambda of it - 1 ran, its delta chain not yet queued
     auto after_delta = [&]() {            // iteration it - 1 is complete
@@ -1117,17 +1117,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
                 h->wc_ops += 1;
                 launch_wcol(d, b, true, delta_pending, true, h->wc_ops * (unsigned long long)d.G, s);
             }
-            {
-                KTimer t(h, DCFM_K_ZDRAW, s);
-                if (delta_pending)
-                    launch_zxchol(d, b, dr, it, s, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
-                                  b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1);
-                else
-                    launch_zxchol(d, b, dr, it, s);
-            }
-            HIPC(h, hipGetLastError());
-            if (delta_pending) after_delta();
-            delta_pending = false;
+            { KTimer t(h, DCFM_K_ZDRAW, s); launch_zdraw(d, b, dr, it, s); }
         } else if (fused) {
             { KTimer t(h, DCFM_K_WPASS, s); launch_wpass(d, b, s); }
             { KTimer t(h, DCFM_K_ZDRAW, s); launch_zxchol(d, b, dr, it, s); }
@@ -1159,7 +1149,21 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             }
             HIPC(h, hipStreamWaitEvent(s, h->e_xchol, 0));
         }
-        { KTimer t(h, DCFM_K_XDRAW, s);  launch_xdraw(d, b, dr, it, s, fused && d.nranks == 1); }
+        if (wc) {   // + the X factorisation and the delta chain of it - 1
+            KTimer t(h, DCFM_K_XDRAW, s);
+            h->wc_xm += 1;
+            if (delta_pending)
+                launch_xdraw_wc(d, b, dr, it, h->wc_xm, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, s);
+            else
+                launch_xdraw_wc(d, b, dr, it, h->wc_xm, nullptr, nullptr, nullptr, nullptr, 0, s);
+            HIPC(h, hipGetLastError());
+            if (delta_pending) after_delta();
+            delta_pending = false;
+        } else {
+            KTimer t(h, DCFM_K_XDRAW, s);
+            launch_xdraw(d, b, dr, it, s, fused && d.nranks == 1);
+        }
         { KTimer t(h, DCFM_K_CPASS, s);  launch_cpass(d, b, s); }
         {
             KTimer t(h, DCFM_K_LAMBDA, s);

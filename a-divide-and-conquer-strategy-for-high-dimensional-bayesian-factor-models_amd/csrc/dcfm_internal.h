@@ -67,7 +67,7 @@ struct Bufs {
     double *xa, *xa_all, *XM;          // per-rank sum of A, gathered sums, X-draw operators
     double *xpart;                     // k_deltaops chunk sums of A (8 x KP x KP)
     unsigned *ticket;                  // k_deltaops last-arrival ticket (0 between launches)
-    unsigned long long *sync;          // k_wcol hand-off counters [A_m out, column sums out] (monotonic)
+    unsigned long long *sync;          // hand-off counters [k_wcol: A_m out, k_xdraw: XM out] (monotonic)
     double *msg_all;                   // packed gather target (fused, nranks > 1), else null
     int2 *tiles;
     int ntiles, LDB;
@@ -120,11 +120,12 @@ void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
 // sums (colsum) and the Y pass W (wpass) in one launch (k_wcol)
 void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_target,
                  hipStream_t s);
-// k_zxchol: X operators (block 0), optionally the delta chain of delta_iter (delta_in != null),
-// and the Z draw tiles
-void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
-                   const double *delta_in = nullptr, const double *tau_in = nullptr, double *delta_out = nullptr,
-                   double *tau_out = nullptr, int64_t delta_iter = 0);
+void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
+// one rank, K <= 32: k_xdraw with the X factorisation from xa (block 0, hand-off counter
+// b.sync[1] up to xm_target) and, when delta_in != null, the delta chain of delta_iter
+void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, unsigned long long xm_target,
+                     const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
+                     int64_t delta_iter, hipStream_t s);
 void launch_asum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,

@@ -411,6 +411,8 @@ __global__ __launch_bounds__(256) void k_asum(Dims d, const double *__restrict__
 // ============================================================================
 constexpr int XCHOL_SMEM = 2 * KP * (KP + 1) + TS16 * (KP + 1) + 3 * TS16 + 2;
 // smem = {Sm, Us, Wk, lds_l, lds_u, flag}; Sm (lower) holds Xprec's upper triangle on entry
+// PUB: XM is published with agent-scope stores (read by other blocks of the same launch, k_xdraw)
+template <bool PUB = false>
 __device__ __forceinline__ void xchol_factor(const Dims &d, double *__restrict__ XM, double *smem) {
     double (*Sm)[KP + 1] = reinterpret_cast<double (*)[KP + 1]>(smem);
     double (*Us)[KP + 1] = Sm + KP;
@@ -428,8 +430,13 @@ __device__ __forceinline__ void xchol_factor(const Dims &d, double *__restrict__
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
         const int a = 16 * ti + q + 4 * g, c = 16 * tj + j;
-        XM[a * KP + c] = d.sr * T[g];
-        XM[KP * KP + a * KP + c] = Us[a][c];
+        if (PUB) {
+            st_agent(XM + a * KP + c, d.sr * T[g]);
+            st_agent(XM + KP * KP + a * KP + c, Us[a][c]);
+        } else {
+            XM[a * KP + c] = d.sr * T[g];
+            XM[KP * KP + a * KP + c] = Us[a][c];
+        }
     }
 }
 
@@ -450,6 +457,20 @@ __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict_
     xchol_factor(d, XM, smem);
 }
 
+// hand-off between blocks of one launch (k_wcol, k_xdraw): payload by agent-scope stores,
+// s_waitcnt vmcnt(0), then a relaxed fetch-add on a monotonic 64-bit counter; consumers poll
+// it (s_sleep) up to the launch's target and read the payload with agent-scope loads
+__device__ __forceinline__ void signal_count(unsigned long long *ctr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this thread's agent-scope stores are done
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_count(unsigned long long *ctr, unsigned long long target) {
+    if (threadIdx.x == 0)
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
+    __syncthreads();
+}
+
 // ============================================================================
 // k_xdraw: X' = Tx S' + Ux eps' as fp64 MFMA (operators from k_xchol).  S is the sum of
 // nsrc [NP][KP] slices in the canonical tree order (TreeSum): the ranks' gathered sums
@@ -467,18 +488,53 @@ __device__ __forceinline__ void xdraw_chunks(int nsrc, int &nch, int &chunk) {
     nch = nsrc / chunk;
     if (nch > 4) { nch = 1; chunk = nsrc; }
 }
+// one wave = one global shard m of the delta / tau chain (defined with k_delta below)
+template <bool COH = false>
+__device__ __forceinline__ void delta_shard(const Dims &d, const double *__restrict__ sall,
+                                            const double *__restrict__ delta_in, const double *__restrict__ tau_in,
+                                            double *__restrict__ delta_out, double *__restrict__ tau_out,
+                                            const DrawsDev &dr, int64_t iter, int m, int t);
+struct DeltaArgs {
+    const double *delta_in, *tau_in;
+    double *delta_out, *tau_out;
+    int64_t iter;                          // iteration whose delta / tau the chain updates
+};
+// Roles of the one-rank launch (xroles != 0), in block order: block 0 factors Xprec from the
+// shard sum xa (dc:117-118) and publishes XM; blocks [1, 1 + ndel) run the previous
+// iteration's delta chain (16 shards per block; dc:155-165), on CUs the 63 row blocks leave
+// idle; the row blocks sum their messages first and wait for XM only before the MFMAs.
+constexpr int XD_SMEM = (2 * KP * (KP + 1) + 4 * 4 * 64 * 2) > XCHOL_SMEM ? (2 * KP * (KP + 1) + 4 * 4 * 64 * 2)
+                                                                          : XCHOL_SMEM;
 __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict__ src, int nsrc,
-                                                const double *__restrict__ XM,
-                                                double *__restrict__ X, DrawsDev dr, int64_t iter) {
-    __shared__ double Ms[2][KP][KP + 1];
-    __shared__ d2 part[4][4][64];
-    for (int e = threadIdx.x; e < 2 * KP * KP; e += 1024) {
-        const int mat = e / (KP * KP), rem = e % (KP * KP);
-        Ms[mat][rem / KP][rem % KP] = XM[e];
+                                                double *__restrict__ XM,
+                                                double *__restrict__ X, DrawsDev dr, int64_t iter, int xroles,
+                                                const double *__restrict__ xa, unsigned long long *xm_ctr,
+                                                unsigned long long xm_target, int ndel,
+                                                const double *__restrict__ sall, DeltaArgs da) {
+    __shared__ double smem[XD_SMEM];
+    int blk = blockIdx.x;
+    if (xroles) {
+        if (blk == 0) {
+            for (int e = threadIdx.x; e < KP * KP; e += 1024) xprec_store(d, smem, e, xa[e]);
+            __syncthreads();
+            xchol_factor<true>(d, XM, smem);
+            signal_count(xm_ctr);
+            return;
+        }
+        if (blk <= ndel) {
+            const int m = (blk - 1) * 16 + (threadIdx.x >> 6);
+            if (m < d.g)
+                delta_shard(d, sall, da.delta_in, da.tau_in, da.delta_out, da.tau_out, dr, da.iter, m,
+                            threadIdx.x & 63);
+            return;
+        }
+        blk -= 1 + ndel;
     }
+    double (*Ms)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);
+    d2 (*part)[4][64] = reinterpret_cast<d2 (*)[4][64]>(smem + 2 * KP * (KP + 1));
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, q = lane >> 4;
     const int tw = w & 3, sw = w >> 2;                 // column group, source chunk
-    const int i0 = blockIdx.x * 16, i = i0 + c;
+    const int i0 = blk * 16, i = i0 + c;
     const bool live = i < d.n;
     const size_t stride = (size_t)d.NP * KP;
     int nch, chunk;
@@ -497,6 +553,11 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
         const double *p = src + (size_t)sw * chunk * stride + (size_t)i * KP + 8 * tw + 2 * q;
         part[sw][tw][lane] =
             tree_sum_f<d2, 8, 10>(chunk, [&](int rk) { return *reinterpret_cast<const d2 *>(p + (size_t)rk * stride); });
+    }
+    if (xroles) wait_count(xm_ctr, xm_target);           // XM of this launch's block 0
+    for (int e = threadIdx.x; e < 2 * KP * KP; e += 1024) {
+        const int mat = e / (KP * KP), rem = e % (KP * KP);
+        Ms[mat][rem / KP][rem % KP] = xroles ? ld_agent(XM + e) : XM[e];
     }
     __syncthreads();
     if (w > 0) return;
@@ -937,7 +998,7 @@ __device__ __forceinline__ size_t sall_off(const Dims &d, int mg) {
 
 // one wave = one global shard m, lane l.  COH: sall was published by other blocks of the
 // same launch (k_wcol) and is read with agent-scope loads
-template <bool COH = false>
+template <bool COH>
 __device__ __forceinline__ void delta_shard(const Dims &d, const double *__restrict__ sall,
                                             const double *__restrict__ delta_in, const double *__restrict__ tau_in,
                                             double *__restrict__ delta_out, double *__restrict__ tau_out,
@@ -1099,30 +1160,16 @@ __global__ __launch_bounds__(256) void k_deltaops(Dims d, const double *__restri
 }
 
 constexpr int ZX_SMEM = ZDRAW_SMEM > XCHOL_SMEM ? ZDRAW_SMEM : XCHOL_SMEM;
-// block 0: the X operators from the ranks' shard sums of A; blocks [1, 1 + ndel): the delta /
-// tau chain of the previous iteration (one rank: its column sums come from k_wcol), 4 shards
-// per block; the rest: k_zdraw tiles.  The chains finish inside the Z pass's time.
-struct DeltaArgs {
-    const double *delta_in, *tau_in;
-    double *delta_out, *tau_out;
-    int64_t iter;                          // iteration whose delta / tau the chain updates
-};
-__global__ __launch_bounds__(ZTHREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_zxchol(Dims d, const double *__restrict__ W,
-                                                const double *__restrict__ ZM, const double *__restrict__ X,
-                                                double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
-                                                int64_t iter, const double *__restrict__ xa_all,
-                                                double *__restrict__ XM, int ndel, const double *__restrict__ sall,
-                                                DeltaArgs da) {
+// block 0: the X operators from the ranks' shard sums of A (several ranks, fused chain); the
+// rest: k_zdraw tiles
+__global__ __launch_bounds__(ZTHREADS) void k_zxchol(Dims d, const double *__restrict__ W,
+                                                     const double *__restrict__ ZM, const double *__restrict__ X,
+                                                     double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
+                                                     int64_t iter, const double *__restrict__ xa_all,
+                                                     double *__restrict__ XM) {
     __shared__ double smem[ZX_SMEM];
-    const int blk = blockIdx.x;
-    if (blk > ndel) {
-        zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blk - 1 - ndel, gridDim.x - 1 - ndel), smem);
-        return;
-    }
-    if (blk > 0) {   // 8 shards per block, one wave each
-        const int m = (blk - 1) * (ZTHREADS / 64) + (threadIdx.x >> 6);
-        if (m < d.g)
-            delta_shard(d, sall, da.delta_in, da.tau_in, da.delta_out, da.tau_out, dr, da.iter, m, threadIdx.x & 63);
+    if (blockIdx.x > 0) {
+        zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blockIdx.x - 1, gridDim.x - 1), smem);
         return;
     }
     for (int e = threadIdx.x; e < KP * KP; e += ZTHREADS) {   // the ranks' shard sums, canonical tree
@@ -1151,17 +1198,6 @@ __global__ __launch_bounds__(ZTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
 // monotonic 64-bit counter; consumers poll it (s_sleep) up to the launch's target and read
 // the payload with agent-scope loads.
 // ============================================================================
-__device__ __forceinline__ void signal_count(unsigned long long *ctr) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this thread's agent-scope stores are done
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void wait_count(unsigned long long *ctr, unsigned long long target) {
-    if (threadIdx.x == 0)
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
-    __syncthreads();
-}
-
 __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsum, int wpass,
                                               unsigned long long ops_target) {
     __shared__ double smem[PREP_SMEM];
@@ -1590,17 +1626,10 @@ void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass
     hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, ops ? 1 : 0, colsum ? 1 : 0, wpass ? 1 : 0,
                        ops_target);
 }
-void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
-                   const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
-                   int64_t delta_iter) {
+void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return;
-    // delta blocks padded to keep the zdraw tiles' first block on XCD 0 (xcd_remap)
-    const int ndel = delta_in ? ((d.g + 7) / 8 + 1 + 7) / 8 * 8 - 1 : 0;
-    DeltaArgs da;
-    da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
-    da.iter = delta_iter;
-    hipLaunchKernelGGL(k_zxchol, dim3(1 + ndel + (d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
-                       dr, iter, d.nranks > 1 ? b.xa_all : b.xa, b.XM, ndel, b.sall, da);
+    hipLaunchKernelGGL(k_zxchol, dim3(1 + (d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
+                       dr, iter, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
     const int total = d.NP * d.kp;
@@ -1616,11 +1645,23 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
                   bool from_shards) {
     if (d.kp != KP) return wide::launch_xdraw(d, b, dr, iter, s);
+    DeltaArgs da = {};
     if (from_shards)   // one rank: sum the G shard messages here (no k_xred)
-        hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter);
+        hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter, 0,
+                           nullptr, nullptr, 0ull, 0, nullptr, da);
     else
         hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(1024), 0, s, d, b.xall, d.nranks, b.XM, b.X, dr,
-                           iter);
+                           iter, 0, nullptr, nullptr, 0ull, 0, nullptr, da);
+}
+void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, unsigned long long xm_target,
+                     const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
+                     int64_t delta_iter, hipStream_t s) {
+    const int ndel = delta_in ? (d.g + 15) / 16 : 0;
+    DeltaArgs da;
+    da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
+    da.iter = delta_iter;
+    hipLaunchKernelGGL(k_xdraw, dim3(1 + ndel + cdiv(d.n, 16)), dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter,
+                       1, b.xa, b.sync + 1, xm_target, ndel, b.sall, da);
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(((d.PP + d.kp) / 32) * d.G * (d.kp / 32));
