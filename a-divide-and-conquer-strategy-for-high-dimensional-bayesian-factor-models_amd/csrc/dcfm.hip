@@ -73,7 +73,7 @@ struct dcfm_handle {
     hipEvent_t e_lam = nullptr, e_prep = nullptr, e_xchol = nullptr, e_batch = nullptr,
                e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
-    unsigned long long wc_ops = 0, wc_xm = 0;   // k_wcol / k_xdraw hand-off counter epochs
+    unsigned long long wc_ops = 0;   // k_wcol launches with the operator roles (hand-off counter epoch)
     bool prep_valid = false;      // fused path: A / ZM hold the next iteration's Z operators
     bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
@@ -507,7 +507,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         ALLOC(tk, 1);
         b.ticket = reinterpret_cast<unsigned *>(tk);
         double *sy = nullptr;
-        ALLOC(sy, 2);                     // zeroed: the k_wcol counters start at 0
+        ALLOC(sy, 2 + 256);               // zeroed: the hand-off counters start at 0 (<= 255 chunks)
         b.sync = reinterpret_cast<unsigned long long *>(sy);
     }
     ALLOC(b.C, G * PP * KP);
@@ -1036,9 +1036,9 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     // operators run on the side stream
     static const bool nofuse = [] { const char *e = std::getenv("DCFM_NOFUSE"); return e && e[0] == '1'; }();
     const bool fused = d.kp == KP && !nofuse;
-    // one rank, fused: per iteration t, k_wcol = [Z operators + shard sum of A of t, column
-    // sums of t-1] beside the W pass of t; k_zdraw; k_xdraw = [X operators, delta chain of
-    // t-1] beside the X draw of t.  The last iteration's chain runs after the loop (k_delta).
+    // one rank, fused: per iteration t, k_wcol = [Z and X operators of t, column sums of t-1]
+    // beside the W pass of t; k_zdraw; k_xdraw = [delta chain of t-1] beside the X draw of t.
+    // The last iteration's chain runs after the loop (k_delta).
     const bool wc = fused && d.nranks == 1;
     bool delta_pending = false;           // k_lambda of it - 1 ran, its delta chain not yet queued
     auto after_delta = [&]() {            // iteration it - 1 is complete
@@ -1115,7 +1115,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             {
                 KTimer t(h, DCFM_K_WPASS, s);
                 h->wc_ops += 1;
-                launch_wcol(d, b, true, delta_pending, true, h->wc_ops * (unsigned long long)d.G, s);
+                launch_wcol(d, b, true, delta_pending, true, h->wc_ops, s);
             }
             { KTimer t(h, DCFM_K_ZDRAW, s); launch_zdraw(d, b, dr, it, s); }
         } else if (fused) {
@@ -1151,12 +1151,11 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         }
         if (wc) {   // + the X factorisation and the delta chain of it - 1
             KTimer t(h, DCFM_K_XDRAW, s);
-            h->wc_xm += 1;
             if (delta_pending)
-                launch_xdraw_wc(d, b, dr, it, h->wc_xm, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+                launch_xdraw_wc(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
                                 b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, s);
             else
-                launch_xdraw_wc(d, b, dr, it, h->wc_xm, nullptr, nullptr, nullptr, nullptr, 0, s);
+                launch_xdraw_wc(d, b, dr, it, nullptr, nullptr, nullptr, nullptr, 0, s);
             HIPC(h, hipGetLastError());
             if (delta_pending) after_delta();
             delta_pending = false;

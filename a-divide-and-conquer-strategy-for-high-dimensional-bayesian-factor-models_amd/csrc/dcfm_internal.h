@@ -67,7 +67,7 @@ struct Bufs {
     double *xa, *xa_all, *XM;          // per-rank sum of A, gathered sums, X-draw operators
     double *xpart;                     // k_deltaops chunk sums of A (8 x KP x KP)
     unsigned *ticket;                  // k_deltaops last-arrival ticket (0 between launches)
-    unsigned long long *sync;          // hand-off counters [k_wcol: A_m out, k_xdraw: XM out] (monotonic)
+    unsigned long long *sync;          // hand-off counters (monotonic): [2 + chunk] = k_wcol A_m of the chunk out
     double *msg_all;                   // packed gather target (fused, nranks > 1), else null
     int2 *tiles;
     int ntiles, LDB;
@@ -118,14 +118,12 @@ void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
                      hipStream_t s, bool ops = true);
 // one rank, K <= 32: the Z operators + shard sum of A (ops), the previous iteration's column
 // sums (colsum) and the Y pass W (wpass) in one launch (k_wcol)
-void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_target,
+void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_epoch,
                  hipStream_t s);
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
-// one rank, K <= 32: k_xdraw with the X factorisation from xa (block 0, hand-off counter
-// b.sync[1] up to xm_target) and, when delta_in != null, the delta chain of delta_iter
-void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, unsigned long long xm_target,
-                     const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
-                     int64_t delta_iter, hipStream_t s);
+// one rank, K <= 32: k_xdraw plus, when delta_in != null, the delta chain of delta_iter
+void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
+                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s);
 void launch_asum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,

@@ -513,7 +513,7 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
                                                 const double *__restrict__ sall, DeltaArgs da) {
     __shared__ double smem[XD_SMEM];
     int blk = blockIdx.x;
-    if (xroles) {
+    if (xroles & 1) {   // producer of XM
         if (blk == 0) {
             for (int e = threadIdx.x; e < KP * KP; e += 1024) xprec_store(d, smem, e, xa[e]);
             __syncthreads();
@@ -521,14 +521,17 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
             signal_count(xm_ctr);
             return;
         }
-        if (blk <= ndel) {
-            const int m = (blk - 1) * 16 + (threadIdx.x >> 6);
+        blk -= 1;
+    }
+    if (xroles & 2) {   // the previous iteration's delta chain
+        if (blk < ndel) {
+            const int m = blk * 16 + (threadIdx.x >> 6);
             if (m < d.g)
                 delta_shard(d, sall, da.delta_in, da.tau_in, da.delta_out, da.tau_out, dr, da.iter, m,
                             threadIdx.x & 63);
             return;
         }
-        blk -= 1 + ndel;
+        blk -= ndel;
     }
     double (*Ms)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);
     d2 (*part)[4][64] = reinterpret_cast<d2 (*)[4][64]>(smem + 2 * KP * (KP + 1));
@@ -554,10 +557,10 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
         part[sw][tw][lane] =
             tree_sum_f<d2, 8, 10>(chunk, [&](int rk) { return *reinterpret_cast<const d2 *>(p + (size_t)rk * stride); });
     }
-    if (xroles) wait_count(xm_ctr, xm_target);           // XM of this launch's block 0
+    if (xroles & 1) wait_count(xm_ctr, xm_target);       // XM of this launch's block 0
     for (int e = threadIdx.x; e < 2 * KP * KP; e += 1024) {
         const int mat = e / (KP * KP), rem = e % (KP * KP);
-        Ms[mat][rem / KP][rem % KP] = xroles ? ld_agent(XM + e) : XM[e];
+        Ms[mat][rem / KP][rem % KP] = (xroles & 1) ? ld_agent(XM + e) : XM[e];
     }
     __syncthreads();
     if (w > 0) return;
@@ -1198,16 +1201,22 @@ __global__ __launch_bounds__(ZTHREADS) void k_zxchol(Dims d, const double *__res
 // monotonic 64-bit counter; consumers poll it (s_sleep) up to the launch's target and read
 // the payload with agent-scope loads.
 // ============================================================================
+// ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7)): the canonical tree of 8 (TreeSum), and of
+// any power-of-two n <= 8 when v[n..8) are zero (x + 0 = x)
+__device__ __forceinline__ double tree8(const double (&v)[8]) {
+    return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+}
+
 __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsum, int wpass,
-                                              unsigned long long ops_target) {
+                                              unsigned long long ops_epoch) {
     __shared__ double smem[PREP_SMEM];
-    const int G = d.G, nxs = xsum_blocks(G);
-    unsigned long long *ops_ctr = b.sync;
+    const int G = d.G, nxs = xsum_blocks(G), chunk = G / nxs;
+    unsigned long long *chunk_ctr = b.sync + 2;   // per chunk of shards: A_m published
     int blk = blockIdx.x;
     if (ops) {
         if (blk < G) {
             prep_gram<true>(d, b.Lam, b.omega, b.A, b.ZM, blk, smem);
-            signal_count(ops_ctr);             // A_m is out; the operators follow
+            signal_count(chunk_ctr + blk / chunk);   // A_m is out; the operators follow
             prep_ops(d, b.ZM, blk, smem);
             return;
         }
@@ -1221,36 +1230,58 @@ __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsu
         blk -= G;
     }
     if (ops) {
-        if (blk < nxs) {
-            wait_count(ops_ctr, ops_target);
-            const int t = threadIdx.x, j = blk;
-            const int chunk = G / nxs, m0 = j * chunk;   // a canonical subtree (xsum_blocks)
-            constexpr int NU = KP * KP / 256, NH = 2;    // elements per thread, per pass
-            // tree sums of NH elements at a time over 8 shards in flight (bounded registers)
-            auto sums = [&](int n, auto &&load, double *out) {
-                for (int u0 = 0; u0 < NU; u0 += NH) {
-                    TreeSum<double, 8> ts[NH];
-                    for (int k = 0; k < n; k += 8) {
-                        double v[NH][8];
-                        static_for<8>([&](auto U) {
-                            if (k + U < n)
-                                for (int u = 0; u < NH; ++u) v[u][U] = load(k + U, u0 + u);
-                        });
-                        static_for<8>([&](auto U) {
-                            if (k + U < n)
-                                for (int u = 0; u < NH; ++u) ts[u].push(v[u][U]);
-                        });
+        if (blk < nxs) {   // chunk j of the shard sum of A, then (last arrival) Xprec and its factors
+            const int t = threadIdx.x, j = blk, m0 = j * chunk;   // chunk: a canonical subtree
+            constexpr int NU = KP * KP / 256;
+            wait_count(chunk_ctr + j, ops_epoch * (unsigned long long)chunk);
+            double vs[NU];
+            if (chunk <= 8) {                                      // one round: the whole chunk
+                double v[NU][8];
+#pragma unroll
+                for (int u = 0; u < NU; ++u)
+#pragma unroll
+                    for (int U = 0; U < 8; ++U)
+                        v[u][U] = (U < chunk) ? ld_agent(b.A + (size_t)(m0 + U) * KP * KP + t + 256 * u) : 0.0;
+#pragma unroll
+                for (int u = 0; u < NU; ++u) vs[u] = tree8(v[u]);   // chunk is a power of two
+            } else {                                               // groups of 8 (subtrees), then their tree
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    TreeSum<double, 6> ts;
+                    for (int k = 0; k < chunk; k += 8) {
+                        double v[8];
+#pragma unroll
+                        for (int U = 0; U < 8; ++U) v[U] = ld_agent(b.A + (size_t)(m0 + k + U) * KP * KP + t + 256 * u);
+                        ts.push(tree8(v));
                     }
-                    for (int u = 0; u < NH; ++u) out[u0 + u] = ts[u].total();
+                    vs[u] = ts.total();
                 }
-            };
-            double vs[NU], xs[NU];
-            sums(chunk, [&](int k, int u) { return ld_agent(b.A + (size_t)(m0 + k) * KP * KP + t + 256 * u); }, vs);
+            }
+#pragma unroll
             for (int u = 0; u < NU; ++u) st_agent(b.xpart + (size_t)j * KP * KP + t + 256 * u, vs[u]);
             if (!last_arrival(b.ticket, (unsigned)nxs, smem)) return;
-            sums(nxs, [&](int k, int u) { return k == j ? vs[u] : ld_agent(b.xpart + (size_t)k * KP * KP + t + 256 * u); },
-                 xs);
-            for (int u = 0; u < NU; ++u) b.xa[t + 256 * u] = xs[u];
+            double xs[NU];
+            {   // canonical tree over the nxs <= 8 chunk sums (for a non-power-of-two G the chunks
+                // are single shards and nxs = G may exceed 8: groups of 8 into a TreeSum)
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    TreeSum<double, 8> ts;
+                    for (int k = 0; k < nxs; k += 8) {
+                        double v[8];
+#pragma unroll
+                        for (int U = 0; U < 8; ++U)
+                            v[U] = (k + U < nxs) ? (k + U == j ? vs[u] : ld_agent(b.xpart + (size_t)(k + U) * KP * KP + t + 256 * u))
+                                                 : 0.0;
+                        static_for<8>([&](auto U) { if (k + U < nxs) ts.push(v[U]); });
+                    }
+                    xs[u] = ts.total();
+                }
+            }
+            __syncthreads();                          // smem (last_arrival's flag) is reused below
+#pragma unroll
+            for (int u = 0; u < NU; ++u) xprec_store(d, smem, t + 256 * u, xs[u]);
+            __syncthreads();
+            xchol_factor(d, b.XM, smem);              // Xprec = g I + rho sum A (dc:117), Rx (dc:118)
             return;
         }
         blk -= nxs;
@@ -1619,12 +1650,12 @@ void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
                        iter, b.A, b.ZM, b.xpart, b.ticket, b.xa, ops ? 1 : 0);
 }
 // k_wcol launch (one rank, K <= 32)
-void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_target,
+void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_epoch,
                  hipStream_t s) {
     const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / 128) * d.G : 0);
     if (nb == 0) return;
     hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, ops ? 1 : 0, colsum ? 1 : 0, wpass ? 1 : 0,
-                       ops_target);
+                       ops_epoch);
 }
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return;
@@ -1653,15 +1684,14 @@ void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
         hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(1024), 0, s, d, b.xall, d.nranks, b.XM, b.X, dr,
                            iter, 0, nullptr, nullptr, 0ull, 0, nullptr, da);
 }
-void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, unsigned long long xm_target,
-                     const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
-                     int64_t delta_iter, hipStream_t s) {
+void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
+                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s) {
     const int ndel = delta_in ? (d.g + 15) / 16 : 0;
     DeltaArgs da;
     da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
     da.iter = delta_iter;
-    hipLaunchKernelGGL(k_xdraw, dim3(1 + ndel + cdiv(d.n, 16)), dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter,
-                       1, b.xa, b.sync + 1, xm_target, ndel, b.sall, da);
+    hipLaunchKernelGGL(k_xdraw, dim3(ndel + cdiv(d.n, 16)), dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter,
+                       delta_in ? 2 : 0, nullptr, nullptr, 0ull, ndel, b.sall, da);
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(((d.PP + d.kp) / 32) * d.G * (d.kp / 32));
