@@ -1085,6 +1085,9 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         h->gen_n[sl] = nb;
         return sl;
     };
+    // K <= 32 kernels draw their variates in place (Philox at the same counters k_draws uses);
+    // the wide kernels read the k_draws buffers, generated a batch ahead on the draw stream
+    const bool gen_draws = !d.inject && d.kp != KP;
     int slot = -1;
     int64_t batch0 = first_iter, batch_n = 0;
     if (!fused) {
@@ -1102,7 +1105,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
                 return rc;
     }
     for (int64_t it = first_iter; it < end_iter; ++it) {
-        if (!d.inject && (it == first_iter || it == batch0 + batch_n)) {
+        if (gen_draws && (it == first_iter || it == batch0 + batch_n)) {
             batch0 = it;
             batch_n = std::min<int64_t>(h->DB, end_iter - it);
             slot = gen_batch(it, -1);
@@ -1110,7 +1113,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             HIPC(h, hipStreamWaitEvent(s, h->e_drawn[slot], 0));
             if (it + batch_n < end_iter && gen_batch(it + batch_n, slot) < 0) return rc_gen;   // next batch
         }
-        const DrawsDev &dr = d.inject ? h->dr : h->gen[slot];
+        const DrawsDev &dr = d.inject ? h->dr : h->gen[gen_draws ? slot : 0];
         if (wc) {
             {
                 KTimer t(h, DCFM_K_WPASS, s);
@@ -1216,7 +1219,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
                              b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);
             }
         }
-        if (!d.inject && it == batch0 + batch_n - 1) {      // the batch's last consumer is queued
+        if (gen_draws && it == batch0 + batch_n - 1) {      // the batch's last consumer is queued
             HIPC(h, hipEventRecord(h->e_used[slot], s));
             h->used_pending[slot] = true;
         }

@@ -300,13 +300,23 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
         wv[t] = *reinterpret_cast<const d2 *>(Wi + 8 * t);
         xv[t] = *reinterpret_cast<const d2 *>(Xi + 8 * t);
     }
-    {   // eps[i][kk], kk = 8t + 2q + e   (dc:104 normrnd; draw buffer, k_draws or injected)
+    if (d.inject) {   // eps[i][kk], kk = 8t + 2q + e   (dc:104 normrnd; injected draw buffer)
         const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int kk = 8 * t + 2 * q;
             ev[t].x = (live && kk < d.K) ? nz[kk] : 0.0;
             ev[t].y = (live && kk + 1 < d.K) ? nz[kk + 1] : 0.0;
+        }
+    } else {          // generated here: Philox pair 4t + q of (SITE_Z, shard, row i) = normals kk, kk + 1
+        const Rng rng(d.seed);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int kk = 8 * t + 2 * q;
+            double n0 = 0.0, n1 = 0.0;
+            if (live && kk < d.K) rng.normal2(SITE_Z, (uint32_t)mg, (uint32_t)i, (uint32_t)(4 * t + q), (uint32_t)iter, n0, n1);
+            ev[t].x = n0;
+            ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
         }
     }
     double wr[2][4];   // W in the C/D layout (row = q + 4g of tile mt): the S' accumulator's start
@@ -373,7 +383,7 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
         }
 }
 
-__global__ __launch_bounds__(ZTHREADS) void k_zdraw(Dims d, const double *__restrict__ W,
+__global__ __launch_bounds__(ZTHREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_zdraw(Dims d, const double *__restrict__ W,
                                                const double *__restrict__ ZM,
                                                const double *__restrict__ X,
                                                double *__restrict__ Z, double *__restrict__ Sp,
@@ -543,13 +553,23 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
     int nch, chunk;
     xdraw_chunks(nsrc, nch, chunk);     // chunk < 1024 (TreeSum levels below); dcfm_create caps g
     d2 sv[4], ev[4];
-    if (w == 0) {   // eps of dc:126 (draw buffer), in flight during the sum
+    if (w == 0 && d.inject) {   // eps of dc:126 (injected draw buffer), in flight during the sum
         const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int kk = 8 * t + 2 * q;
             ev[t].x = (live && kk < d.K) ? nx[kk] : 0.0;
             ev[t].y = (live && kk + 1 < d.K) ? nx[kk + 1] : 0.0;
+        }
+    } else if (w == 0) {        // generated here (SITE_X, row i): Philox pair 4t + q
+        const Rng rng(d.seed);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int kk = 8 * t + 2 * q;
+            double n0 = 0.0, n1 = 0.0;
+            if (live && kk < d.K) rng.normal2(SITE_X, 0u, (uint32_t)i, (uint32_t)(4 * t + q), (uint32_t)iter, n0, n1);
+            ev[t].x = n0;
+            ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
         }
     }
     if (sw < nch) {
@@ -757,9 +777,27 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
     const double pin0 = rv0 ? pin[rowoff + r0] : 0.0, pin1 = rv1 ? pin[rowoff + r1] : 0.0;
     const double c0 = valid ? C[rowoff + r0] : 0.0, c1 = valid ? C[rowoff + r1] : 0.0;
     const uint32_t dk = drow * (uint32_t)d.K;
-    const double z0 = rv0 ? dr.NL[dk + r0] : 0.0, z1 = rv1 ? dr.NL[dk + r1] : 0.0;       // dc:142
-    const double G0 = rv0 ? dr.Gpsi[dk + r0] : 0.0, G1 = rv1 ? dr.Gpsi[dk + r1] : 0.0;   // dc:150
-    const double Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;                           // dc:170
+    double z0, z1, G0, G1, Gps;
+    if (d.inject) {   // the injected draw buffers
+        z0 = rv0 ? dr.NL[dk + r0] : 0.0; z1 = rv1 ? dr.NL[dk + r1] : 0.0;       // dc:142
+        G0 = rv0 ? dr.Gpsi[dk + r0] : 0.0; G1 = rv1 ? dr.Gpsi[dk + r1] : 0.0;   // dc:150
+        Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;                           // dc:170
+    } else {          // generated here, at the counters k_draws would use (identical values)
+        const Rng rng(d.seed);
+        const uint32_t it32 = (uint32_t)iter, mg32 = (uint32_t)mg, j32 = (uint32_t)jj;
+        // lane l draws normal pair l (indices 2l, 2l + 1); row index r comes from lane r / 2
+        double n0 = 0.0, n1 = 0.0;
+        if (valid && 2 * l < d.K) rng.normal2(SITE_LAMBDA, mg32, j32, (uint32_t)l, it32, n0, n1);
+        const int src0 = (qw << 4) | (r0 >> 1), src1 = (qw << 4) | (r1 >> 1);
+        const double a0 = __shfl(n0, src0, 64), b0 = __shfl(n1, src0, 64);
+        const double a1 = __shfl(n0, src1, 64), b1 = __shfl(n1, src1, 64);
+        z0 = rv0 ? ((r0 & 1) ? b0 : a0) : 0.0;
+        z1 = rv1 ? ((r1 & 1) ? b1 : a1) : 0.0;
+        const double shp = d.df * 0.5 + 0.5;
+        G0 = rv0 ? rng.gamma(shp, SITE_PSI, mg32, j32, (uint32_t)r0, it32) : 0.0;
+        G1 = rv1 ? rng.gamma(shp, SITE_PSI, mg32, j32, (uint32_t)r1, it32) : 0.0;
+        Gps = (valid && l == 0) ? rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg32, j32, 0u, it32) : 0.0;
+    }
     const double yyj = (valid && l == 0) ? yy[(uint32_t)(m * d.PP + jj)] : 0.0;
     const double *Ea = E + ((uint32_t)m * KP + r0) * KP, *Eb = E + ((uint32_t)m * KP + r1) * KP;
     constexpr int KH = KP / 2;       // rows < 16 only ever touch columns < 16 (lower triangle)
@@ -1165,7 +1203,7 @@ __global__ __launch_bounds__(256) void k_deltaops(Dims d, const double *__restri
 constexpr int ZX_SMEM = ZDRAW_SMEM > XCHOL_SMEM ? ZDRAW_SMEM : XCHOL_SMEM;
 // block 0: the X operators from the ranks' shard sums of A (several ranks, fused chain); the
 // rest: k_zdraw tiles
-__global__ __launch_bounds__(ZTHREADS) void k_zxchol(Dims d, const double *__restrict__ W,
+__global__ __launch_bounds__(ZTHREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_zxchol(Dims d, const double *__restrict__ W,
                                                      const double *__restrict__ ZM, const double *__restrict__ X,
                                                      double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
                                                      int64_t iter, const double *__restrict__ xa_all,

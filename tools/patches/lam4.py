@@ -1,0 +1,8 @@
+"""A/B: k_lambda limited to 4 waves per SIMD worth of registers."""
+import sys
+f = sys.argv[1] + "/kernels.hip"
+s = open(f).read()
+old = "__global__ __launch_bounds__(64) void k_lambda("
+assert old in s
+s = s.replace(old, "__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_lambda(")
+open(f, "w").write(s)
