@@ -467,6 +467,118 @@ __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict_
     xchol_factor(d, XM, smem);
 }
 
+// ============================================================================
+// k_draws: every standard variate one iteration consumes (SURVEY Appendix B), from
+// the counter-based Philox stream, into buffers with the injected-draw layout
+// (T = 1).  ALU-bound; it runs on the side stream one iteration ahead, overlapping
+// the HBM-bound Y passes, so the sweep kernels only load their variates.
+// Segments (wave-aligned): NZ pairs (local shards), NX pairs, NL pairs (local),
+// Gpsi (local), Gps (local), Gdelta (all g shards: every rank runs every chain).
+// Pointers are indexed by GLOBAL shard mg (as the injected full-g arrays are).
+// ============================================================================
+// Block plan of k_draws: every segment gets whole blocks, and a block covers
+// 256 / LR rows of one shard with LR in {16, 32, 64} lanes per row (the smallest that
+// holds a row's pairs / gammas, K <= 128), so a thread's (shard, row, index) comes
+// from shifts and one block-uniform division — no per-element integer division.
+// The rejection-sampled gammas (delta: one per thread; ps: one per thread) come first
+// in block order so their longer threads start early; the bulk normals follow.
+struct DrawPlan {
+    int lrn, lrg;                    // lanes per row: normal pairs, gamma row (Gpsi)
+    int nrb_n, nrb_p, nrb_g, nrb_s;  // row-blocks per shard: n rows, P rows (normals), P rows (Gpsi), Gps
+    int b_gdel, b_gps, b_gpsi, b_nz, b_nx, total;  // segment end blocks (cumulative); NL last
+};
+__host__ __device__ inline int lanes_for(int c) { return c <= 16 ? 16 : (c <= 32 ? 32 : 64); }
+__host__ __device__ inline DrawPlan draw_plan(const Dims &d) {
+    DrawPlan pl;
+    const int kp2 = (d.K + 1) / 2;
+    pl.lrn = lanes_for(kp2);
+    pl.lrg = lanes_for(d.K);
+    const int rpn = 256 / pl.lrn, rpg = 256 / pl.lrg;
+    pl.nrb_n = (d.n + rpn - 1) / rpn;
+    pl.nrb_p = (d.P + rpn - 1) / rpn;
+    pl.nrb_g = (d.P + rpg - 1) / rpg;
+    pl.nrb_s = (d.P + 255) / 256;
+    pl.b_gdel = (d.g * d.K + 255) / 256;          // Gdelta of all g shards
+    pl.b_gps = pl.b_gdel + d.G * pl.nrb_s;
+    pl.b_gpsi = pl.b_gps + d.G * pl.nrb_g;
+    pl.b_nz = pl.b_gpsi + d.G * pl.nrb_n;
+    pl.b_nx = pl.b_nz + pl.nrb_n;
+    pl.total = pl.b_nx + d.G * pl.nrb_p;
+    return pl;
+}
+
+// normals of one row: lane pair index pr = 0..kp2-1 -> out[2 pr], out[2 pr + 1]
+__device__ __forceinline__ void draw_normal_row(const Rng &rng, uint32_t site, uint32_t mg, uint32_t row,
+                                                uint32_t it, int K, int lane, int lr, double *out) {
+    const int kp2 = (K + 1) / 2;
+    for (int pr = lane; pr < kp2; pr += lr) {
+        double n0, n1;
+        rng.normal2(site, mg, row, (uint32_t)pr, it, n0, n1);
+        out[2 * pr] = n0;
+        if (2 * pr + 1 < K) out[2 * pr + 1] = n1;
+    }
+}
+
+// two launches per iteration: the gamma segments (rejection loops, more registers)
+// and the normal segments (high occupancy); b_off = first block of the launch
+// block b of the draw plan (256 threads)
+template <bool GAMMAS>
+__device__ __forceinline__ void draws_block(const Dims &d, const DrawsDev &dr, int64_t iter, const DrawPlan &pl,
+                                            int b) {
+    const Rng rng(d.seed);
+    const uint32_t it = (uint32_t)iter;
+    const int t = threadIdx.x, K = d.K;
+    if (GAMMAS) {
+    if (b < pl.b_gdel) {                               // dc:158,163 delta, K x g, all shards
+        const int x = b * 256 + t;
+        if (x >= d.g * K) return;
+        const int h = x % K, mg = x / K;
+        const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - h);
+        const_cast<double *>(dr.Gdelta)[(size_t)mg * K + h] = rng.gamma(shape, SITE_DELTA, (uint32_t)mg, 0, (uint32_t)h, it);
+        return;
+    }
+    if (b < pl.b_gps) {                                // dc:170 ps, P x g, shape as + n/2
+        const int bb = b - pl.b_gdel, m = bb / pl.nrb_s, j = (bb % pl.nrb_s) * 256 + t;
+        if (j >= d.P) return;
+        const uint32_t mg = (uint32_t)(d.shard0 + m);
+        const_cast<double *>(dr.Gps)[(size_t)mg * d.P + j] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg, (uint32_t)j, 0, it);
+        return;
+    }
+    if (b < pl.b_gpsi) {                               // dc:150 psi, device layout [g][P][K]
+        const int bb = b - pl.b_gps, m = bb / pl.nrb_g, rb = bb % pl.nrb_g;
+        const int sh = pl.lrg == 16 ? 4 : (pl.lrg == 32 ? 5 : 6);
+        const int j = rb * (256 / pl.lrg) + (t >> sh), lane = t & (pl.lrg - 1);
+        if (j >= d.P) return;
+        const uint32_t mg = (uint32_t)(d.shard0 + m);
+        double *o = const_cast<double *>(dr.Gpsi) + ((size_t)mg * d.P + j) * K;
+        const double shape = d.df * 0.5 + 0.5;
+        for (int k = lane; k < K; k += pl.lrg) o[k] = rng.gamma(shape, SITE_PSI, mg, (uint32_t)j, (uint32_t)k, it);
+        return;
+    }
+    return;
+    }
+    const int sh = pl.lrn == 16 ? 4 : (pl.lrn == 32 ? 5 : 6), lane = t & (pl.lrn - 1), rsub = t >> sh;
+    if (b < pl.b_nx) {                                 // dc:104 Z (K x n x g), dc:126 X (K x n)
+        const bool xs = b >= pl.b_nz;
+        const int bb = xs ? b - pl.b_nz : b - pl.b_gpsi;
+        const int m = xs ? 0 : bb / pl.nrb_n, rb = xs ? bb : bb % pl.nrb_n;
+        const int i = rb * (256 / pl.lrn) + rsub;
+        if (i >= d.n) return;
+        const uint32_t mg = xs ? 0u : (uint32_t)(d.shard0 + m);
+        double *o = xs ? const_cast<double *>(dr.NX) + (size_t)i * K
+                       : const_cast<double *>(dr.NZ) + ((size_t)mg * d.n + i) * K;
+        draw_normal_row(rng, xs ? SITE_X : SITE_Z, mg, (uint32_t)i, it, K, lane, pl.lrn, o);
+        return;
+    }
+    {                                                  // dc:142 Lambda (K x P x g)
+        const int bb = b - pl.b_nx, m = bb / pl.nrb_p, rb = bb % pl.nrb_p;
+        const int j = rb * (256 / pl.lrn) + rsub;
+        if (j >= d.P) return;
+        const uint32_t mg = (uint32_t)(d.shard0 + m);
+        draw_normal_row(rng, SITE_LAMBDA, mg, (uint32_t)j, it, K, lane, pl.lrn,
+                        const_cast<double *>(dr.NL) + ((size_t)mg * d.P + j) * K);
+    }
+}
 // hand-off between blocks of one launch (k_wcol, k_xdraw): payload by agent-scope stores,
 // s_waitcnt vmcnt(0), then a relaxed fetch-add on a monotonic 64-bit counter; consumers poll
 // it (s_sleep) up to the launch's target and read the payload with agent-scope loads
@@ -777,27 +889,11 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
     const double pin0 = rv0 ? pin[rowoff + r0] : 0.0, pin1 = rv1 ? pin[rowoff + r1] : 0.0;
     const double c0 = valid ? C[rowoff + r0] : 0.0, c1 = valid ? C[rowoff + r1] : 0.0;
     const uint32_t dk = drow * (uint32_t)d.K;
-    double z0, z1, G0, G1, Gps;
-    if (d.inject) {   // the injected draw buffers
-        z0 = rv0 ? dr.NL[dk + r0] : 0.0; z1 = rv1 ? dr.NL[dk + r1] : 0.0;       // dc:142
-        G0 = rv0 ? dr.Gpsi[dk + r0] : 0.0; G1 = rv1 ? dr.Gpsi[dk + r1] : 0.0;   // dc:150
-        Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;                           // dc:170
-    } else {          // generated here, at the counters k_draws would use (identical values)
-        const Rng rng(d.seed);
-        const uint32_t it32 = (uint32_t)iter, mg32 = (uint32_t)mg, j32 = (uint32_t)jj;
-        // lane l draws normal pair l (indices 2l, 2l + 1); row index r comes from lane r / 2
-        double n0 = 0.0, n1 = 0.0;
-        if (valid && 2 * l < d.K) rng.normal2(SITE_LAMBDA, mg32, j32, (uint32_t)l, it32, n0, n1);
-        const int src0 = (qw << 4) | (r0 >> 1), src1 = (qw << 4) | (r1 >> 1);
-        const double a0 = __shfl(n0, src0, 64), b0 = __shfl(n1, src0, 64);
-        const double a1 = __shfl(n0, src1, 64), b1 = __shfl(n1, src1, 64);
-        z0 = rv0 ? ((r0 & 1) ? b0 : a0) : 0.0;
-        z1 = rv1 ? ((r1 & 1) ? b1 : a1) : 0.0;
-        const double shp = d.df * 0.5 + 0.5;
-        G0 = rv0 ? rng.gamma(shp, SITE_PSI, mg32, j32, (uint32_t)r0, it32) : 0.0;
-        G1 = rv1 ? rng.gamma(shp, SITE_PSI, mg32, j32, (uint32_t)r1, it32) : 0.0;
-        Gps = (valid && l == 0) ? rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg32, j32, 0u, it32) : 0.0;
-    }
+    // the row's draws: injected, or generated for this iteration by k_wcol's draw role (one
+    // rank, K <= 32) / k_draws, at their counters — the same buffer layout either way
+    const double z0 = rv0 ? dr.NL[dk + r0] : 0.0, z1 = rv1 ? dr.NL[dk + r1] : 0.0;       // dc:142
+    const double G0 = rv0 ? dr.Gpsi[dk + r0] : 0.0, G1 = rv1 ? dr.Gpsi[dk + r1] : 0.0;   // dc:150
+    const double Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;                           // dc:170
     const double yyj = (valid && l == 0) ? yy[(uint32_t)(m * d.PP + jj)] : 0.0;
     const double *Ea = E + ((uint32_t)m * KP + r0) * KP, *Eb = E + ((uint32_t)m * KP + r1) * KP;
     constexpr int KH = KP / 2;       // rows < 16 only ever touch columns < 16 (lower triangle)
@@ -1246,7 +1342,7 @@ __device__ __forceinline__ double tree8(const double (&v)[8]) {
 }
 
 __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsum, int wpass,
-                                              unsigned long long ops_epoch) {
+                                              unsigned long long ops_epoch, int ldraws, DrawsDev dr, int64_t iter) {
     __shared__ double smem[PREP_SMEM];
     const int G = d.G, nxs = xsum_blocks(G), chunk = G / nxs;
     unsigned long long *chunk_ctr = b.sync + 2;   // per chunk of shards: A_m published
@@ -1323,6 +1419,19 @@ __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsu
             return;
         }
         blk -= nxs;
+    }
+    if (ldraws) {   // generated draws of this iteration's k_lambda (NL, Gpsi, Gps) into dr, T = 1
+        const DrawPlan pl = draw_plan(d);
+        const int ng = pl.b_gpsi - pl.b_gdel, nn = pl.total - pl.b_nx;
+        if (blk < ng) {
+            draws_block<true>(d, dr, iter, pl, pl.b_gdel + blk);
+            return;
+        }
+        if (blk < ng + nn) {
+            draws_block<false>(d, dr, iter, pl, pl.b_nx + blk - ng);
+            return;
+        }
+        blk -= ng + nn;
     }
     if (wpass) {
         const int nw = gridDim.x - (int)(blockIdx.x - blk);
@@ -1524,116 +1633,10 @@ __global__ __launch_bounds__(256) void k_eta(Dims d, const double *__restrict__ 
     }
 }
 
-// ============================================================================
-// k_draws: every standard variate one iteration consumes (SURVEY Appendix B), from
-// the counter-based Philox stream, into buffers with the injected-draw layout
-// (T = 1).  ALU-bound; it runs on the side stream one iteration ahead, overlapping
-// the HBM-bound Y passes, so the sweep kernels only load their variates.
-// Segments (wave-aligned): NZ pairs (local shards), NX pairs, NL pairs (local),
-// Gpsi (local), Gps (local), Gdelta (all g shards: every rank runs every chain).
-// Pointers are indexed by GLOBAL shard mg (as the injected full-g arrays are).
-// ============================================================================
-// Block plan of k_draws: every segment gets whole blocks, and a block covers
-// 256 / LR rows of one shard with LR in {16, 32, 64} lanes per row (the smallest that
-// holds a row's pairs / gammas, K <= 128), so a thread's (shard, row, index) comes
-// from shifts and one block-uniform division — no per-element integer division.
-// The rejection-sampled gammas (delta: one per thread; ps: one per thread) come first
-// in block order so their longer threads start early; the bulk normals follow.
-struct DrawPlan {
-    int lrn, lrg;                    // lanes per row: normal pairs, gamma row (Gpsi)
-    int nrb_n, nrb_p, nrb_g, nrb_s;  // row-blocks per shard: n rows, P rows (normals), P rows (Gpsi), Gps
-    int b_gdel, b_gps, b_gpsi, b_nz, b_nx, total;  // segment end blocks (cumulative); NL last
-};
-__host__ __device__ inline int lanes_for(int c) { return c <= 16 ? 16 : (c <= 32 ? 32 : 64); }
-__host__ __device__ inline DrawPlan draw_plan(const Dims &d) {
-    DrawPlan pl;
-    const int kp2 = (d.K + 1) / 2;
-    pl.lrn = lanes_for(kp2);
-    pl.lrg = lanes_for(d.K);
-    const int rpn = 256 / pl.lrn, rpg = 256 / pl.lrg;
-    pl.nrb_n = (d.n + rpn - 1) / rpn;
-    pl.nrb_p = (d.P + rpn - 1) / rpn;
-    pl.nrb_g = (d.P + rpg - 1) / rpg;
-    pl.nrb_s = (d.P + 255) / 256;
-    pl.b_gdel = (d.g * d.K + 255) / 256;          // Gdelta of all g shards
-    pl.b_gps = pl.b_gdel + d.G * pl.nrb_s;
-    pl.b_gpsi = pl.b_gps + d.G * pl.nrb_g;
-    pl.b_nz = pl.b_gpsi + d.G * pl.nrb_n;
-    pl.b_nx = pl.b_nz + pl.nrb_n;
-    pl.total = pl.b_nx + d.G * pl.nrb_p;
-    return pl;
-}
-
-// normals of one row: lane pair index pr = 0..kp2-1 -> out[2 pr], out[2 pr + 1]
-__device__ __forceinline__ void draw_normal_row(const Rng &rng, uint32_t site, uint32_t mg, uint32_t row,
-                                                uint32_t it, int K, int lane, int lr, double *out) {
-    const int kp2 = (K + 1) / 2;
-    for (int pr = lane; pr < kp2; pr += lr) {
-        double n0, n1;
-        rng.normal2(site, mg, row, (uint32_t)pr, it, n0, n1);
-        out[2 * pr] = n0;
-        if (2 * pr + 1 < K) out[2 * pr + 1] = n1;
-    }
-}
-
-// two launches per iteration: the gamma segments (rejection loops, more registers)
-// and the normal segments (high occupancy); b_off = first block of the launch
 template <bool GAMMAS>
 __global__ __launch_bounds__(256) void k_draws(Dims d, DrawsDev dr, int64_t iter) {
     const DrawPlan pl = draw_plan(d);
-    const Rng rng(d.seed);
-    const uint32_t it = (uint32_t)iter;
-    const int b = blockIdx.x + (GAMMAS ? 0 : pl.b_gpsi), t = threadIdx.x, K = d.K;
-    if (GAMMAS) {
-    if (b < pl.b_gdel) {                               // dc:158,163 delta, K x g, all shards
-        const int x = b * 256 + t;
-        if (x >= d.g * K) return;
-        const int h = x % K, mg = x / K;
-        const double shape = (h == 0) ? d.ad1 + 0.5 * d.P * d.K : d.ad2 + 0.5 * d.P * (d.K - h);
-        const_cast<double *>(dr.Gdelta)[(size_t)mg * K + h] = rng.gamma(shape, SITE_DELTA, (uint32_t)mg, 0, (uint32_t)h, it);
-        return;
-    }
-    if (b < pl.b_gps) {                                // dc:170 ps, P x g, shape as + n/2
-        const int bb = b - pl.b_gdel, m = bb / pl.nrb_s, j = (bb % pl.nrb_s) * 256 + t;
-        if (j >= d.P) return;
-        const uint32_t mg = (uint32_t)(d.shard0 + m);
-        const_cast<double *>(dr.Gps)[(size_t)mg * d.P + j] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg, (uint32_t)j, 0, it);
-        return;
-    }
-    if (b < pl.b_gpsi) {                               // dc:150 psi, device layout [g][P][K]
-        const int bb = b - pl.b_gps, m = bb / pl.nrb_g, rb = bb % pl.nrb_g;
-        const int sh = pl.lrg == 16 ? 4 : (pl.lrg == 32 ? 5 : 6);
-        const int j = rb * (256 / pl.lrg) + (t >> sh), lane = t & (pl.lrg - 1);
-        if (j >= d.P) return;
-        const uint32_t mg = (uint32_t)(d.shard0 + m);
-        double *o = const_cast<double *>(dr.Gpsi) + ((size_t)mg * d.P + j) * K;
-        const double shape = d.df * 0.5 + 0.5;
-        for (int k = lane; k < K; k += pl.lrg) o[k] = rng.gamma(shape, SITE_PSI, mg, (uint32_t)j, (uint32_t)k, it);
-        return;
-    }
-    return;
-    }
-    const int sh = pl.lrn == 16 ? 4 : (pl.lrn == 32 ? 5 : 6), lane = t & (pl.lrn - 1), rsub = t >> sh;
-    if (b < pl.b_nx) {                                 // dc:104 Z (K x n x g), dc:126 X (K x n)
-        const bool xs = b >= pl.b_nz;
-        const int bb = xs ? b - pl.b_nz : b - pl.b_gpsi;
-        const int m = xs ? 0 : bb / pl.nrb_n, rb = xs ? bb : bb % pl.nrb_n;
-        const int i = rb * (256 / pl.lrn) + rsub;
-        if (i >= d.n) return;
-        const uint32_t mg = xs ? 0u : (uint32_t)(d.shard0 + m);
-        double *o = xs ? const_cast<double *>(dr.NX) + (size_t)i * K
-                       : const_cast<double *>(dr.NZ) + ((size_t)mg * d.n + i) * K;
-        draw_normal_row(rng, xs ? SITE_X : SITE_Z, mg, (uint32_t)i, it, K, lane, pl.lrn, o);
-        return;
-    }
-    {                                                  // dc:142 Lambda (K x P x g)
-        const int bb = b - pl.b_nx, m = bb / pl.nrb_p, rb = bb % pl.nrb_p;
-        const int j = rb * (256 / pl.lrn) + rsub;
-        if (j >= d.P) return;
-        const uint32_t mg = (uint32_t)(d.shard0 + m);
-        draw_normal_row(rng, SITE_LAMBDA, mg, (uint32_t)j, it, K, lane, pl.lrn,
-                        const_cast<double *>(dr.NL) + ((size_t)mg * d.P + j) * K);
-    }
+    draws_block<GAMMAS>(d, dr, iter, pl, blockIdx.x + (GAMMAS ? 0 : pl.b_gpsi));
 }
 
 __global__ __launch_bounds__(256) void k_rng_fill(uint64_t seed, int kind, double shape, int site,
@@ -1689,11 +1692,17 @@ void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
 }
 // k_wcol launch (one rank, K <= 32)
 void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_epoch,
-                 hipStream_t s) {
-    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / 128) * d.G : 0);
+                 const DrawsDev *ldraws, int64_t iter, hipStream_t s) {
+    int nd = 0;
+    if (ldraws) {
+        const DrawPlan pl = draw_plan(d);
+        nd = (pl.b_gpsi - pl.b_gdel) + (pl.total - pl.b_nx);
+    }
+    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + nd + (wpass ? (d.NP / 128) * d.G : 0);
     if (nb == 0) return;
+    DrawsDev dr = ldraws ? *ldraws : DrawsDev{};
     hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, ops ? 1 : 0, colsum ? 1 : 0, wpass ? 1 : 0,
-                       ops_epoch);
+                       ops_epoch, nd > 0 ? 1 : 0, dr, iter);
 }
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return;
