@@ -1085,9 +1085,9 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         h->gen_n[sl] = nb;
         return sl;
     };
-    // Generated draws (Philox, counter-addressed): one rank, K <= 32 (wc) — the Z / X normals
-    // are drawn in place by the draw kernels and k_lambda's variates by k_wcol's draw role into
-    // gen[0]; every other path reads k_draws buffers generated a batch ahead on the draw stream
+    // Generated draws (Philox, counter-addressed): one rank, K <= 32 (wc) — every kernel draws
+    // its own variates in place (Z / X normals, k_lambda's normals and gammas, the delta
+    // gammas); the other paths read k_draws buffers generated a batch ahead on the draw stream
     const bool gen_draws = !d.inject && !wc;
     int slot = -1;
     int64_t batch0 = first_iter, batch_n = 0;
@@ -1114,16 +1114,12 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             HIPC(h, hipStreamWaitEvent(s, h->e_drawn[slot], 0));
             if (it + batch_n < end_iter && gen_batch(it + batch_n, slot) < 0) return rc_gen;   // next batch
         }
-        if (wc && !d.inject) {            // k_wcol draws this iteration's k_lambda variates into gen[0]
-            h->gen[0].first_iter = it;
-            h->gen[0].n_iter = 1;
-        }
         const DrawsDev &dr = d.inject ? h->dr : h->gen[gen_draws ? slot : 0];
         if (wc) {
             {
                 KTimer t(h, DCFM_K_WPASS, s);
                 h->wc_ops += 1;
-                launch_wcol(d, b, true, delta_pending, true, h->wc_ops, d.inject ? nullptr : &h->gen[0], it, s);
+                launch_wcol(d, b, true, delta_pending, true, h->wc_ops, s);
             }
             { KTimer t(h, DCFM_K_ZDRAW, s); launch_zdraw(d, b, dr, it, s); }
         } else if (fused) {
@@ -1174,7 +1170,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         { KTimer t(h, DCFM_K_CPASS, s);  launch_cpass(d, b, s); }
         {
             KTimer t(h, DCFM_K_LAMBDA, s);
-            launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s);
+            launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, wc && !d.inject);
         }
         h->plam_valid = false;
         if (wc) {
@@ -1253,7 +1249,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     }
     if (delta_pending) {   // the last iteration's column sums + delta chain
         KTimer t(h, DCFM_K_DELTA, s);
-        launch_wcol(d, b, false, true, false, 0, nullptr, 0, s);
+        launch_wcol(d, b, false, true, false, 0, s);
         const DrawsDev &dr = d.inject ? h->dr : h->gen[0];   // gammas drawn in place unless injected
         launch_delta(d, b, dr, end_iter - 1, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
                      b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);

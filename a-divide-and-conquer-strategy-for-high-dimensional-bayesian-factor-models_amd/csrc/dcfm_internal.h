@@ -118,9 +118,8 @@ void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
                      hipStream_t s, bool ops = true);
 // one rank, K <= 32: the Z operators + shard sum of A (ops), the previous iteration's column
 // sums (colsum) and the Y pass W (wpass) in one launch (k_wcol)
-// ldraws (generated mode): also this iteration's k_lambda variates (NL, Gpsi, Gps) into *ldraws
 void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_epoch,
-                 const DrawsDev *ldraws, int64_t iter, hipStream_t s);
+                 hipStream_t s);
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 // one rank, K <= 32: k_xdraw plus, when delta_in != null, the delta chain of delta_iter
 void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
@@ -130,8 +129,9 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
                   bool from_shards = false);
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s);
+// gen: K <= 32 draws its variates in place (one rank's fused chain) instead of reading dr
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
-                   const double *tau_cur, const double *plam_src, hipStream_t s);
+                   const double *tau_cur, const double *plam_src, hipStream_t s, bool gen = false);
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                   const double *delta_in, const double *tau_in, double *delta_out,

@@ -864,7 +864,7 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
                                                const double *__restrict__ plam_src, double *__restrict__ ps,
                                                double *__restrict__ omega,
                                                double *__restrict__ cpart, DrawsDev dr,
-                                               int64_t iter) {
+                                               int64_t iter, int gen) {
     // per system: the current column pair (L[r][k], L[r][k+1]) of every row r, then x
     __shared__ __attribute__((aligned(16))) double LS[4][2 * KP];
     const int m = blockIdx.y;
@@ -889,11 +889,28 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
     const double pin0 = rv0 ? pin[rowoff + r0] : 0.0, pin1 = rv1 ? pin[rowoff + r1] : 0.0;
     const double c0 = valid ? C[rowoff + r0] : 0.0, c1 = valid ? C[rowoff + r1] : 0.0;
     const uint32_t dk = drow * (uint32_t)d.K;
-    // the row's draws: injected, or generated for this iteration by k_wcol's draw role (one
-    // rank, K <= 32) / k_draws, at their counters — the same buffer layout either way
-    const double z0 = rv0 ? dr.NL[dk + r0] : 0.0, z1 = rv1 ? dr.NL[dk + r1] : 0.0;       // dc:142
-    const double G0 = rv0 ? dr.Gpsi[dk + r0] : 0.0, G1 = rv1 ? dr.Gpsi[dk + r1] : 0.0;   // dc:150
-    const double Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;                           // dc:170
+    double z0, z1, G0, G1, Gps;
+    if (!gen) {       // injected, or k_draws buffers (the paths other than one rank's fused chain)
+        z0 = rv0 ? dr.NL[dk + r0] : 0.0; z1 = rv1 ? dr.NL[dk + r1] : 0.0;       // dc:142
+        G0 = rv0 ? dr.Gpsi[dk + r0] : 0.0; G1 = rv1 ? dr.Gpsi[dk + r1] : 0.0;   // dc:150
+        Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;                           // dc:170
+    } else {          // drawn here, at the counters k_draws uses (identical values); independent
+                      // of the factorisation below, so it fills the wave's issue gaps
+        const Rng rng(d.seed);
+        const uint32_t it32 = (uint32_t)iter, mg32 = (uint32_t)mg, j32 = (uint32_t)jj;
+        // lane l draws normal pair l (indices 2l, 2l + 1); row index r comes from lane r / 2
+        double n0 = 0.0, n1 = 0.0;
+        if (valid && 2 * l < d.K) rng.normal2(SITE_LAMBDA, mg32, j32, (uint32_t)l, it32, n0, n1);
+        const int src0 = (qw << 4) | (r0 >> 1), src1 = (qw << 4) | (r1 >> 1);
+        const double a0 = __shfl(n0, src0, 64), b0 = __shfl(n1, src0, 64);
+        const double a1 = __shfl(n0, src1, 64), b1 = __shfl(n1, src1, 64);
+        z0 = rv0 ? ((r0 & 1) ? b0 : a0) : 0.0;
+        z1 = rv1 ? ((r1 & 1) ? b1 : a1) : 0.0;
+        const double shp = d.df * 0.5 + 0.5;
+        G0 = rv0 ? rng.gamma(shp, SITE_PSI, mg32, j32, (uint32_t)r0, it32) : 0.0;
+        G1 = rv1 ? rng.gamma(shp, SITE_PSI, mg32, j32, (uint32_t)r1, it32) : 0.0;
+        Gps = (valid && l == 0) ? rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg32, j32, 0u, it32) : 0.0;
+    }
     const double yyj = (valid && l == 0) ? yy[(uint32_t)(m * d.PP + jj)] : 0.0;
     const double *Ea = E + ((uint32_t)m * KP + r0) * KP, *Eb = E + ((uint32_t)m * KP + r1) * KP;
     constexpr int KH = KP / 2;       // rows < 16 only ever touch columns < 16 (lower triangle)
@@ -1342,7 +1359,7 @@ __device__ __forceinline__ double tree8(const double (&v)[8]) {
 }
 
 __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsum, int wpass,
-                                              unsigned long long ops_epoch, int ldraws, DrawsDev dr, int64_t iter) {
+                                              unsigned long long ops_epoch) {
     __shared__ double smem[PREP_SMEM];
     const int G = d.G, nxs = xsum_blocks(G), chunk = G / nxs;
     unsigned long long *chunk_ctr = b.sync + 2;   // per chunk of shards: A_m published
@@ -1419,19 +1436,6 @@ __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsu
             return;
         }
         blk -= nxs;
-    }
-    if (ldraws) {   // generated draws of this iteration's k_lambda (NL, Gpsi, Gps) into dr, T = 1
-        const DrawPlan pl = draw_plan(d);
-        const int ng = pl.b_gpsi - pl.b_gdel, nn = pl.total - pl.b_nx;
-        if (blk < ng) {
-            draws_block<true>(d, dr, iter, pl, pl.b_gdel + blk);
-            return;
-        }
-        if (blk < ng + nn) {
-            draws_block<false>(d, dr, iter, pl, pl.b_nx + blk - ng);
-            return;
-        }
-        blk -= ng + nn;
     }
     if (wpass) {
         const int nw = gridDim.x - (int)(blockIdx.x - blk);
@@ -1692,17 +1696,11 @@ void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
 }
 // k_wcol launch (one rank, K <= 32)
 void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_epoch,
-                 const DrawsDev *ldraws, int64_t iter, hipStream_t s) {
-    int nd = 0;
-    if (ldraws) {
-        const DrawPlan pl = draw_plan(d);
-        nd = (pl.b_gpsi - pl.b_gdel) + (pl.total - pl.b_nx);
-    }
-    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + nd + (wpass ? (d.NP / 128) * d.G : 0);
+                 hipStream_t s) {
+    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / 128) * d.G : 0);
     if (nb == 0) return;
-    DrawsDev dr = ldraws ? *ldraws : DrawsDev{};
     hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, ops ? 1 : 0, colsum ? 1 : 0, wpass ? 1 : 0,
-                       ops_epoch, nd > 0 ? 1 : 0, dr, iter);
+                       ops_epoch);
 }
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return;
@@ -1749,10 +1747,10 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     }
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
-                   const double *tau_cur, const double *plam_src, hipStream_t s) {
+                   const double *tau_cur, const double *plam_src, hipStream_t s, bool gen) {
     if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, plam_src, s);
     hipLaunchKernelGGL(k_lambda, dim3(cdiv(d.P, 4), d.G), dim3(64), 0, s, d, b.C, b.E, b.yy, tau_cur,
-                       b.Lam, b.psi, plam_src, b.ps, b.omega, b.cpart, dr, iter);
+                       b.Lam, b.psi, plam_src, b.ps, b.omega, b.cpart, dr, iter, gen ? 1 : 0);
 }
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(d.G, d.kp / 32);

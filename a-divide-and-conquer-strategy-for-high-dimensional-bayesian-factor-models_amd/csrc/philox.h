@@ -66,7 +66,7 @@ __device__ __forceinline__ double u01_53(uint32_t hi, uint32_t lo) {
 // Box-Muller pair with Philox); these cover exactly the uniforms' range in ~1/3 of
 // that, to within a few ulp (the variates are checked statistically, tests/test_gpu_rng.py).
 
-// log(u), u in [2^-53, 1]: u = 2^e m, m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s),
+// log(u), u in [2^-106, 1] (a uniform or the product of two): u = 2^e m, m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s),
 // s = (m-1)/(m+1), |s| <= 0.1716: series to s^23 (truncation < 1e-18 relative)
 __device__ __forceinline__ double log_u01(double u) {
     double m = __builtin_amdgcn_frexp_mant(u);              // [0.5, 1)
@@ -169,10 +169,11 @@ struct Rng {
     __device__ __forceinline__ double gamma(double shape, uint32_t site, uint32_t shard, uint32_t row,
                                             uint32_t idx, uint32_t iter) const {
         if (shape == 1.0 || shape == 2.0) {
-            // integer shape: sum of shape exponentials, -log(u1 [* u2]) — exact, no rejection
+            // integer shape: sum of shape exponentials, -log(u1 [* u2]) — exact, no rejection; one
+            // log of the product (>= 2^-106, a normal double) instead of a sum of two logs
             const u32x4 a = raw(site, shard, row, 0x80000000u | ((idx & 0x7FFFFFu) << 8), iter);
             const double u1 = u01_53(a.x, a.y);
-            return shape == 1.0 ? -log_u01(u1) : -(log_u01(u1) + log_u01(u01_53(a.z, a.w)));
+            return -log_u01(shape == 1.0 ? u1 : u1 * u01_53(a.z, a.w));
         }
         return gamma_mt(shape, site, shard, row, idx, iter);
     }
