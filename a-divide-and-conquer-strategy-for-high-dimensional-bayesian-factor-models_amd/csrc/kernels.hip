@@ -1470,6 +1470,11 @@ __global__ __launch_bounds__(256) void k_save(Dims d, const double *__restrict__
 // 8 x 8-tile supertiles (dcfm_create), XCD-contiguous (xcd_remap): the tiles an XCD
 // has in flight share 8 row and 8 column panels of Lb in its L2.  The tile's place
 // in the rank's packed Sigma block comes from (ti, tj).
+// Cross-shard tiles (no row and column of the same shard: coef = rho everywhere, ~95% of
+// the tiles at c3) start their accumulators FROM the old Sigma values, loaded with the
+// first panel chunk, and stage the row panel scaled by rho / effsamp: the epilogue is
+// plain stores, so the read half of the read-modify-write never waits at the end of the
+// tile.  Tiles with same-shard pairs (and the diagonal) keep the epilogue update.
 // 4 waves in 2x2, each 64x64 = 4x4 tiles of v_mfma_f64_16x16x4.  The k extent
 // (batch x K) runs in chunks of 16 through double-buffered LDS, stored k-major
 // with a 144-double pitch: an MFMA operand read (16 consecutive rows x 4 k) is a
@@ -1491,6 +1496,10 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
     const int r = lane & 15, q = lane >> 4;
     const int p = d.p;
     const int wa = (wave >> 1) * 64, wb = (wave & 1) * 64;
+    // cross-shard tile: the rows' shards all lie below the columns' (tj < ti, rows >= columns)
+    const int clast = min(p, T.y * ASM_TILE + ASM_TILE) - 1;
+    const bool cross = (T.x * ASM_TILE) / d.P > clast / d.P;
+    const double sA = cross ? d.rho * inv_eff : 1.0;     // row-panel scale while staging
     // global -> LDS: thread t stages row (t >> 1) of both panels, k = 8 (t & 1) .. +7
     const int srow = t >> 1, shalf = t & 1;
     const int ga = T.x * ASM_TILE + srow, gb = T.y * ASM_TILE + srow;
@@ -1510,17 +1519,26 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int k = 8 * shalf + 2 * i;
-            As[buf][k][srow] = ra[i].x;
-            As[buf][k + 1][srow] = ra[i].y;
+            As[buf][k][srow] = sA * ra[i].x;
+            As[buf][k + 1][srow] = sA * ra[i].y;
             Bs[buf][k][srow] = rb[i].x;
             Bs[buf][k + 1][srow] = rb[i].y;
         }
     };
     d4 acc[4][4];
+    if (cross) {   // acc = the tile's old values (C/D layout: row q + 4g of 16-row tile u)
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) acc[u][v] = d4{0.0, 0.0, 0.0, 0.0};
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) acc[u][v][g] = St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r];
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[u][v] = d4{0.0, 0.0, 0.0, 0.0};
+    }
     gload(0);
     lstore(0);
     __syncthreads();
@@ -1541,6 +1559,15 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
         }
         if (more) lstore(buf ^ 1);
         __syncthreads();
+    }
+    if (cross) {   // acc = old + (rho / effsamp) L_a L_b': plain stores (the whole tile is below the diagonal)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r] = acc[u][v][g];
+        return;
     }
     // epilogue: lower-triangle read-modify-write of the tile (tile-packed, row-major inside),
     // loads issued together (predicated, no branches around them), shard test from the LDS table
