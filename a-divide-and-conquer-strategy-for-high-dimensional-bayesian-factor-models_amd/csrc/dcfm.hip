@@ -993,12 +993,14 @@ static int flush_batch(dcfm_handle *h) {
         if (!h->loop) NCCLC(h, ncclGroupEnd());
         if (rc) return rc;
     }
-    const int used = h->batch * d.K, kext = round_up(used, ASM_KC);   // k_assemble chunk
+    // k extent: the batch's columns rounded to the MFMA k-step (4); k_assemble stages whole
+    // chunks of ASM_KC columns, so columns [used, round_up(used, ASM_KC)) must be zero
+    const int used = h->batch * d.K, kext = round_up(used, 4), kstage = round_up(used, ASM_KC);
     const double effsamp = (double)h->cfg.mcmc / (double)h->cfg.thin;   // dc:45 (Q8)
-    // k_save wrote columns [0, used) of every row; only the chunk's tail [used, kext) can
+    // k_save wrote columns [0, used) of every row; only the chunk's tail [used, kstage) can
     // hold an earlier batch's samples: zero just that (not the p x LDB buffer)
-    if (kext > used)
-        HIPC(h, hipMemset2DAsync(b.Lb[lb] + used, (size_t)b.LDB * sizeof(double), 0, (size_t)(kext - used) * sizeof(double),
+    if (kstage > used)
+        HIPC(h, hipMemset2DAsync(b.Lb[lb] + used, (size_t)b.LDB * sizeof(double), 0, (size_t)(kstage - used) * sizeof(double),
                                  (size_t)d.p, h->sasm));
     {
         KTimer t(h, DCFM_K_ASSEMBLE, h->sasm);

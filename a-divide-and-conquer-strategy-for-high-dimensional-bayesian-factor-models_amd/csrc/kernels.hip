@@ -1545,8 +1545,10 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
     for (int kc = 0, buf = 0; kc < kext; kc += AKC, buf ^= 1) {
         const bool more = kc + AKC < kext;
         if (more) gload(kc + AKC);
+        const int nk4 = min(AKC, kext - kc);   // k extent of this chunk (a multiple of 4)
 #pragma unroll
         for (int s4 = 0; s4 < AKC / 4; ++s4) {
+            if (4 * s4 >= nk4) break;            // block-uniform: the last chunk may be partial
             double a[4], b[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) a[u] = As[buf][4 * s4 + q][wa + 16 * u + r];
