@@ -74,7 +74,6 @@ struct dcfm_handle {
                e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
     unsigned long long wc_ops = 0;   // k_wcol launches with the operator roles (hand-off counter epoch)
-    bool prep_valid = false;      // fused path: A / ZM hold the next iteration's Z operators
     bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
     int lb = 0;                   // Lb buffer being filled
@@ -501,7 +500,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         ALLOC(b.xa_all, (size_t)nranks * KP * KP);
     }
     ALLOC(b.XM, 2 * KP * KP);
-    ALLOC(b.xpart, (size_t)G * KP * KP);  // k_deltaops: xsum_blocks(G) <= G chunk sums
+    ALLOC(b.xpart, (size_t)G * KP * KP);  // k_wcol: xsum_blocks(G) <= G chunk sums
     {
         double *tk = nullptr;
         ALLOC(tk, 1);
@@ -749,7 +748,6 @@ int dcfm_init_state(dcfm_handle *h) {
     HIPC(h, hipStreamSynchronize(h->stream));
     h->cur = 0;
     h->plam_valid = true;      // Plam = psi o tau' was formed (dc:86), as set_state's caller Plam
-    h->prep_valid = false;
     h->have_state = true;
     return reset_numeric(h);
 }
@@ -886,7 +884,6 @@ int dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s) {
     k_to_dev(d, s->delta, v);   if ((rc = up(h, h->b.delta, v))) return rc;
     k_to_dev(d, s->tauh, v);    if ((rc = up(h, h->b.tau, v))) return rc;
     h->plam_valid = true;
-    h->prep_valid = false;
     h->have_state = true;
     return reset_numeric(h);
 }
@@ -1034,13 +1031,16 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     const size_t nkg = (size_t)d.g * KW;
     const int64_t end_iter = first_iter + n_iter;
     // K <= 32: the per-shard operators ride in the fused launches on the main stream
-    // (k_colgram, k_deltaops, k_zxchol); K > 32 (or DCFM_NOFUSE=1): prep and the X
+    // (k_wcol, k_zxchol / k_xdraw); K > 32 (or DCFM_NOFUSE=1): prep and the X
     // operators run on the side stream
     static const bool nofuse = [] { const char *e = std::getenv("DCFM_NOFUSE"); return e && e[0] == '1'; }();
     const bool fused = d.kp == KP && !nofuse;
-    // one rank, fused: per iteration t, k_wcol = [Z and X operators of t, column sums of t-1]
-    // beside the W pass of t; k_zdraw; k_xdraw = [delta chain of t-1] beside the X draw of t.
-    // The last iteration's chain runs after the loop (k_delta).
+    // fused (K <= 32): per iteration t, k_wcol = [Z operators and shard sum of A of t, column
+    // sums of t-1] beside the W pass of t.  One rank: the last chunk also factors Xprec, then
+    // k_zdraw and k_xdraw = [delta chain of t-1] beside the X draw.  Several ranks: the
+    // [column sums | A sum] all-gather, k_zxchol = [X operators, delta chain of t-1] beside the
+    // Z draw, then k_xred, the X message gather and k_xdraw.  The last iteration's chain runs
+    // after the loop (k_delta).
     const bool wc = fused && d.nranks == 1;
     bool delta_pending = false;           // k_lambda of it - 1 ran, its delta chain not yet queued
     auto after_delta = [&]() {            // iteration it - 1 is complete
@@ -1087,26 +1087,13 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         h->gen_n[sl] = nb;
         return sl;
     };
-    // Generated draws (Philox, counter-addressed): one rank, K <= 32 (wc) — every kernel draws
-    // its own variates in place (Z / X normals, k_lambda's normals and gammas, the delta
-    // gammas); the other paths read k_draws buffers generated a batch ahead on the draw stream
-    const bool gen_draws = !d.inject && !wc;
+    // Generated draws (Philox, counter-addressed): the fused K <= 32 chain (any rank count) draws
+    // every variate in place (Z / X normals, k_lambda's normals and gammas, the delta gammas);
+    // the other paths read k_draws buffers generated a batch ahead on the draw stream
+    const bool gen_draws = !d.inject && !fused;
     int slot = -1;
     int64_t batch0 = first_iter, batch_n = 0;
-    if (!fused) {
-        HIPC(h, hipEventRecord(h->e_lam, s));      // Lambda/omega of the previous iteration are final
-        h->prep_valid = false;
-    } else if (wc) {
-        h->prep_valid = false;                     // k_wcol forms every iteration's operators itself
-    } else if (!h->prep_valid) {                   // operators of first_iter from the state as set
-        KTimer t(h, DCFM_K_PREP, s);
-        launch_colgram(d, b, false, s);
-        launch_deltaops(d, b, h->dr, first_iter, false, nullptr, nullptr, nullptr, nullptr, s);
-        if (d.nranks > 1)   // the packed message (column sums unused here) or the A sum alone
-            if (int rc = d.sgap ? coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)
-                                : coll_allgather(h, CH_MAIN, b.xa, b.xa_all, KW * KW, s))
-                return rc;
-    }
+    if (!fused) HIPC(h, hipEventRecord(h->e_lam, s));   // Lambda/omega of the previous iteration are final
     for (int64_t it = first_iter; it < end_iter; ++it) {
         if (gen_draws && (it == first_iter || it == batch0 + batch_n)) {
             batch0 = it;
@@ -1124,14 +1111,32 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
                 launch_wcol(d, b, true, delta_pending, true, h->wc_ops, s);
             }
             { KTimer t(h, DCFM_K_ZDRAW, s); launch_zdraw(d, b, dr, it, s); }
-        } else if (fused) {
-            { KTimer t(h, DCFM_K_WPASS, s); launch_wpass(d, b, s); }
-            { KTimer t(h, DCFM_K_ZDRAW, s); launch_zxchol(d, b, dr, it, s); }
-            if (d.nranks > 1) {   // one rank: k_xdraw sums the shard messages itself
-                { KTimer t(h, DCFM_K_XRED, s); launch_xred(d, b, s); }
-                KTimer t(h, DCFM_K_COMM, s);
-                if (int rc = coll_allgather(h, CH_MAIN, b.xin, b.xall, (size_t)d.NP * KW, s)) return rc;
+        } else if (fused) {   // several ranks: k_wcol (no X factorisation), ONE all-gather of
+                              // [column sums of it - 1 | local A sum], then k_zxchol = X operators
+                              // + delta chain of it - 1 + Z draw; the X message gather
+            {
+                KTimer t(h, DCFM_K_WPASS, s);
+                h->wc_ops += 1;
+                launch_wcol(d, b, true, delta_pending, true, h->wc_ops, s);
             }
+            {
+                KTimer t(h, DCFM_K_COMM, s);
+                if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)) return rc;
+            }
+            {
+                KTimer t(h, DCFM_K_ZDRAW, s);
+                if (delta_pending)
+                    launch_zxchol(d, b, dr, it, s, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+                                  b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1);
+                else
+                    launch_zxchol(d, b, dr, it, s);
+            }
+            HIPC(h, hipGetLastError());
+            if (delta_pending) after_delta();
+            delta_pending = false;
+            { KTimer t(h, DCFM_K_XRED, s); launch_xred(d, b, s); }
+            KTimer t(h, DCFM_K_COMM, s);
+            if (int rc = coll_allgather(h, CH_MAIN, b.xin, b.xall, (size_t)d.NP * KW, s)) return rc;
         } else {
             // side stream: A_m, R_m, Rx from this iteration's incoming Lambda, omega (dc:98-100,112-118)
             HIPC(h, hipStreamWaitEvent(ss, h->e_lam, 0));
@@ -1172,43 +1177,11 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         { KTimer t(h, DCFM_K_CPASS, s);  launch_cpass(d, b, s); }
         {
             KTimer t(h, DCFM_K_LAMBDA, s);
-            launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, wc && !d.inject);
+            launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, fused && !d.inject);
         }
         h->plam_valid = false;
-        if (wc) {
-            delta_pending = true;     // column sums + delta chain ride in the next k_wcol
-        } else if (fused && d.sgap) {   // several ranks: ONE all-gather of [column sums | A sum]
-            { KTimer t(h, DCFM_K_COLSUM, s); launch_colgram(d, b, true, s); }
-            {   // Z operators + the local A sum (independent of delta), then the message
-                KTimer t(h, DCFM_K_DELTA, s);
-                launch_deltaops(d, b, dr, it, false, nullptr, nullptr, nullptr, nullptr, s, true);
-            }
-            {
-                KTimer t(h, DCFM_K_COMM, s);
-                if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)) return rc;
-            }
-            {
-                KTimer t(h, DCFM_K_DELTA, s);
-                launch_deltaops(d, b, dr, it, true, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
-                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s, false);
-            }
-            h->prep_valid = true;
-        } else if (fused) {   // + the next iteration's grams and Z operators
-            { KTimer t(h, DCFM_K_COLSUM, s); launch_colgram(d, b, true, s); }
-            if (d.nranks > 1) {
-                KTimer t(h, DCFM_K_COMM, s);
-                if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.sall, (size_t)d.G * KW, s)) return rc;
-            }
-            {
-                KTimer t(h, DCFM_K_DELTA, s);
-                launch_deltaops(d, b, dr, it, true, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
-                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);
-            }
-            if (d.nranks > 1) {
-                KTimer t(h, DCFM_K_COMM, s);
-                if (int rc = coll_allgather(h, CH_MAIN, b.xa, b.xa_all, KW * KW, s)) return rc;
-            }
-            h->prep_valid = true;
+        if (fused) {
+            delta_pending = true;     // column sums + delta chain ride in the next iteration's launches
         } else {
             HIPC(h, hipEventRecord(h->e_lam, s));
             { KTimer t(h, DCFM_K_COLSUM, s); launch_colsum(d, b, s); }
@@ -1226,7 +1199,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             HIPC(h, hipEventRecord(h->e_used[slot], s));
             h->used_pending[slot] = true;
         }
-        if (!wc) {
+        if (!fused) {
             h->cur ^= 1;
             if (h->trace_n < h->trace_cap) {                              // dcfm_set_trace
                 launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4, s);
@@ -1249,9 +1222,11 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             }
         }
     }
-    if (delta_pending) {   // the last iteration's column sums + delta chain
+    if (delta_pending) {   // the last iteration's column sums (+ their gather) and delta chain
         KTimer t(h, DCFM_K_DELTA, s);
         launch_wcol(d, b, false, true, false, 0, s);
+        if (d.nranks > 1)
+            if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)) return rc;
         const DrawsDev &dr = d.inject ? h->dr : h->gen[0];   // gammas drawn in place unless injected
         launch_delta(d, b, dr, end_iter - 1, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
                      b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, s);

@@ -65,8 +65,8 @@ struct Bufs {
     double *W, *A, *ZM, *Sp, *xin, *xall, *C, *E, *cpart, *sloc, *sall;
     double *Lb[2], *wsum[2], *Sigma;
     double *xa, *xa_all, *XM;          // per-rank sum of A, gathered sums, X-draw operators
-    double *xpart;                     // k_deltaops chunk sums of A (8 x KP x KP)
-    unsigned *ticket;                  // k_deltaops last-arrival ticket (0 between launches)
+    double *xpart;                     // k_wcol chunk sums of A (xsum_blocks(G) x KP x KP)
+    unsigned *ticket;                  // k_wcol last-arrival ticket (0 between launches)
     unsigned long long *sync;          // hand-off counters (monotonic): [2 + chunk] = k_wcol A_m of the chunk out
     double *msg_all;                   // packed gather target (fused, nranks > 1), else null
     int2 *tiles;
@@ -74,7 +74,7 @@ struct Bufs {
     int T0, T1;                        // owned tile rows of Sigma (block-sharded, see above)
 };
 
-// k_wcol / k_deltaops shard sum of A
+// k_wcol shard sum of A
 constexpr int XSUM_BLOCKS = 8;
 // blocks of the A sum: G / chunk, chunk = a power of two dividing G, grown while more than
 // XSUM_BLOCKS chunks remain — so each chunk is a subtree of the canonical tree (TreeSum) and
@@ -110,17 +110,16 @@ void launch_prep(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s);
-// fused one-rank narrow launches (kernels.hip: k_colgram, k_deltaops, k_zxchol)
-void launch_colgram(const Dims &d, const Bufs &b, bool colsum, hipStream_t s);
-// ops: the xsum-tree + Z-operator blocks; delta: the delta/tau chain blocks (reads sall)
-void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool delta,
-                     const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
-                     hipStream_t s, bool ops = true);
-// one rank, K <= 32: the Z operators + shard sum of A (ops), the previous iteration's column
-// sums (colsum) and the Y pass W (wpass) in one launch (k_wcol)
+// fused K <= 32 launches (kernels.hip: k_wcol, k_zxchol, k_xdraw roles)
+// K <= 32: the Z operators + shard sum of A (ops), the previous iteration's column sums
+// (colsum) and the Y pass W (wpass) in one launch (k_wcol); one rank also factors Xprec
 void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_epoch,
                  hipStream_t s);
-void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
+// k_zxchol: X operators from the ranks' gathered A sums (block 0), optionally the delta chain of
+// delta_iter (delta_in != null; column sums from b.sall), and the Z draw tiles
+void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
+                   const double *delta_in = nullptr, const double *tau_in = nullptr, double *delta_out = nullptr,
+                   double *tau_out = nullptr, int64_t delta_iter = 0);
 // one rank, K <= 32: k_xdraw plus, when delta_in != null, the delta chain of delta_iter
 void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
                      const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s);

@@ -1218,33 +1218,11 @@ __global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__
 }
 
 // ============================================================================
-// Fused single-stream launches (one rank, K <= 32).  Cross-stream event hand-offs
-// cost ~6 us each on the critical path, and latency-bound work slows ~2x when it
-// shares CUs with the MFMA-bound Y passes, so the small per-shard K x K work rides
-// in the launches that leave the GPU idle, and the X operators in front of a Y pass:
-//   k_colgram:  blocks [0, G) = A_m grams (prep_gram), the rest k_colsum tiles
-//   k_deltaops: blocks [0, nxs) = the shard sum xa of A (chunk sums, then the last
-//               arrival adds them in chunk order); then G blocks of Z operators from
-//               A_m (prep_ops); the rest k_delta (4 shards per block, one wave each)
-//   k_zxchol:   block 0 = the X operators from the ranks' xa (k_xchol), the rest k_zdraw tiles
-// With several ranks the main stream all-gathers xa after k_deltaops, the X message
-// after k_xred and the column sums after k_colgram (RCCL, same order on every rank).
-// The gram and operators are those of the NEXT iteration (they read this iteration's
-// Lambda and ps); dcfm_run runs a prologue after set_state.
+// Fused single-stream launches (K <= 32).  Cross-stream event hand-offs cost ~6 us each
+// on the critical path, and latency-bound work slows ~2x when it shares CUs with the
+// MFMA-bound Y passes, so the small per-shard K x K work rides in the launches of the
+// Y passes (k_wcol, k_zxchol, k_xdraw) as extra roles (dcfm_run names the plan).
 // ============================================================================
-__global__ __launch_bounds__(256) void k_colgram(Dims d, const double *__restrict__ cpart,
-                                                 double *__restrict__ sloc, const double *__restrict__ Lam,
-                                                 const double *__restrict__ omega, double *__restrict__ A,
-                                                 double *__restrict__ ZM) {
-    __shared__ double smem[PREP_SMEM];
-    if ((int)blockIdx.x < d.G) {
-        prep_gram(d, Lam, omega, A, ZM, blockIdx.x, smem);
-        return;
-    }
-    colsum_tile<KP>(d, cpart, sloc, blockIdx.x - d.G, 0, smem);
-}
-
-
 // The chunk sums are handed to the last arrival with agent-scope relaxed atomics (sc1:
 // coherent across the XCDs' L2s without write-back / invalidate), ordered by the stores'
 // completion before the ticket — __threadfence's buffer_wbl2 / buffer_inv flush the XCD's
@@ -1265,65 +1243,25 @@ __device__ __forceinline__ bool last_arrival(unsigned *ticket, unsigned count, d
     return last;
 }
 
-// blocks [0, nxs) of k_deltaops: chunk sums of A over the local shards into xpart, then
-// the last arrival adds them in chunk order into xa (k_zxchol forms the X operators)
-__device__ __forceinline__ void xsum_tree(const Dims &d, const double *__restrict__ A, double *__restrict__ xpart,
-                                          unsigned *__restrict__ ticket, double *__restrict__ xa, int j, int nxs,
-                                          double *smem) {
-    const int t = threadIdx.x;
-    const int chunk = d.G / nxs, m0 = j * chunk;   // a canonical subtree (xsum_blocks)
-    double v[KP * KP / 256];
-#pragma unroll
-    for (int u = 0; u < KP * KP / 256; ++u) {
-        const int e = t + 256 * u;
-        const double acc = tree_sum(A + (size_t)m0 * KP * KP + e, chunk, (size_t)KP * KP);
-        v[u] = acc;
-        st_agent(xpart + (size_t)j * KP * KP + e, acc);
-    }
-    if (!last_arrival(ticket, (unsigned)nxs, smem)) return;
-#pragma unroll
-    for (int u = 0; u < KP * KP / 256; ++u) {
-        const int e = t + 256 * u;
-        xa[e] = tree_sum_f<double>(nxs, [&](int jj) { return (jj == j) ? v[u] : ld_agent(xpart + (size_t)jj * KP * KP + e); });
-    }
-}
-
-__global__ __launch_bounds__(256) void k_deltaops(Dims d, const double *__restrict__ sall,
-                                                  const double *__restrict__ delta_in,
-                                                  const double *__restrict__ tau_in,
-                                                  double *__restrict__ delta_out, double *__restrict__ tau_out,
-                                                  DrawsDev dr, int64_t iter, const double *__restrict__ A,
-                                                  double *__restrict__ ZM, double *__restrict__ xpart,
-                                                  unsigned *__restrict__ ticket, double *__restrict__ xa,
-                                                  int ops) {
-    __shared__ double smem[PREP_SMEM];
-    const int nxs = xsum_blocks(d.G);
-    int b = blockIdx.x + (ops ? 0 : nxs + d.G);   // !ops: the delta blocks alone
-    if (b < nxs) {
-        xsum_tree(d, A, xpart, ticket, xa, b, nxs, smem);
-        return;
-    }
-    b -= nxs;
-    if (b < d.G) {
-        prep_load(d, A, b, smem);
-        prep_ops(d, ZM, b, smem);
-        return;
-    }
-    const int m = (b - d.G) * 4 + (threadIdx.x >> 6);
-    if (m < d.g) delta_shard(d, sall, delta_in, tau_in, delta_out, tau_out, dr, iter, m, threadIdx.x & 63);
-}
-
 constexpr int ZX_SMEM = ZDRAW_SMEM > XCHOL_SMEM ? ZDRAW_SMEM : XCHOL_SMEM;
-// block 0: the X operators from the ranks' shard sums of A (several ranks, fused chain); the
-// rest: k_zdraw tiles
-__global__ __launch_bounds__(ZTHREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_zxchol(Dims d, const double *__restrict__ W,
-                                                     const double *__restrict__ ZM, const double *__restrict__ X,
-                                                     double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
-                                                     int64_t iter, const double *__restrict__ xa_all,
-                                                     double *__restrict__ XM) {
+// block 0: the X operators from the ranks' shard sums of A (several ranks, fused chain);
+// blocks [1, 1 + ndel): the previous iteration's delta / tau chain from the gathered column
+// sums (8 shards per block, one wave each), beside the Z pass; the rest: k_zdraw tiles
+__global__ __launch_bounds__(ZTHREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_zxchol(
+        Dims d, const double *__restrict__ W, const double *__restrict__ ZM, const double *__restrict__ X,
+        double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr, int64_t iter,
+        const double *__restrict__ xa_all, double *__restrict__ XM, int ndel, const double *__restrict__ sall,
+        DeltaArgs da) {
     __shared__ double smem[ZX_SMEM];
-    if (blockIdx.x > 0) {
-        zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blockIdx.x - 1, gridDim.x - 1), smem);
+    const int blk = blockIdx.x;
+    if (blk > ndel) {
+        zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blk - 1 - ndel, gridDim.x - 1 - ndel), smem);
+        return;
+    }
+    if (blk > 0) {
+        const int m = (blk - 1) * (ZTHREADS / 64) + (threadIdx.x >> 6);
+        if (m < d.g)
+            delta_shard(d, sall, da.delta_in, da.tau_in, da.delta_out, da.tau_out, dr, da.iter, m, threadIdx.x & 63);
         return;
     }
     for (int e = threadIdx.x; e < KP * KP; e += ZTHREADS) {   // the ranks' shard sums, canonical tree
@@ -1359,7 +1297,7 @@ __device__ __forceinline__ double tree8(const double (&v)[8]) {
 }
 
 __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsum, int wpass,
-                                              unsigned long long ops_epoch) {
+                                              unsigned long long ops_epoch, int xchol) {
     __shared__ double smem[PREP_SMEM];
     const int G = d.G, nxs = xsum_blocks(G), chunk = G / nxs;
     unsigned long long *chunk_ctr = b.sync + 2;   // per chunk of shards: A_m published
@@ -1427,6 +1365,11 @@ __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsu
                     }
                     xs[u] = ts.total();
                 }
+            }
+            if (!xchol) {   // several ranks: the local sum into the packed message (all-gathered next)
+#pragma unroll
+                for (int u = 0; u < NU; ++u) b.xa[t + 256 * u] = xs[u];
+                return;
             }
             __syncthreads();                          // smem (last_arrival's flag) is reused below
 #pragma unroll
@@ -1708,33 +1651,25 @@ void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
     hipLaunchKernelGGL(k_zdraw, dim3((d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
                        dr, iter);
 }
-void launch_colgram(const Dims &d, const Bufs &b, bool colsum, hipStream_t s) {
-    if (d.kp != KP) return;
-    hipLaunchKernelGGL(k_colgram, dim3(d.G + (colsum ? d.G : 0)), dim3(256), 0, s, d, b.cpart, b.sloc, b.Lam,
-                       b.omega, b.A, b.ZM);
-}
-void launch_deltaops(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool delta,
-                     const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
-                     hipStream_t s, bool ops) {
-    if (d.kp != KP) return;
-    const int nxs = xsum_blocks(d.G);
-    const int nb = (ops ? nxs + d.G : 0) + (delta ? (d.g + 3) / 4 : 0);
-    if (nb == 0) return;
-    hipLaunchKernelGGL(k_deltaops, dim3(nb), dim3(256), 0, s, d, b.sall, delta_in, tau_in, delta_out, tau_out, dr,
-                       iter, b.A, b.ZM, b.xpart, b.ticket, b.xa, ops ? 1 : 0);
-}
-// k_wcol launch (one rank, K <= 32)
+// k_wcol launch (K <= 32)
 void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_epoch,
                  hipStream_t s) {
     const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / 128) * d.G : 0);
     if (nb == 0) return;
     hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, ops ? 1 : 0, colsum ? 1 : 0, wpass ? 1 : 0,
-                       ops_epoch);
+                       ops_epoch, d.nranks == 1 ? 1 : 0);
 }
-void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
+                   const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
+                   int64_t delta_iter) {
     if (d.kp != KP) return;
-    hipLaunchKernelGGL(k_zxchol, dim3(1 + (d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
-                       dr, iter, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
+    // delta blocks padded so that the zdraw tiles' first block sits on XCD 0 (xcd_remap)
+    const int ndel = delta_in ? ((d.g + 7) / 8 + 1 + 7) / 8 * 8 - 1 : 0;
+    DeltaArgs da;
+    da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
+    da.iter = delta_iter;
+    hipLaunchKernelGGL(k_zxchol, dim3(1 + ndel + (d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM, b.X, b.Z,
+                       b.Sp, dr, iter, d.nranks > 1 ? b.xa_all : b.xa, b.XM, ndel, b.sall, da);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
     const int total = d.NP * d.kp;
