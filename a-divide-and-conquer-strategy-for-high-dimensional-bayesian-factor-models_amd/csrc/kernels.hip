@@ -835,27 +835,41 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
 
 // ============================================================================
 // k_lambda: loading rows.                                   dc:140-145 (+150,156,169-171)
-// One wave = 4 loading rows j; a 16-lane DPP row (quarter wave) owns one row:
-// lane l holds rows l and l+16 of Q_j = diag(Plam_j) + ps_j E_m in registers
-// (qa, qb).  Per pair of pivots (k, k+1):
-//   * the 2x2 pivot block and the rhs entries are broadcast inside the quarter
-//     with v_mov_dpp row_newbcast (compile-time lanes, no SGPR round trip),
-//   * each lane forms its rows' L entries, writes them to the pair-packed LDS
-//     image, and applies the rank-2 trailing update from LDS,
-//   * the forward solve L v = ps_j C_j rides along (dc:143 vlam = Llam \ blam).
-// Rows < 16 finish after pivot 15, so the second half of the factorisation
-// touches only qb (compile-time pruning; ~3x fewer VALU ops per row than a
-// 32-lane row).  Then Lambda_j = L' \ (v + z) (dc:143-144) right-looking from
-// the bottom, psi_j (dc:150), SS_j = yy_j - 2 x.C_j + x'E x and ps_j, omega_j
-// (dc:169-171), with x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j from the solve itself
-// (x'Q_j x = |L'x|^2 = |w|^2), so E is read once.  Plam_j = psi_j o tau' (dc:176) is
-// formed from the previous iteration's psi and tau unless plam_src is given (first
-// iteration after dcfm_set_state).  Every global load of the row, the row's draws
-// included, is issued up front: with 2 waves per SIMD nothing else hides a load
-// issued after the factorisation (measured: 64 -> 53 us at c3).
+// One wave = 8 loading rows j; an aligned 8-lane group owns one row: lane l holds rows
+// r_b = l + 8b (b = 0..3) of Q_j = diag(Plam_j) + ps_j E_m in registers, row r_b only
+// up to column 8b + 7 (the lower triangle, compile-time pruned: 80 values per lane, ~1.6x
+// the minimal work instead of ~3.5x for 16 lanes x 2 rows).  Per pair of pivots (k, k+1):
+//   * every lane writes its rows' current column pair (and rhs) to the group's LDS image,
+//   * all lanes read the 2x2 pivot block and the rhs pair from it and form the pivots,
+//   * each row forms its L entries and the coefficients (alpha, beta) of the rank-2 update
+//     q[c] -= alpha Q[c][k] + beta Q[c][k+1] (the L column pair expressed through the
+//     unnormalised image, so one LDS round per step), and the forward solve
+//     L v = ps_j C_j rides along (dc:143 vlam = Llam \ blam).
+// Then Lambda_j = L' \ (v + z) (dc:143-144) from the bottom, the sums over rows below a
+// column as 8-lane DPP reductions; psi_j (dc:150), SS_j = yy_j - 2 x.C_j + x'E x and
+// ps_j, omega_j (dc:169-171), with x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j from the
+// solve itself (x'Q_j x = |L'x|^2 = |w|^2), so E is read once.  Plam_j = psi_j o tau'
+// (dc:176) is formed from the previous iteration's psi and tau unless plam_src is given
+// (first iteration after dcfm_set_state).  The row's variates (drawn in place, or loaded
+// from a draw buffer) are formed first, before the rows of Q_j occupy the registers.
 // psi o lambda^2 of the row -> cpart[m][j][:] (k_colsum sums the rows).
 // ============================================================================
+template <int CTRL>
+__device__ __forceinline__ double dpp8_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+// sum over the aligned 8-lane group (identical bits in every lane: each stage adds a
+// commutative pair)
+__device__ __forceinline__ double rowsum8(double v) {
+    v += dpp8_d<0xB1>(v);     // quad_perm [1,0,3,2]
+    v += dpp8_d<0x4E>(v);     // quad_perm [2,3,0,1]
+    v += dpp8_d<0x141>(v);    // row_half_mirror: the other quad of the 8
+    return v;
+}
 
+constexpr int LAM_ROWS = 8;   // loading rows per wave
 __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict__ C,
                                                const double *__restrict__ E,
                                                const double *__restrict__ yy,
@@ -865,197 +879,256 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
                                                double *__restrict__ omega,
                                                double *__restrict__ cpart, DrawsDev dr,
                                                int64_t iter, int gen) {
-    // per system: the current column pair (L[r][k], L[r][k+1]) of every row r, then x
-    __shared__ __attribute__((aligned(16))) double LS[4][2 * KP];
+    // per system: rows' unnormalised column pair of the current step (+1 row of padding:
+    // the 8 systems' images start 4 banks apart), and the rhs of the forward solve
+    __shared__ __attribute__((aligned(16))) double LS[LAM_ROWS][KP + 1][2];
+    __shared__ __attribute__((aligned(16))) double BS[LAM_ROWS][KP + 2];
+    // per system: v = L^{-1} blam (dc:143) and 1 / L[r][r], written at each pivot step
+    __shared__ __attribute__((aligned(16))) double VS[LAM_ROWS][KP + 2];
+    __shared__ __attribute__((aligned(16))) double IS[LAM_ROWS][KP + 2];
     const int m = blockIdx.y;
     const int mg = d.shard0 + m;
-    const int lane = threadIdx.x, qw = lane >> 4, l = lane & 15;
-    const int j = blockIdx.x * 4 + qw;
+    const int lane = threadIdx.x, grp = lane >> 3, l = lane & 7;
+    const int j = blockIdx.x * LAM_ROWS + grp;
     const bool valid = j < d.P;
     const int jj = valid ? j : 0;
-    const int r0 = l, r1 = l + 16;
-    const bool rv0 = valid && r0 < d.K, rv1 = valid && r1 < d.K;
-    // 32-bit element offsets (base + 32-bit VGPR offset addressing; every array here is
-    // < 2^31 elements at the supported sizes) keep the per-lane address state small
     const uint32_t rowoff = (uint32_t)(m * d.PP + jj) * KP;
+    const uint32_t toff = (uint32_t)mg * KP;
+    bool rv[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) rv[b] = valid && l + 8 * b < d.K;
+    const double psj = valid ? ps[(uint32_t)(m * d.PP + jj)] : 0.0;
+    const double yyj = (valid && l == 0) ? yy[(uint32_t)(m * d.PP + jj)] : 0.0;
+    const double *pin = plam_src ? plam_src : psi;
+    // Plam_j (dc:176) and blam = ps_j eta' Y_j (dc:141), loaded ahead of the draw code
+    auto plam_of = [&](int b) {
+        const int r = l + 8 * b;
+        const double p = rv[b] ? pin[rowoff + r] : 0.0;
+        return plam_src ? p : p * (rv[b] ? tau_cur[toff + r] : 0.0);
+    };
+    double plam[4], bv[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        plam[b] = plam_of(b);
+        bv[b] = psj * (valid ? C[rowoff + l + 8 * b] : 0.0);
+    }
+    // ---- the row's variates: z (dc:142), the psi gammas (dc:150), the ps gamma (dc:170),
+    //      formed before the 80-value rows are live (the draw code needs ~60 registers)
+    double z[4], G[4], Gps = 0.0;
     const uint32_t ti = (uint32_t)(iter - dr.first_iter);
     const uint32_t drow = (ti * (uint32_t)d.g + (uint32_t)mg) * (uint32_t)d.P + (uint32_t)jj;
-    const uint32_t toff = (uint32_t)mg * KP;
-    // ---- loads that form Q_j and b_j, and the row's draws (all issued up front: the
-    //      draws arrive during the Q build and factorisation instead of stalling the solve)
-    const double psj = valid ? ps[(uint32_t)(m * d.PP + jj)] : 0.0;
-    const double tr0 = rv0 ? tau_cur[toff + r0] : 0.0, tr1 = rv1 ? tau_cur[toff + r1] : 0.0;
-    const double *pin = plam_src ? plam_src : psi;
-    const double pin0 = rv0 ? pin[rowoff + r0] : 0.0, pin1 = rv1 ? pin[rowoff + r1] : 0.0;
-    const double c0 = valid ? C[rowoff + r0] : 0.0, c1 = valid ? C[rowoff + r1] : 0.0;
     const uint32_t dk = drow * (uint32_t)d.K;
-    double z0, z1, G0, G1, Gps;
-    if (!gen) {       // injected, or k_draws buffers (the paths other than one rank's fused chain)
-        z0 = rv0 ? dr.NL[dk + r0] : 0.0; z1 = rv1 ? dr.NL[dk + r1] : 0.0;       // dc:142
-        G0 = rv0 ? dr.Gpsi[dk + r0] : 0.0; G1 = rv1 ? dr.Gpsi[dk + r1] : 0.0;   // dc:150
-        Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;                           // dc:170
-    } else {          // drawn here, at the counters k_draws uses (identical values); independent
-                      // of the factorisation below, so it fills the wave's issue gaps
+    if (!gen) {       // injected, or k_draws buffers (the paths other than the fused chain)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            z[b] = rv[b] ? dr.NL[dk + l + 8 * b] : 0.0;
+            G[b] = rv[b] ? dr.Gpsi[dk + l + 8 * b] : 0.0;
+        }
+        Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;
+    } else {          // drawn here, at the counters k_draws uses (identical values)
         const Rng rng(d.seed);
         const uint32_t it32 = (uint32_t)iter, mg32 = (uint32_t)mg, j32 = (uint32_t)jj;
-        // lane l draws normal pair l (indices 2l, 2l + 1); row index r comes from lane r / 2
-        double n0 = 0.0, n1 = 0.0;
-        if (valid && 2 * l < d.K) rng.normal2(SITE_LAMBDA, mg32, j32, (uint32_t)l, it32, n0, n1);
-        const int src0 = (qw << 4) | (r0 >> 1), src1 = (qw << 4) | (r1 >> 1);
-        const double a0 = __shfl(n0, src0, 64), b0 = __shfl(n1, src0, 64);
-        const double a1 = __shfl(n0, src1, 64), b1 = __shfl(n1, src1, 64);
-        z0 = rv0 ? ((r0 & 1) ? b0 : a0) : 0.0;
-        z1 = rv1 ? ((r1 & 1) ? b1 : a1) : 0.0;
+        // lane l draws normal pairs l and l + 8 (indices 2l, 2l+1, 2l+16, 2l+17); row r_b
+        // = l + 8b takes element r_b & 1 of pair (l >> 1) + 4b, i.e. pair slot b >> 1 of
+        // lane (l >> 1) + 4 (b & 1) of the group
+        double n0 = 0.0, n1 = 0.0, n2 = 0.0, n3 = 0.0;
+        if (valid) {
+            rng.normal2(SITE_LAMBDA, mg32, j32, (uint32_t)l, it32, n0, n1);
+            rng.normal2(SITE_LAMBDA, mg32, j32, (uint32_t)l + 8u, it32, n2, n3);
+        }
+        const int odd = l & 1;   // lanes l and l ^ 1 read the same source: both elements move
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int src = (grp << 3) | ((l >> 1) + 4 * (b & 1));
+            const double x0 = __shfl((b >> 1) ? n2 : n0, src, 64);
+            const double x1 = __shfl((b >> 1) ? n3 : n1, src, 64);
+            z[b] = rv[b] ? (odd ? x1 : x0) : 0.0;
+        }
         const double shp = d.df * 0.5 + 0.5;
-        G0 = rv0 ? rng.gamma(shp, SITE_PSI, mg32, j32, (uint32_t)r0, it32) : 0.0;
-        G1 = rv1 ? rng.gamma(shp, SITE_PSI, mg32, j32, (uint32_t)r1, it32) : 0.0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            G[b] = rv[b] ? rng.gamma(shp, SITE_PSI, mg32, j32, (uint32_t)(l + 8 * b), it32) : 0.0;
         Gps = (valid && l == 0) ? rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg32, j32, 0u, it32) : 0.0;
     }
-    const double yyj = (valid && l == 0) ? yy[(uint32_t)(m * d.PP + jj)] : 0.0;
-    const double *Ea = E + ((uint32_t)m * KP + r0) * KP, *Eb = E + ((uint32_t)m * KP + r1) * KP;
-    constexpr int KH = KP / 2;       // rows < 16 only ever touch columns < 16 (lower triangle)
-    double qa[KH], qb[KP];
+    // ---- Q_j rows r_b, columns <= 8b + 7: ps_j * eta2 + diag(Plam_j) (dc:141), identity padding
+    double q0[8], q1[16], q2[24], q3[32];
+    auto build = [&](auto &q, auto NB) {
+        constexpr int b = decltype(NB)::value, nc = 8 * b + 8;
+        const int r = l + 8 * b;
+        const double *Er = E + ((uint32_t)m * KP + r) * KP;
 #pragma unroll
-    for (int c = 0; c < KP; c += 2) {
-        const d2 eb = *reinterpret_cast<const d2 *>(Eb + c);
-        qb[c] = eb.x; qb[c + 1] = eb.y;
-        if (c < KH) {
-            const d2 ea = *reinterpret_cast<const d2 *>(Ea + c);
-            qa[c] = ea.x; qa[c + 1] = ea.y;
+        for (int c = 0; c < nc; c += 2) {
+            const d2 e = *reinterpret_cast<const d2 *>(Er + c);
+            q[c] = psj * e.x;
+            q[c + 1] = psj * e.y;
         }
-    }
-    // ---- Q_j rows r0, r1: ps_j * eta2 + diag(Plam_j) (dc:141), identity padding
-    const double plam0 = plam_src ? pin0 : pin0 * tr0, plam1 = plam_src ? pin1 : pin1 * tr1;   // dc:176
 #pragma unroll
-    for (int c = 0; c < KP; ++c) {
-        qb[c] = psj * qb[c];
-        if (c == r1) qb[c] = rv1 ? plam1 + qb[c] : 1.0;
-        if (c < KH) {
-            qa[c] = psj * qa[c];
-            if (c == r0) qa[c] = rv0 ? plam0 + qa[c] : 1.0;
-        }
-    }
-    double bva = psj * c0, bvb = psj * c1;        // blam = ps_j eta' Y_j (dc:141)
-    double va = 0.0, vb = 0.0;                    // v = L^{-1} blam (dc:143), rows r0, r1
-    double ia = 0.0, ib = 0.0;                    // 1 / L[r][r], rows r0, r1
-    double *Ls = LS[qw];
-    // ---- factorisation, two pivots per step, forward solve fused; the pair's L
-    //      column goes through the LDS staging row Ls (overwritten every step)
+        for (int c = 8 * b; c < nc; ++c)
+            if (c == r) q[c] = rv[b] ? plam[b] + q[c] : 1.0;
+    };
+    build(q0, std::integral_constant<int, 0>{});
+    build(q1, std::integral_constant<int, 1>{});
+    build(q2, std::integral_constant<int, 2>{});
+    build(q3, std::integral_constant<int, 3>{});
+    double(*Ls)[2] = LS[grp];
+    double *Bs = BS[grp], *Vs = VS[grp], *Is = IS[grp];
+    // ---- factorisation, two pivots per step, forward solve fused
     static_for<KP / 2>([&](auto JC) {
-        constexpr int jp = decltype(JC)::value, k = 2 * jp;
-        double a, b, c2, bk, bk1;
-        if constexpr (k < 16) {
-            a = bcast16<k>(qa[k]);
-            b = bcast16<k + 1>(qa[k]);
-            c2 = bcast16<k + 1>(qa[k + 1]);
-            bk = bcast16<k>(bva);
-            bk1 = bcast16<k + 1>(bva);
-        } else {
-            a = bcast16<k - 16>(qb[k]);
-            b = bcast16<k - 15>(qb[k]);
-            c2 = bcast16<k - 15>(qb[k + 1]);
-            bk = bcast16<k - 16>(bvb);
-            bk1 = bcast16<k - 15>(bvb);
-        }
+        constexpr int k = 2 * decltype(JC)::value;
+        constexpr int b0 = k / 8;               // the first block with rows >= k
+        auto put = [&](auto &q, auto NB) {
+            constexpr int b = decltype(NB)::value;
+            if constexpr (b >= b0) {
+                const int r = l + 8 * b;
+                d2 v;
+                v.x = q[k];
+                v.y = q[k + 1];
+                *reinterpret_cast<d2 *>(Ls[r]) = v;
+                Bs[r] = bv[b];
+            }
+        };
+        put(q0, std::integral_constant<int, 0>{});
+        put(q1, std::integral_constant<int, 1>{});
+        put(q2, std::integral_constant<int, 2>{});
+        put(q3, std::integral_constant<int, 3>{});
+        __builtin_amdgcn_wave_barrier();
+        const d2 pk = *reinterpret_cast<const d2 *>(Ls[k]);
+        const d2 pk1 = *reinterpret_cast<const d2 *>(Ls[k + 1]);
+        const d2 bb = *reinterpret_cast<const d2 *>(Bs + k);
+        const double a = pk.x, bq = pk1.x, c2 = pk1.y;
         const double i00 = rsqrt_f64(a);
-        const double l00 = a * i00, l10 = b * i00;
+        const double l00 = a * i00, l10 = bq * i00;
         const double d11 = c2 - l10 * l10;
         const double i11 = rsqrt_f64(d11);
         const double l11 = d11 * i11;
-        const double v0 = bk * i00, v1 = (bk1 - l10 * v0) * i11;
-        auto rowpiv = [&](auto &q, int r, double &bv, double &vr, double &ir, double &lr0, double &lr1) {
-            if (r > k + 1) {
-                lr0 = q[k] * i00;
-                lr1 = (q[k + 1] - lr0 * l10) * i11;
-            } else if (r == k + 1) {
-                lr0 = l10;
-                lr1 = l11;
-            } else if (r == k) {
-                lr0 = l00;
-                lr1 = 0.0;
-            } else {
-                lr0 = 0.0;
-                lr1 = 0.0;
+        const double v0 = bb.x * i00, v1 = (bb.y - l10 * v0) * i11;
+        const double t10 = l10 * i11;
+        if (l == 0) {
+            d2 v, iv;
+            v.x = v0; v.y = v1; iv.x = i00; iv.y = i11;
+            *reinterpret_cast<d2 *>(Vs + k) = v;
+            *reinterpret_cast<d2 *>(Is + k) = iv;
+        }
+        double al[4], be[4];
+        auto piv = [&](auto &q, auto NB) {
+            constexpr int b = decltype(NB)::value;
+            al[b] = 0.0;
+            be[b] = 0.0;
+            if constexpr (b >= b0) {
+                const int r = l + 8 * b;
+                const double lr0 = q[k] * i00;
+                const double lr1 = (q[k + 1] - lr0 * l10) * i11;
+                if (r > k + 1) {
+                    q[k] = lr0;
+                    q[k + 1] = lr1;
+                    al[b] = i00 * fma(-lr1, t10, lr0);
+                    be[b] = lr1 * i11;
+                    bv[b] = fma(-lr1, v1, fma(-lr0, v0, bv[b]));
+                } else if (r == k + 1) {
+                    q[k] = l10;
+                    q[k + 1] = l11;
+                } else if (r == k) {
+                    q[k] = l00;
+                    q[k + 1] = 0.0;
+                }
             }
-            q[k] = lr0;
-            q[k + 1] = lr1;
-            if (r >= k) {
-                d2 v;
-                v.x = lr0;
-                v.y = lr1;
-                *reinterpret_cast<d2 *>(Ls + 2 * r) = v;
-            }
-            if (r == k) { vr = v0; ir = i00; }
-            if (r == k + 1) { vr = v1; ir = i11; }
-            if (r > k + 1) bv = fma(-lr1, v1, fma(-lr0, v0, bv));
         };
-        double la0 = 0.0, la1 = 0.0, lb0, lb1;
-        if constexpr (k < 16) rowpiv(qa, r0, bva, va, ia, la0, la1);
-        rowpiv(qb, r1, bvb, vb, ib, lb0, lb1);
+        piv(q0, std::integral_constant<int, 0>{});
+        piv(q1, std::integral_constant<int, 1>{});
+        piv(q2, std::integral_constant<int, 2>{});
+        piv(q3, std::integral_constant<int, 3>{});
+        // rank-2 trailing update of every row's columns k+2 .. 8b+7 from the image; the
+        // FMAs are pinned per column (hipcc would otherwise sink each to its consumer)
+        {
+            constexpr int cs = k + 2, ce = KP;
 #pragma unroll
-        for (int c = k + 2; c < KP; ++c) {
-            const d2 lc = *reinterpret_cast<const d2 *>(Ls + 2 * c);
-            if constexpr (k < 16) {
-                if (c < KH) qa[c < KH ? c : 0] = fma(-la1, lc.y, fma(-la0, lc.x, qa[c < KH ? c : 0]));
+            for (int c = cs; c < ce; ++c) {
+                const d2 qc = *reinterpret_cast<const d2 *>(Ls[c]);
+                if (c < 8) q0[c < 8 ? c : 0] = fma(-be[0], qc.y, fma(-al[0], qc.x, q0[c < 8 ? c : 0]));
+                if (c < 16) q1[c < 16 ? c : 0] = fma(-be[1], qc.y, fma(-al[1], qc.x, q1[c < 16 ? c : 0]));
+                if (c < 24) q2[c < 24 ? c : 0] = fma(-be[2], qc.y, fma(-al[2], qc.x, q2[c < 24 ? c : 0]));
+                q3[c] = fma(-be[3], qc.y, fma(-al[3], qc.x, q3[c]));
             }
-            qb[c] = fma(-lb1, lc.y, fma(-lb0, lc.x, qb[c]));
-        }
 #pragma unroll
-        for (int c = k + 2; c < KP; ++c) {
-            if (k < 16 && c < KH) asm volatile("" : "+v"(qa[c < KH ? c : 0]));
-            asm volatile("" : "+v"(qb[c]));
+            for (int c = cs; c < ce; ++c) {
+                if (c < 8) asm volatile("" : "+v"(q0[c < 8 ? c : 0]));
+                if (c < 16) asm volatile("" : "+v"(q1[c < 16 ? c : 0]));
+                if (c < 24) asm volatile("" : "+v"(q2[c < 24 ? c : 0]));
+                asm volatile("" : "+v"(q3[c]));
+            }
         }
     });
-    // ---- back solve L' x = w, w = v + z (dc:142-144), pivots (c, c-1) from the bottom.
-    //      x_c = (w_c - sum_{r>c} L[r][c] x_r) / L[c][c]: the sums over the rows below are
-    //      dot products across the 16 lanes (rowsum16); L stays in the lanes' registers.
-    const double wa = va + z0, wb = vb + z1;
-    double xa = 0.0, xb = 0.0;
+    // ---- back solve L' x = w, w = v + z (dc:142-144), pivots (c, c-1) from the bottom:
+    //      x_c = (w_c - sum_{r>c} L[r][c] x_r) / L[c][c], the sums over the group's lanes
+    double x[4] = {0.0, 0.0, 0.0, 0.0};
+    double ww = 0.0, wv = 0.0;          // |w|^2 and w.v over the lane's rows
     static_for<KP / 2>([&](auto JC) {
-        constexpr int c = KP - 1 - 2 * decltype(JC)::value;     // odd: rows c, c-1 on the same side of 16
+        constexpr int c = KP - 1 - 2 * decltype(JC)::value;     // odd; c and c-1 in block cb
+        constexpr int cb = c / 8;
         double pa = 0.0, pb = 0.0;
-        if constexpr (c < 16) {
-            if (r0 > c) { pa = qa[c < 16 ? c : 0] * xa; pb = qa[c < 16 ? c - 1 : 0] * xa; }
-        }
-        pa = fma(qb[c], xb, pa);                  // r1 > c for c < 16; below the row for c >= 16
-        pb = fma(qb[c - 1], xb, pb);
-        if constexpr (c >= 16) {
-            if (r1 <= c) { pa = 0.0; pb = 0.0; }
-        }
-        pa = rowsum16(pa);
-        pb = rowsum16(pb);
+        auto part = [&](auto &q, auto NB) {
+            constexpr int b = decltype(NB)::value;
+            if constexpr (b > cb) {                              // every row of the block is > c
+                pa = fma(q[c], x[b], pa);
+                pb = fma(q[c - 1], x[b], pb);
+            } else if constexpr (b == cb) {    // rows l + 8b > c only: x is still 0 for the others
+                pa = fma(q[c], x[b], pa);
+                pb = fma(q[c - 1], x[b], pb);
+            }
+        };
+        part(q0, std::integral_constant<int, 0>{});
+        part(q1, std::integral_constant<int, 1>{});
+        part(q2, std::integral_constant<int, 2>{});
+        part(q3, std::integral_constant<int, 3>{});
+        pa = rowsum8(pa);
+        pb = rowsum8(pb);
+        auto &qc = [&]() -> auto & {
+            if constexpr (cb == 0) return q0;
+            else if constexpr (cb == 1) return q1;
+            else if constexpr (cb == 2) return q2;
+            else return q3;
+        }();
+        const d2 vv = *reinterpret_cast<const d2 *>(Vs + c - 1);
+        const d2 iv = *reinterpret_cast<const d2 *>(Is + c - 1);
         double t = 0.0;
-        if constexpr (c >= 16) {
-            if (r1 == c) { xb = (wb - pa) * ib; t = qb[c - 1] * xb; }
-            const double tb = bcast16<(c >= 16 ? c - 16 : 0)>(t);
-            if (r1 == c - 1) xb = (wb - pb - tb) * ib;
-        } else {
-            if (r0 == c) { xa = (wa - pa) * ia; t = qa[c < 16 ? c - 1 : 0] * xa; }
-            const double tb = bcast16<(c < 16 ? c : 0)>(t);
-            if (r0 == c - 1) xa = (wa - pb - tb) * ia;
+        if (l + 8 * cb == c) {
+            const double wc = vv.y + z[cb];
+            x[cb] = (wc - pa) * iv.y;
+            t = qc[c - 1] * x[cb];                               // L[c][c-1] x_c
+            ww = fma(wc, wc, ww);
+            wv = fma(wc, vv.y, wv);
+        }
+        const double tb = dpp8_d<0x101>(t);                      // row_shl:1: lane c%8 -> c%8 - 1
+        if (l + 8 * cb == c - 1) {
+            const double wc = vv.x + z[cb];
+            x[cb] = (wc - pb - tb) * iv.x;
+            ww = fma(wc, wc, ww);
+            wv = fma(wc, vv.x, wv);
         }
     });
-    if (!rv0) xa = 0.0;
-    if (!rv1) xb = 0.0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        if (!rv[b]) x[b] = 0.0;
     // ---- SS_j = yy_j - 2 x.C_j + x'E x (dc:169 by identity, no Y pass).  x = L'^{-1} w, so
-    //      x'Q_j x = |w|^2 and x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j: no E re-read.
-    double contrib = fma(wa, wa, wb * wb);
-    contrib = fma(-plam0 * xa, xa, contrib);
-    contrib = fma(-plam1 * xb, xb, contrib);
-    contrib = contrib / psj - 2.0 * fma(xa, c0, xb * c1);
+    //      x'Q_j x = |w|^2 and x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j: no E re-read;
+    //      ps_j x.C_j = x.blam = x.(L v) = (L'x).v = w.v: no C re-read.
+    double px = 0.0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) px = fma(plam_of(b) * x[b], x[b], px);   // reloaded (L2): not held live
+    double contrib = (ww - px - 2.0 * wv) / psj;
     contrib = valid ? contrib : 0.0;
-    contrib = rowsum16(contrib);
+    contrib = rowsum8(contrib);
     // ---- psi (dc:150, tau of the previous iteration, Q11) and the outputs
-    double psa = 0.0, psb = 0.0;
-    if (rv0) psa = (1.0 / (d.df * 0.5 + 0.5 * (xa * xa * tr0))) * G0;
-    if (rv1) psb = (1.0 / (d.df * 0.5 + 0.5 * (xb * xb * tr1))) * G1;
     if (valid) {
-        Lam[rowoff + r0] = xa;
-        Lam[rowoff + r1] = xb;
-        cpart[rowoff + r0] = psa * (xa * xa);       // mat = psijh .* Lambda.^2 (dc:156)
-        cpart[rowoff + r1] = psb * (xb * xb);
-        if (rv0) psi[rowoff + r0] = psa;
-        if (rv1) psi[rowoff + r1] = psb;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int r = l + 8 * b;
+            const double tr = rv[b] ? tau_cur[toff + r] : 0.0;
+            const double ps_b = rv[b] ? (1.0 / (d.df * 0.5 + 0.5 * (x[b] * x[b] * tr))) * G[b] : 0.0;
+            Lam[rowoff + r] = x[b];
+            cpart[rowoff + r] = ps_b * (x[b] * x[b]);           // mat = psijh .* Lambda.^2 (dc:156)
+            if (rv[b]) psi[rowoff + r] = ps_b;
+        }
         if (l == 0) {
             const double SS = yyj + contrib;
             const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;   // dc:170
@@ -1713,8 +1786,8 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, const double *plam_src, hipStream_t s, bool gen) {
     if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, plam_src, s);
-    hipLaunchKernelGGL(k_lambda, dim3(cdiv(d.P, 4), d.G), dim3(64), 0, s, d, b.C, b.E, b.yy, tau_cur,
-                       b.Lam, b.psi, plam_src, b.ps, b.omega, b.cpart, dr, iter, gen ? 1 : 0);
+    hipLaunchKernelGGL(k_lambda, dim3(cdiv(d.P, LAM_ROWS), d.G), dim3(64), 0, s, d, b.C, b.E, b.yy, tau_cur, b.Lam,
+                       b.psi, plam_src, b.ps, b.omega, b.cpart, dr, iter, gen ? 1 : 0);
 }
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(d.G, d.kp / 32);
