@@ -1499,13 +1499,10 @@ __global__ __launch_bounds__(256) void k_save(Dims d, const double *__restrict__
 // ============================================================================
 constexpr int AKC = ASM_KC, ALD = ASM_TILE + 16, ASM_THREADS = 256;
 
-__global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__restrict__ Lb, int LDB,
-                                                     int kext, const double *__restrict__ wsum,
-                                                     double inv_eff, const int2 *__restrict__ tiles, int T0,
-                                                     double *__restrict__ Sig) {
-    __shared__ double As[2][AKC][ALD], Bs[2][AKC][ALD];
-    __shared__ int shard_of[2][ASM_TILE];      // shard of the tile's rows / columns (epilogue coef)
-    const int2 T = tiles[xcd_remap(blockIdx.x, gridDim.x)];
+__device__ __forceinline__ void assemble_tile(const Dims &d, const double *__restrict__ Lb, int LDB, int kext,
+                                              const double *__restrict__ wsum, double inv_eff, int2 T, int T0,
+                                              double *__restrict__ Sig, double (*As)[AKC][ALD],
+                                              double (*Bs)[AKC][ALD], int (*shard_of)[ASM_TILE]) {
     double *__restrict__ St = Sig + (size_t)(tri(T.x) - tri(T0) + T.y) * ASM_TILE * ASM_TILE;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     shard_of[t >> 7][t & 127] = ((t < ASM_TILE ? T.x : T.y) * ASM_TILE + (t & 127)) / d.P;
@@ -1541,6 +1538,7 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
             Bs[buf][k + 1][srow] = rb[i].y;
         }
     };
+    gload(0);      // ahead of the tile's Sigma loads: staging chunk 0 waits only for its panels
     d4 acc[4][4];
     if (cross) {   // acc = the tile's old values (C/D layout: row q + 4g of 16-row tile u)
 #pragma unroll
@@ -1555,7 +1553,6 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
 #pragma unroll
             for (int v = 0; v < 4; ++v) acc[u][v] = d4{0.0, 0.0, 0.0, 0.0};
     }
-    gload(0);
     lstore(0);
     __syncthreads();
     for (int kc = 0, buf = 0; kc < kext; kc += AKC, buf ^= 1) {
@@ -1623,6 +1620,16 @@ __global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__res
             }
         }
     }
+}
+
+__global__ __launch_bounds__(256, 2) void k_assemble(Dims d, const double *__restrict__ Lb, int LDB,
+                                                     int kext, const double *__restrict__ wsum,
+                                                     double inv_eff, const int2 *__restrict__ tiles, int T0,
+                                                     double *__restrict__ Sig) {
+    __shared__ double As[2][AKC][ALD], Bs[2][AKC][ALD];
+    __shared__ int shard_of[2][ASM_TILE];      // shard of the tile's rows / columns (epilogue coef)
+    assemble_tile(d, Lb, LDB, kext, wsum, inv_eff, tiles[xcd_remap(blockIdx.x, gridDim.x)], T0, Sig, As, Bs,
+                  shard_of);
 }
 
 // Column stripe [c0, c0 + nc) of the symmetric Sigmaout from this rank's tile-packed block
