@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 // column tile kt (KW/32 tiles, adjacent in the 1-D grid so the wide layouts re-read Y from L2),
 // reduction over j in chunks of 8: lane (r, q) holds Y[i0+r][8t+2q .. +1] (16 B);
 // k-step 2t uses element 0, 2t+1 element 1; the B operand (w_j L[j][2r], w_j L[j][2r+1])
-// uses the same j <-> (q, e) map.  Register double-buffered prefetch of 2 chunks.
+// uses the same j <-> (q, e) map.  Register prefetch 3 chunks ahead (ring of 4).
 // ============================================================================
 template <int KW>
 __device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restrict__ Y,
@@ -232,12 +232,21 @@ __device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restri
         acc[1][0] = mfma16x16x4(y1.y, b10, acc[1][0]);                              \
         acc[1][1] = mfma16x16x4(y1.y, b11, acc[1][1]);                              \
     }
+    // ring of 4 register buffers: chunk t + 3 is requested while chunk t multiplies, so three
+    // chunks (6 KB per wave) are in flight behind the MFMAs (nch is a multiple of 4: PP % 32 == 0)
+    d2 yC0, yC1, wC, lC0, lC1, yD0, yD1, wD, lD0, lD1;
     WP_LOAD(0, yA0, yA1, wA, lA0, lA1);
-    for (int t = 0; t < nch; t += 2) {
-        if (t + 1 < nch) WP_LOAD(t + 1, yB0, yB1, wB, lB0, lB1);
+    if (1 < nch) WP_LOAD(1, yB0, yB1, wB, lB0, lB1);
+    if (2 < nch) WP_LOAD(2, yC0, yC1, wC, lC0, lC1);
+    for (int t = 0; t < nch; t += 4) {
+        if (t + 3 < nch) WP_LOAD(t + 3, yD0, yD1, wD, lD0, lD1);
         WP_MMA(yA0, yA1, wA, lA0, lA1);
-        if (t + 2 < nch) WP_LOAD(t + 2, yA0, yA1, wA, lA0, lA1);
+        if (t + 4 < nch) WP_LOAD(t + 4, yA0, yA1, wA, lA0, lA1);
         if (t + 1 < nch) WP_MMA(yB0, yB1, wB, lB0, lB1);
+        if (t + 5 < nch) WP_LOAD(t + 5, yB0, yB1, wB, lB0, lB1);
+        if (t + 2 < nch) WP_MMA(yC0, yC1, wC, lC0, lC1);
+        if (t + 6 < nch) WP_LOAD(t + 6, yC0, yC1, wC, lC0, lC1);
+        if (t + 3 < nch) WP_MMA(yD0, yD1, wD, lD0, lD1);
     }
 #undef WP_LOAD
 #undef WP_MMA
@@ -734,7 +743,8 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
 // summed in LDS in a fixed order.
 // Lane (r, q) loads 16 B: Y[i][c0+2r .. +1] and eta[i][2r .. +1] (formed on the
 // fly from X and Z), i = 4s + q, so the MFMA tiles are even/odd columns x
-// even/odd k.  Register double-buffered prefetch, 4 k-steps per batch.
+// even/odd k.  Register double-buffered prefetch, 4 k-steps per batch (a ring of 3: same
+// time at c3 and c4, 180 VGPRs).
 // ============================================================================
 // IS_E: the A operand is eta itself, columns te*32.. (Yp = nullptr; Xa/Za point at
 // them); SAME_T: te == kt, so the A operand is the B operand (no extra loads).
