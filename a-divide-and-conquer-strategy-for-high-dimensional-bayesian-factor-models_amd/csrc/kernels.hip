@@ -911,17 +911,20 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
     const double yyj = (valid && l == 0) ? yy[(uint32_t)(m * d.PP + jj)] : 0.0;
     const double *pin = plam_src ? plam_src : psi;
     // Plam_j (dc:176) and blam = ps_j eta' Y_j (dc:141), loaded ahead of the draw code
-    auto plam_of = [&](int b) {
-        const int r = l + 8 * b;
-        const double p = rv[b] ? pin[rowoff + r] : 0.0;
-        return plam_src ? p : p * (rv[b] ? tau_cur[toff + r] : 0.0);
-    };
-    double plam[4], bv[4];
+    // (addresses are in range for every lane: jj is clamped and r < KP; the values are
+    // selected after the loads, so no load waits behind a branch)
+    double pv[4], tv[4], cv[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-        plam[b] = plam_of(b);
-        bv[b] = psj * (valid ? C[rowoff + l + 8 * b] : 0.0);
+        pv[b] = pin[rowoff + l + 8 * b];
+        tv[b] = tau_cur[toff + l + 8 * b];
+        cv[b] = C[rowoff + l + 8 * b];
     }
+    auto plam_of = [&](int b) {
+        const int r = l + 8 * b;
+        const double p = pin[rowoff + r], tr = tau_cur[toff + r];
+        return rv[b] ? (plam_src ? p : p * tr) : 0.0;
+    };
     // ---- the row's variates: z (dc:142), the psi gammas (dc:150), the ps gamma (dc:170),
     //      formed before the 80-value rows are live (the draw code needs ~60 registers)
     double z[4], G[4], Gps = 0.0;
@@ -961,21 +964,37 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
         Gps = (valid && l == 0) ? rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg32, j32, 0u, it32) : 0.0;
     }
     // ---- Q_j rows r_b, columns <= 8b + 7: ps_j * eta2 + diag(Plam_j) (dc:141), identity padding
+    //      (every row's E loads are issued before the first is consumed: one L2 round trip)
+    double plam[4], bv[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        plam[b] = rv[b] ? (plam_src ? pv[b] : pv[b] * tv[b]) : 0.0;
+        bv[b] = valid ? psj * cv[b] : 0.0;
+    }
     double q0[8], q1[16], q2[24], q3[32];
-    auto build = [&](auto &q, auto NB) {
+    auto load = [&](auto &q, auto NB) {
         constexpr int b = decltype(NB)::value, nc = 8 * b + 8;
-        const int r = l + 8 * b;
-        const double *Er = E + ((uint32_t)m * KP + r) * KP;
+        const double *Er = E + ((uint32_t)m * KP + l + 8 * b) * KP;
 #pragma unroll
         for (int c = 0; c < nc; c += 2) {
             const d2 e = *reinterpret_cast<const d2 *>(Er + c);
-            q[c] = psj * e.x;
-            q[c + 1] = psj * e.y;
+            q[c] = e.x;
+            q[c + 1] = e.y;
         }
+    };
+    auto build = [&](auto &q, auto NB) {
+        constexpr int b = decltype(NB)::value, nc = 8 * b + 8;
+        const int r = l + 8 * b;
+#pragma unroll
+        for (int c = 0; c < nc; ++c) q[c] *= psj;
 #pragma unroll
         for (int c = 8 * b; c < nc; ++c)
             if (c == r) q[c] = rv[b] ? plam[b] + q[c] : 1.0;
     };
+    load(q0, std::integral_constant<int, 0>{});
+    load(q1, std::integral_constant<int, 1>{});
+    load(q2, std::integral_constant<int, 2>{});
+    load(q3, std::integral_constant<int, 3>{});
     build(q0, std::integral_constant<int, 0>{});
     build(q1, std::integral_constant<int, 1>{});
     build(q2, std::integral_constant<int, 2>{});

@@ -278,457 +278,204 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
 }
 
 // ============================================================================
-// k_lambda: one workgroup per loading row j of shard m.               dc:140-145 (+150,156,169-171)
-//   Q_j = diag(Plam_j) + ps_j E_m (lower triangle read, as chol(...,'lower')),
-//   distributed as 8x8 register blocks over the nb = ceil(K/8) block rows:
-//     wave 0, threads 0..NB-1     diagonal blocks (J, J)
-//     wave 0, threads 32..32+NB-1 the right-hand side b = ps_j C_j as an extra
-//                                  block row: the forward solve L v = b rides
-//                                  along the factorisation (v_k = b_k / L_kk)
-//     waves 1.., threads 64..      off-diagonal blocks (I, J), I > J
-//   Right-looking: per pivot k the owners of block column k/8 scale column k into
-//   LDS, everyone with columns > k applies the rank-1 update from registers.
-//   Plam_j = psi_j o tau' (dc:176) is formed here from the previous iteration's psi
-//   and tau unless plam_src is given (first iteration after dcfm_set_state).
-//   Then Lambda_j = L' \ (v + z) (blocked back solve, z = normrnd dc:142),
-//   psi_j (dc:150), SS_j = yy_j - 2 x.C_j + x'E x, ps_j, omega_j (dc:169-171).
-//   Rows r >= K inside the last block are an identity pad.
+// k_lambda_w: one wave per loading row j (K = 33..128).        dc:140-145 (+150,156,169-171)
+// Q_j = R'R (R = Llam', dc:142) on the NB x NB upper tiles T_{Kc,I} (Kc <= I) of Q_j, all held
+// in this wave's registers in the fp64 MFMA C/D layout (lane (c16, q) holds T[q + 4g][c16],
+// g = 0..3).  That layout is the B operand of a product with k = q + 4g and the A operand of
+// its transpose, so per block column J, with U_JJ = L_JJ^{-1} from chol_inv16 (LDS):
+//   panel     R_{J,I}  = U_JJ T_{J,I}                (A = U_JJ from LDS, B = registers)
+//   trailing  T_{Kc,I} -= R_{J,Kc}' R_{J,I}           (both operands in registers)
+//   forward   b_I -= R_{J,I}' v_J,  v_J = U_JJ b_J    (dc:143, sums over q by lane shuffles)
+// and the back solve R x = v + z (dc:142-144) sums each block row's products in registers
+// before one reduction over the 16 lanes of a tile row.  No workgroup barriers: the row's
+// whole chain is one wave, and the CU's other waves (other rows) fill its latency.  The
+// epilogue forms psi (dc:150), cpart (dc:156) and SS_j = yy_j - 2 x.C_j + x'E x (dc:169 by
+// identity: x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j since x'Q_j x = |w|^2), ps, omega.
 // ============================================================================
-constexpr int lambda_threads(int KW) { return 64 + ((KW / 8) * (KW / 8 - 1) / 2 + 63) / 64 * 64; }
+template <int NB>
+__host__ __device__ constexpr int utix(int Kc, int I) { return Kc * NB - Kc * (Kc - 1) / 2 + (I - Kc); }
 
-template <int KW>
-__global__ __launch_bounds__(lambda_threads(KW)) void k_lambda(
-    Dims d, const double *__restrict__ C, const double *__restrict__ E, const double *__restrict__ yy,
-    const double *__restrict__ tau_cur, const double *__restrict__ plam_src, double *__restrict__ Lam,
-    double *__restrict__ psi, double *__restrict__ ps, double *__restrict__ omega, double *__restrict__ cpart,
-    DrawsDev dr, int64_t iter) {
-    constexpr int NB = KW / 8;
-    __shared__ __attribute__((aligned(16))) double col[KW + 8];   // pivot column; col[KW] = v_k
-    __shared__ __attribute__((aligned(16))) double sw[KW], sx[KW];
-    __shared__ double ikk[KW];
-    __shared__ double red[4];
-    const int j = blockIdx.x, m = blockIdx.y, mg = d.shard0 + m;
-    const int t = threadIdx.x, K = d.K;
-    const int nb = (K + 7) >> 3, nd = 8 * nb;
-    // role: 0 diagonal block, 1 right-hand side, 2 off-diagonal block, 3 idle
-    int role = 3, I = 0, J = 0;
-    if (t < 32) {
-        if (t < nb) { role = 0; I = J = t; }
-    } else if (t < 64) {
-        if (t - 32 < nb) { role = 1; J = t - 32; I = NB; }
-    } else {
-        int o = t - 64, jj = 0;
-        while (jj < NB - 1 && o >= NB - 1 - jj) { o -= NB - 1 - jj; ++jj; }
-        if (jj < NB - 1) {
-            J = jj;
-            I = jj + 1 + o;
-            if (I < nb) role = 2;
-        }
-    }
-    const double *Em = E + (size_t)m * KW * KW;
-    const size_t rowoff = ((size_t)m * d.PP + j) * KW;
-    const double psj = ps[(size_t)m * d.PP + j];
-    double a[8][8];
+// T_{Kc,I} -= R_{J,Kc}' R_{J,I}  (block column J's trailing update of one upper tile)
+template <int NB, int J, int Kc, int I>
+__device__ __forceinline__ void trail_tile(d4 *T) {
+    constexpr int a = utix<NB>(J, Kc), b = utix<NB>(J, I), t = utix<NB>(Kc, I);
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-        for (int v = 0; v < 8; ++v) a[u][v] = 0.0;
-    if (role == 0 || role == 2) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-#pragma unroll
-            for (int v = 0; v < 8; ++v) {
-                const int r = 8 * I + u, c = 8 * J + v;
-                double val;
-                if (r < K && c < K) {
-                    val = psj * Em[(size_t)r * KW + c];                  // ps_j * eta2 (dc:141)
-                    if (r == c) {                                         // diag(Plam_j) + ...
-                        const double pl = plam_src ? plam_src[rowoff + r]
-                                                   : psi[rowoff + r] * tau_cur[(size_t)mg * KW + r];   // dc:176
-                        val = pl + val;
-                    }
-                } else {
-                    val = (r == c) ? 1.0 : 0.0;
-                }
-                a[u][v] = val;
-            }
-        if (role == 0 && I == 0) ikk[0] = rsqrt_f64(a[0][0]);
-    } else if (role == 1) {
-#pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            const int c = 8 * J + v;
-            a[0][v] = (c < K) ? psj * C[rowoff + c] : 0.0;                // blam (dc:141)
-        }
-    }
-    __syncthreads();
-    // ---- factorisation with fused forward solve (dc:142 chol, dc:143 Llam \ blam)
-    for (int Jk = 0; Jk < nb; ++Jk) {
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-            const int k = 8 * Jk + kk;
-            if (J == Jk && role != 3) {
-                const double ik = ikk[k];
-                if (role == 0) {
-                    a[kk][kk] *= ik;
-#pragma unroll
-                    for (int u = kk + 1; u < 8; ++u) {
-                        a[u][kk] *= ik;
-                        col[8 * J + u] = a[u][kk];
-                    }
-                } else if (role == 2) {
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        a[u][kk] *= ik;
-                        col[8 * I + u] = a[u][kk];
-                    }
-                } else {
-                    a[0][kk] *= ik;
-                    col[KW] = a[0][kk];
-                }
-            }
-            __syncthreads();
-            if (role != 3 && J >= Jk) {
-                const bool same = (J == Jk);
-                double lc[8];
-#pragma unroll
-                for (int v = 0; v < 8; v += 2) {
-                    const d2 x2 = *reinterpret_cast<const d2 *>(col + 8 * J + v);
-                    lc[v] = x2.x;
-                    lc[v + 1] = x2.y;
-                }
-                if (role == 0) {
-#pragma unroll
-                    for (int v = 0; v < 8; ++v)
-                        if (!same || v > kk) {
-#pragma unroll
-                            for (int u = v; u < 8; ++u) a[u][v] -= lc[u] * lc[v];
-                        }
-                } else if (role == 2) {
-                    double lr[8];
-#pragma unroll
-                    for (int u = 0; u < 8; u += 2) {
-                        const d2 x2 = *reinterpret_cast<const d2 *>(col + 8 * I + u);
-                        lr[u] = x2.x;
-                        lr[u + 1] = x2.y;
-                    }
-#pragma unroll
-                    for (int v = 0; v < 8; ++v)
-                        if (!same || v > kk) {
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) a[u][v] -= lr[u] * lc[v];
-                        }
-                } else {
-                    const double lb = col[KW];
-#pragma unroll
-                    for (int v = 0; v < 8; ++v)
-                        if (!same || v > kk) a[0][v] -= lb * lc[v];
-                }
-            }
-            if (role == 0) {   // next pivot, from the owner's own registers
-                if (kk < 7) {
-                    if (J == Jk && k + 1 < nd) ikk[k + 1] = rsqrt_f64(a[kk + 1 < 8 ? kk + 1 : 7][kk + 1 < 8 ? kk + 1 : 7]);
-                } else if (J == Jk + 1) {
-                    ikk[k + 1] = rsqrt_f64(a[0][0]);
-                }
-            }
-            __syncthreads();
-        }
-    }
-    // ---- w = v + z   (dc:142 normrnd; dc:143-144: Lambda_j = L' \ (v + z))
-    if (role == 1) {
-#pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            const int c = 8 * J + v;
-            const double z = (c < K) ? dr.NL[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + c] : 0.0;
-            sw[c] = a[0][v] + z;
-        }
-    }
-    __syncthreads();
-    // ---- blocked back solve L' x = w, block rows from the bottom
-    for (int Jb = nb - 1; Jb >= 0; --Jb) {
-        if (role == 0 && J == Jb) {
-            double wv[8];
-#pragma unroll
-            for (int v = 0; v < 8; ++v) wv[v] = sw[8 * J + v];
-#pragma unroll
-            for (int v = 7; v >= 0; --v) {
-                const double xv = wv[v] * ikk[8 * J + v];
-                sx[8 * J + v] = xv;
-#pragma unroll
-                for (int u = 0; u < v; ++u) wv[u] -= a[v][u] * xv;
-            }
-        }
-        __syncthreads();
-        if (role == 2 && I == Jb) {
-            double xl[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) xl[u] = sx[8 * I + u];
-#pragma unroll
-            for (int v = 0; v < 8; ++v) {
-                double acc = sw[8 * J + v];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) acc -= a[u][v] * xl[u];
-                sw[8 * J + v] = acc;
-            }
-        }
-        __syncthreads();
-    }
-    // ---- epilogue: Lambda_j, psi_j (dc:150), SS identity and ps_j (dc:169-171)
-    double contrib = 0.0;
-    if (t < KW) {
-        const int r = t;
-        const double xr = (r < K) ? sx[r] : 0.0;
-        const double cjr = C[rowoff + r];
-        double ex = 0.0;                                                 // (E x)_r
-        {
-            double e8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-            int c = 0;
-            for (; c + 8 <= K; c += 8) {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) e8[u] += Em[(size_t)(c + u) * KW + r] * sx[c + u];
-            }
-            for (; c < K; ++c) e8[0] += Em[(size_t)c * KW + r] * sx[c];
-            ex = ((e8[0] + e8[1]) + (e8[2] + e8[3])) + ((e8[4] + e8[5]) + (e8[6] + e8[7]));
-        }
-        contrib = xr * (ex - 2.0 * cjr);
-        double psir = 0.0;
-        if (r < K) {
-            const double tr = tau_cur[(size_t)mg * KW + r];
-            const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xr * xr * tr));
-            const double G = dr.Gpsi[(((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j) * d.K + r];
-            psir = scale * G;
-            psi[rowoff + r] = psir;
-        }
-        Lam[rowoff + r] = xr;
-        cpart[rowoff + r] = psir * (xr * xr);          // mat = psijh .* Lambda.^2 (dc:156)
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) contrib += __shfl_xor(contrib, o, 64);
-    if ((t & 63) == 0) red[t >> 6] = contrib;
-    __syncthreads();
-    if (t == 0) {
-        double s = 0.0;
-        for (int w = 0; w < (KW + 63) / 64; ++w) s += red[w];
-        const double SS = yy[(size_t)m * d.PP + j] + s;
-        const double G = dr.Gps[((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j];
-        const double psn = (1.0 / (d.bs + 0.5 * SS)) * G;     // dc:170
-        ps[(size_t)m * d.PP + j] = psn;
-        omega[(size_t)m * d.PP + j] = 1.0 / psn;              // dc:171 (Q1)
-    }
+    for (int s4 = 0; s4 < 4; ++s4) T[t] = mfma16x16x4(-T[a][s4], T[b][s4], T[t]);
 }
 
-// ============================================================================
-// k_lambda_t: one 256-thread workgroup per loading row j, MFMA-tiled.   dc:140-145 (+150,156,169-171)
-// Q_j's lower triangle (nb = ceil(K/16) tile rows) as 16x16 tiles held in registers in
-// the fp64 MFMA C/D layout (lane (c, q) holds tile[q + 4g][c], g = 0..3), tile t (row-major
-// lower order) on wave t % 4, slot t / 4.  Per block column J:
-//   a. the diagonal tile goes to LDS;  b. wave 0 factors and inverts it (chol_inv16:
-//   U_JJ = L_JJ^{-1}) and advances the forward solve v_J = U_JJ b_J;  c. the panel tiles
-//   become L_IJ = A_IJ U_JJ' (one 16x16x16 MFMA product each, A_IJ through LDS into the
-//   A-operand layout), staged row-major in LDS, and update b_I -= L_IJ v_J;  d. every
-//   trailing tile takes A_IK -= L_IJ L_KJ' (4 MFMAs, both operands read from the panel).
-// Three barriers per block column (the per-pivot kernel needs two per pivot).  The L
-// tiles stay in the registers for the blocked back solve x = L^{-T}(v + z); the epilogue
-// forms psi, cpart and SS_j from |w|^2 (no E product), then ps, omega.
-// ============================================================================
-#ifndef DCFM_LT_MINW
-#define DCFM_LT_MINW 3
-#endif
 template <int KW, int NB>
-__global__ __launch_bounds__(256, DCFM_LT_MINW) void k_lambda_t(
+__global__ __launch_bounds__(64) void k_lambda_w(
     Dims d, const double *__restrict__ C, const double *__restrict__ E, const double *__restrict__ yy,
     const double *__restrict__ tau_cur, const double *__restrict__ plam_src, double *__restrict__ Lam,
     double *__restrict__ psi, double *__restrict__ ps, double *__restrict__ omega, double *__restrict__ cpart,
     DrawsDev dr, int64_t iter) {
-    // NB = ceil(K/16) tile rows exactly (template: slot arrays and unrolled loops sized to it)
-    constexpr int NBM = NB, NTM = NBM * (NBM + 1) / 2, SL = (NTM + 3) / 4, LD = 17, TZ = 16 * LD;
-    __shared__ double Sd[TZ], Ud[TZ], Pn[NBM * TZ];
-    __shared__ double vb[KW], vx[KW], part[NBM * 16];
+    constexpr int NT = NB * (NB + 1) / 2, LD = 17, TZ = 16 * LD, NH = KW / 64;
+    __shared__ double Sd[TZ], Ud[TZ];
+    __shared__ double vb[KW], vx[KW], ein[5][KW];   // per row index r: NL, Gpsi, tau, C, Plam
     __shared__ double lds_l[32], lds_u[16];
-    __shared__ double ein[5][KW];   // per row index r: NL, Gpsi, tau, C, Plam
     const int j = blockIdx.x, m = blockIdx.y, mg = d.shard0 + m;
-    const int t = threadIdx.x, lane = t & 63, c16 = lane & 15, q = lane >> 4;
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);   // scalar: tile coordinates live in SGPRs
+    const int lane = threadIdx.x, c16 = lane & 15, q = lane >> 4;
     const int K = d.K;
-    constexpr int nb = NB, NT = NTM;
     const double *Em = E + (size_t)m * KW * KW;
     const size_t rowoff = ((size_t)m * d.PP + j) * KW;
     const double psj = ps[(size_t)m * d.PP + j];
-    // the row's draws and epilogue inputs, issued with the Q_j loads: a load issued after
-    // the factorisation stalls the solve (nothing else hides it at 3 waves per SIMD)
-    // (parked in LDS, not registers: the NB = 7, 8 tile sets use every VGPR of 3 waves/SIMD)
+    // ---- every load issued before the first wait (indices clamped, values selected after)
     const size_t drow = ((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j;
-    if (t < KW) {
-        double zr = 0.0, Gr = 0.0, trr = 0.0, cr = 0.0, plr = 0.0;
-        if (t < K) {
-            zr = dr.NL[drow * d.K + t];                                     // dc:142
-            Gr = dr.Gpsi[drow * d.K + t];                                   // dc:150
-            trr = tau_cur[(size_t)mg * KW + t];
-            cr = C[rowoff + t];
-            plr = plam_src ? plam_src[rowoff + t] : psi[rowoff + t] * trr;  // dc:176
-        }
-        ein[0][t] = zr;
-        ein[1][t] = Gr;
-        ein[2][t] = trr;
-        ein[3][t] = cr;
-        ein[4][t] = plr;
+    double zr[NH], Gr[NH], trr[NH], cr[NH], pr[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const int r = lane + 64 * h, re = r < K ? r : 0;
+        zr[h] = dr.NL[drow * K + re];                                       // dc:142
+        Gr[h] = dr.Gpsi[drow * K + re];                                     // dc:150
+        trr[h] = tau_cur[(size_t)mg * KW + re];
+        cr[h] = C[rowoff + re];
+        pr[h] = (plam_src ? plam_src : psi)[rowoff + re];
     }
     const double yyj = yy[(size_t)m * d.PP + j], Gps = dr.Gps[drow];   // dc:169-170
-    // ---- Q_j tiles (dc:141: ps_j eta2 + diag(Plam_j)), identity padding
-    d4 acc[SL];
-    int tI[SL], tK[SL];
+    d4 T[NT];
+    static_for<NB>([&](auto KC) {
+        constexpr int Kc = decltype(KC)::value;
+        static_for<NB>([&](auto IC) {
+            constexpr int I = decltype(IC)::value;
+            if constexpr (I >= Kc) {
 #pragma unroll
-    for (int sl = 0; sl < SL; ++sl) {
-        const int tt = 4 * sl + wave;
-        tI[sl] = -1;
-        tK[sl] = -1;
-        acc[sl] = d4{0.0, 0.0, 0.0, 0.0};
-        if (tt < NT) {
-            int I, Kc;
-            tile::tri_pair(tt, I, Kc);
-            tI[sl] = I;
-            tK[sl] = Kc;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int r = 16 * I + q + 4 * g, c = 16 * Kc + c16;
-                double val = (r == c) ? 1.0 : 0.0;
-                if (r < K && c < K) {
-                    val = psj * Em[(size_t)r * KW + c];
-                    if (r == c) {
-                        const double pl = plam_src ? plam_src[rowoff + r]
-                                                   : psi[rowoff + r] * tau_cur[(size_t)mg * KW + r];   // dc:176
-                        val = pl + val;
-                    }
-                }
-                acc[sl][g] = val;
+                for (int g = 0; g < 4; ++g)
+                    T[utix<NB>(Kc, I)][g] = Em[(size_t)(16 * Kc + q + 4 * g) * KW + 16 * I + c16];
             }
-        }
+        });
+    });
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const int r = lane + 64 * h;
+        const bool tl = r < K;
+        ein[0][r] = tl ? zr[h] : 0.0;
+        ein[1][r] = tl ? Gr[h] : 0.0;
+        ein[2][r] = tl ? trr[h] : 0.0;
+        ein[3][r] = tl ? cr[h] : 0.0;
+        ein[4][r] = tl ? (plam_src ? pr[h] : pr[h] * trr[h]) : 0.0;    // Plam_j (dc:176)
+        vb[r] = tl ? psj * cr[h] : 0.0;                                  // blam (dc:141)
     }
-    if (t < KW) vb[t] = psj * ein[3][t];                              // blam (dc:141)
-    // ---- blocked factorisation with the forward solve
-    for (int J = 0; J < nb; ++J) {
-        const int td = J * (J + 1) / 2 + J, ow = td & 3, os = td >> 2;
-        if (wave == ow) {
-#pragma unroll
-            for (int sl = 0; sl < SL; ++sl)
-                if (sl == os) {
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) Sd[(q + 4 * g) * LD + c16] = acc[sl][g];
-                }
-        }
-        __syncthreads();
-        if (wave == 0) {
-            chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
-            __builtin_amdgcn_wave_barrier();
-            double v = 0.0;
-            if (lane < 16) {
-#pragma unroll
-                for (int c = 0; c < 16; ++c) v = fma(Ud[lane * LD + c], vb[16 * J + c], v);   // U is lower
-            }
-            __builtin_amdgcn_wave_barrier();
-            if (lane < 16) vb[16 * J + lane] = v;                       // v_J (dc:143)
-        }
-        __syncthreads();
-        // panel tiles (I, J), I > J, and the diagonal owner keeps U_JJ for the back solve
-#pragma unroll
-        for (int sl = 0; sl < SL; ++sl) {
-            if (tK[sl] == J && tI[sl] > J) {
-                double *P = Pn + tI[sl] * TZ;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) P[(q + 4 * g) * LD + c16] = acc[sl][g];   // A_IJ row-major
-                __builtin_amdgcn_wave_barrier();
-                d4 L = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4)       // L_IJ = A_IJ U_JJ':  A[i][k] = A_IJ[i][k], B[k][c] = U_JJ[c][k]
-                    L = mfma16x16x4(P[c16 * LD + 4 * s4 + q], Ud[c16 * LD + 4 * s4 + q], L);
-                acc[sl] = L;
-                __builtin_amdgcn_wave_barrier();
-                const double vJ = vb[16 * J + c16];
+    __syncthreads();
+    // ---- Q_j tiles: ps_j eta2 + diag(Plam_j) (dc:141), identity padding
+    static_for<NB>([&](auto KC) {
+        constexpr int Kc = decltype(KC)::value;
+        static_for<NB>([&](auto IC) {
+            constexpr int I = decltype(IC)::value;
+            if constexpr (I >= Kc) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    P[(q + 4 * g) * LD + c16] = L[g];                  // L_IJ row-major
-                    const double sv = rowsum16(L[g] * vJ);             // (L_IJ v_J)[q + 4g]
-                    if (c16 == 0) vb[16 * tI[sl] + q + 4 * g] -= sv;
+                    const int r = 16 * Kc + q + 4 * g, c = 16 * I + c16;
+                    double val = (r == c) ? 1.0 : 0.0;
+                    if (r < K && c < K) val = psj * T[utix<NB>(Kc, I)][g] + (r == c ? ein[4][r] : 0.0);
+                    T[utix<NB>(Kc, I)][g] = val;
                 }
-            } else if (tK[sl] == J && tI[sl] == J) {
-#pragma unroll
-                for (int g = 0; g < 4; ++g) acc[sl][g] = Ud[(q + 4 * g) * LD + c16];   // U_JJ, C/D layout
             }
-            __builtin_amdgcn_sched_barrier(0);
-        }
+        });
+    });
+    // ---- blocked factorisation with the forward solve
+    static_for<NB>([&](auto JC) {
+        constexpr int J = decltype(JC)::value, tJ = utix<NB>(J, J);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) Sd[(q + 4 * g) * LD + c16] = T[tJ][g];
         __syncthreads();
-        // trailing tiles (I, Kc), I >= Kc > J:  A_IK -= L_IJ L_KJ'
+        chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
+        __syncthreads();
+        double v = 0.0;
+        if (lane < 16) {
 #pragma unroll
-        for (int sl = 0; sl < SL; ++sl) {
-            if (tK[sl] > J) {
-                const double *PI = Pn + tI[sl] * TZ, *PK = Pn + tK[sl] * TZ;
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4)
-                    acc[sl] = mfma16x16x4(-PI[c16 * LD + 4 * s4 + q], PK[c16 * LD + 4 * s4 + q], acc[sl]);
-            }
-            __builtin_amdgcn_sched_barrier(0);   // one slot's operands live at a time
+            for (int c = 0; c < 16; ++c) v = fma(Ud[lane * LD + c], vb[16 * J + c], v);   // U is lower
         }
-    }
-    // ---- w = v + z (dc:142 normrnd), blocked back solve x_J = U_JJ' (w_J - sum_{I>J} L_IJ' x_I)
-    if (t < K) vb[t] += ein[0][t];
+        double u[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) u[s4] = Ud[c16 * LD + 4 * s4 + q];     // A operand of U_JJ
+#pragma unroll
+        for (int g = 0; g < 4; ++g) T[tJ][g] = Ud[(q + 4 * g) * LD + c16];      // U_JJ kept (back solve)
+        __syncthreads();
+        if (lane < 16) vb[16 * J + lane] = v;                                  // v_J (dc:143)
+        __syncthreads();
+        double vj[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) vj[g] = vb[16 * J + q + 4 * g];
+        static_for<NB>([&](auto IC) {                     // panel R_{J,I} = U_JJ T_{J,I}
+            constexpr int I = decltype(IC)::value;
+            if constexpr (I > J) {
+                constexpr int t = utix<NB>(J, I);
+                d4 R = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4) R = mfma16x16x4(u[s4], T[t][s4], R);
+                T[t] = R;
+                double pv = 0.0;                          // (R_{J,I}' v_J)[c16]: sum over rows q + 4g
+#pragma unroll
+                for (int g = 0; g < 4; ++g) pv = fma(R[g], vj[g], pv);
+                pv += __shfl_xor(pv, 16, 64);
+                pv += __shfl_xor(pv, 32, 64);
+                if (q == 0) vb[16 * I + c16] -= pv;
+            }
+        });
+        static_for<NB>([&](auto KC) {                     // trailing T_{Kc,I} -= R_{J,Kc}' R_{J,I}
+            constexpr int Kc = decltype(KC)::value;
+            static_for<NB>([&](auto IC) {
+                constexpr int I = decltype(IC)::value;
+                if constexpr (Kc > J && I >= Kc) trail_tile<NB, J, Kc, I>(T);
+            });
+        });
+    });
+    // ---- w = v + z (dc:142 normrnd), back solve R x = w (dc:144):
+    //      x_J = U_JJ' (w_J - sum_{I>J} R_{J,I} x_I); lane (c16, .) holds x_I[c16] in xr[I]
     __syncthreads();
-    for (int J = nb - 1; J >= 0; --J) {
 #pragma unroll
-        for (int sl = 0; sl < SL; ++sl) {
-            if (tK[sl] == J && tI[sl] > J) {                           // part_I = L_IJ' x_I
-                double p = 0.0;
+    for (int h = 0; h < NH; ++h) vb[lane + 64 * h] += ein[0][lane + 64 * h];
+    __syncthreads();
+    double xr[NB];
+    static_for<NB>([&](auto JJ) {
+        constexpr int J = NB - 1 - decltype(JJ)::value;
+        double pg[4] = {0.0, 0.0, 0.0, 0.0};
+        static_for<NB>([&](auto IC) {
+            constexpr int I = decltype(IC)::value;
+            if constexpr (I > J) {
 #pragma unroll
-                for (int g = 0; g < 4; ++g) p = fma(acc[sl][g], vx[16 * tI[sl] + q + 4 * g], p);
-                p += __shfl_xor(p, 16, 64);
-                p += __shfl_xor(p, 32, 64);
-                if (q == 0) part[tI[sl] * 16 + c16] = p;
+                for (int g = 0; g < 4; ++g) pg[g] = fma(T[utix<NB>(J, I)][g], xr[I], pg[g]);
             }
-        }
-        __syncthreads();
-        const int td = J * (J + 1) / 2 + J, ow = td & 3, os = td >> 2;
-        if (wave == ow) {
+        });
+        double sx = 0.0;
 #pragma unroll
-            for (int sl = 0; sl < SL; ++sl)
-                if (sl == os) {                                        // x_J = U_JJ' y
-                    double p = 0.0;
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const int r = q + 4 * g;
-                        double y = vb[16 * J + r];
-                        for (int I = J + 1; I < nb; ++I) y -= part[I * 16 + r];
-                        p = fma(acc[sl][g], y, p);
-                    }
-                    p += __shfl_xor(p, 16, 64);
-                    p += __shfl_xor(p, 32, 64);
-                    if (q == 0) vx[16 * J + c16] = p;
-                }
+        for (int g = 0; g < 4; ++g) {
+            double y = vb[16 * J + q + 4 * g];
+            if constexpr (J < NB - 1) y -= rowsum16(pg[g]);
+            sx = fma(T[utix<NB>(J, J)][g], y, sx);        // (U_JJ' y)[c16]: sum over rows q + 4g
         }
-        __syncthreads();
-    }
-    // ---- epilogue: Lambda_j, psi_j (dc:150), and SS_j = yy_j - 2 x.C_j + x'E x (dc:169 by
-    //      identity) with x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j, since x'Q_j x = |w|^2
-    //      for x = L'^{-1} w: no Lambda_m E_m product (formerly k_ss), then ps_j, omega_j
+        sx += __shfl_xor(sx, 16, 64);
+        sx += __shfl_xor(sx, 32, 64);
+        xr[J] = sx;
+    });
+#pragma unroll
+    for (int I = 0; I < NB; ++I)
+        if (q == 0) vx[16 * I + c16] = xr[I];
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+        if (lane + 64 * h >= 16 * NB) vx[lane + 64 * h] = 0.0;
+    __syncthreads();
+    // ---- epilogue: Lambda_j, psi_j (dc:150), cpart (dc:156), SS_j (dc:169), ps_j, omega_j
     double ssr = 0.0;
-    if (t < KW) {
-        const int r = t;
-        const double xr = (r < K) ? vx[r] : 0.0;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const int r = lane + 64 * h;
+        const double xv = (r < K) ? vx[r] : 0.0;
         double psir = 0.0;
         if (r < K) {
-            const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xr * xr * ein[2][r]));
+            const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xv * xv * ein[2][r]));
             psir = scale * ein[1][r];
             psi[rowoff + r] = psir;
             const double w = vb[r];
-            ssr = fma(w, w, -ein[4][r] * xr * xr) / psj - 2.0 * xr * ein[3][r];
+            ssr += fma(w, w, -ein[4][r] * xv * xv) / psj - 2.0 * xv * ein[3][r];
         }
-        Lam[rowoff + r] = xr;
-        cpart[rowoff + r] = psir * (xr * xr);          // mat = psijh .* Lambda.^2 (dc:156)
+        Lam[rowoff + r] = xv;
+        cpart[rowoff + r] = psir * (xv * xv);          // mat = psijh .* Lambda.^2 (dc:156)
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) ssr += __shfl_xor(ssr, o, 64);
-    if (lane == 0) part[wave] = ssr;                   // part[] is free after the back solve
-    __syncthreads();
-    if (t == 0) {
-        const double SS = yyj + ((part[0] + part[1]) + (part[2] + part[3]));
+    if (lane == 0) {
+        const double SS = yyj + ssr;
         const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;      // dc:170
         ps[(size_t)m * d.PP + j] = psn;
         omega[(size_t)m * d.PP + j] = 1.0 / psn;                 // dc:171 (Q1)
@@ -938,16 +685,9 @@ void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *tau_cur,
                    const double *plam_src, hipStream_t s) {
-    static const bool legacy = [] { const char *e = std::getenv("DCFM_LAMBDA_BLOCKED8"); return e && e[0] == '1'; }();
-    if (legacy) {
-        WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_lambda<KW>, dim3(d.P, d.G), dim3(lambda_threads(KW)), 0, s, d, b.C,
-                                               b.E, b.yy, tau_cur, plam_src, b.Lam, b.psi, b.ps, b.omega, b.cpart,
-                                               dr, iter));
-        return;
-    }
     const dim3 grid(d.P, d.G);
-#define LT(KWV, NBV)                                                                                              \
-    hipLaunchKernelGGL((k_lambda_t<KWV, NBV>), grid, dim3(256), 0, s, d, b.C, b.E, b.yy, tau_cur, plam_src, b.Lam, \
+#define LT(KWV, NBV)                                                                                             \
+    hipLaunchKernelGGL((k_lambda_w<KWV, NBV>), grid, dim3(64), 0, s, d, b.C, b.E, b.yy, tau_cur, plam_src, b.Lam, \
                        b.psi, b.ps, b.omega, b.cpart, dr, iter)
     switch ((d.K + 15) / 16) {            // K = 33..128: 3..8 tile rows
     case 3: LT(64, 3); break;

@@ -320,28 +320,34 @@ __device__ __forceinline__ double quad_bcast(double x) {
     return __hiloint2double(hi, lo);
 }
 
-// one step k = 4 kk + J of chol_inv16 (below); explicit scalars keep it in registers
+// one step k = 4 kk + J of chol_inv16 (below); explicit scalars keep it in registers.
+// The LDS hand-off carries UNSCALED values (column k below the pivot, row k of the
+// inverse), so it is issued at the start of the step and its round trip overlaps the
+// pivot's rsqrt chain; the scales come in afterwards as f = a_rk / a_kk (l_r l_c =
+// a_rk a_ck / a_kk, l_r u_c = a_rk R_kc / a_kk) and row k of the inverse times 1/sqrt(a_kk).
 template <int J>
 __device__ __forceinline__ void chol16_step(double &a0, double &a1, double &a2, double &a3, double &R0, double &R1,
                                             double &R2, double &R3, int kk, int r, int cg, double *lds_l,
                                             double *lds_u) {
     const int k = 4 * kk + J;
-    const double piv = readlane_d(a0, 4 * k + J);
-    const double ik = rsqrt_f64(piv);
-    const double v = quad_bcast<J>(a0);
-    const double l = (r > k) ? v * ik : (r == k ? piv * ik : 0.0);
-    if (cg == 0) lds_l[r] = l;
+    if (cg == J) lds_l[r] = (r > k) ? a0 : 0.0;                 // a[r][k], zero on and above the pivot
     if (r == k) {
-        R0 *= ik; R1 *= ik; R2 *= ik; R3 *= ik;
         lds_u[cg] = R0; lds_u[4 + cg] = R1; lds_u[8 + cg] = R2; lds_u[12 + cg] = R3;
     }
     __builtin_amdgcn_wave_barrier();
     const double *pl = lds_l + 4 * kk + cg;
     const double l0 = pl[0], l1 = pl[4], l2 = pl[8], l3 = pl[12];
     const double u0 = lds_u[cg], u1 = lds_u[4 + cg], u2 = lds_u[8 + cg], u3 = lds_u[12 + cg];
-    a0 = fma(-l, l0, a0); a1 = fma(-l, l1, a1); a2 = fma(-l, l2, a2); a3 = fma(-l, l3, a3);
-    const double lr = (r > k) ? l : 0.0;
-    R0 = fma(-lr, u0, R0); R1 = fma(-lr, u1, R1); R2 = fma(-lr, u2, R2); R3 = fma(-lr, u3, R3);
+    __builtin_amdgcn_sched_barrier(0);                          // the reads are in flight during the chain
+    const double v = quad_bcast<J>(a0);                         // a[r][k]
+    const double piv = readlane_d(a0, 4 * k + J);
+    const double ik = rsqrt_f64(piv);
+    const double f = (r > k) ? v * (ik * ik) : 0.0;
+    a0 = fma(-f, l0, a0); a1 = fma(-f, l1, a1); a2 = fma(-f, l2, a2); a3 = fma(-f, l3, a3);
+    R0 = fma(-f, u0, R0); R1 = fma(-f, u1, R1); R2 = fma(-f, u2, R2); R3 = fma(-f, u3, R3);
+    if (r == k) {
+        R0 *= ik; R1 *= ik; R2 *= ik; R3 *= ik;
+    }
     __builtin_amdgcn_wave_barrier();
 }
 

@@ -2,8 +2,6 @@
 (read once per process, so each case runs in a child process):
   DCFM_NOFUSE=1          K <= 32 through the side-stream layout (k_prep / k_asum /
                          k_xchol / k_wpass / k_zdraw / k_colsum / k_delta with events)
-  DCFM_LAMBDA_BLOCKED8=1 K > 32 loading rows through the 8x8 register-block kernel
-                         instead of the MFMA-tiled k_lambda_t
 Each child runs the injected-draw chain of a tests/test_gpu_parity.py case and checks
 every state field after every iteration against the oracle at the same 1e-10 bar."""
 import os
@@ -42,9 +40,7 @@ print("WORST", worst)
 """
 
 
-@pytest.mark.parametrize("env,case", [("DCFM_NOFUSE", "basic"), ("DCFM_NOFUSE", "K30"),
-                                      ("DCFM_LAMBDA_BLOCKED8", "K100_c4_shape"),
-                                      ("DCFM_LAMBDA_BLOCKED8", "K40_ragged")])
+@pytest.mark.parametrize("env,case", [("DCFM_NOFUSE", "basic"), ("DCFM_NOFUSE", "K30")])
 def test_alternate_path_parity(env, case):
     import test_gpu_parity as T
     if case not in T.CASES:
