@@ -320,15 +320,24 @@ __device__ __forceinline__ double quad_bcast(double x) {
     return __hiloint2double(hi, lo);
 }
 
+// 1/x to full fp64 precision from the hardware estimate: e = 1 - x y, y (1 + e + e^2 + e^3)
+// (error e^4; four dependent operations after v_rcp_f64)
+__device__ __forceinline__ double rcp_f64(double x) {
+    const double y = __builtin_amdgcn_rcp(x);
+    const double e = fma(-x, y, 1.0);
+    return fma(y, fma(fma(e, e, e), e, e), y);
+}
+
 // one step k = 4 kk + J of chol_inv16 (below); explicit scalars keep it in registers.
-// The LDS hand-off carries UNSCALED values (column k below the pivot, row k of the
-// inverse), so it is issued at the start of the step and its round trip overlaps the
-// pivot's rsqrt chain; the scales come in afterwards as f = a_rk / a_kk (l_r l_c =
-// a_rk a_ck / a_kk, l_r u_c = a_rk R_kc / a_kk) and row k of the inverse times 1/sqrt(a_kk).
+// Elimination in LDL' form: the update a_rc -= a_rk a_ck / a_kk (= l_r l_c) and the unit
+// inverse W_r -= (a_rk / a_kk) W_k need only 1/a_kk, so the per-pivot chain is readlane ->
+// rcp -> multiplier -> update, with no square root; the LDS hand-off (column k below the
+// pivot, row k of W, both unscaled) is issued first and overlaps it.  The pivot a_kk = d_k
+// is kept by row k's lanes for the final scaling L^{-1} = D^{-1/2} W.
 template <int J>
 __device__ __forceinline__ void chol16_step(double &a0, double &a1, double &a2, double &a3, double &R0, double &R1,
-                                            double &R2, double &R3, int kk, int r, int cg, double *lds_l,
-                                            double *lds_u) {
+                                            double &R2, double &R3, double &dr, int kk, int r, int cg,
+                                            double *lds_l, double *lds_u) {
     const int k = 4 * kk + J;
     if (cg == J) lds_l[r] = (r > k) ? a0 : 0.0;                 // a[r][k], zero on and above the pivot
     if (r == k) {
@@ -341,25 +350,22 @@ __device__ __forceinline__ void chol16_step(double &a0, double &a1, double &a2, 
     __builtin_amdgcn_sched_barrier(0);                          // the reads are in flight during the chain
     const double v = quad_bcast<J>(a0);                         // a[r][k]
     const double piv = readlane_d(a0, 4 * k + J);
-    const double ik = rsqrt_f64(piv);
-    const double f = (r > k) ? v * (ik * ik) : 0.0;
+    const double f = (r > k) ? v * rcp_f64(piv) : 0.0;
     a0 = fma(-f, l0, a0); a1 = fma(-f, l1, a1); a2 = fma(-f, l2, a2); a3 = fma(-f, l3, a3);
     R0 = fma(-f, u0, R0); R1 = fma(-f, u1, R1); R2 = fma(-f, u2, R2); R3 = fma(-f, u3, R3);
-    if (r == k) {
-        R0 *= ik; R1 *= ik; R2 *= ik; R3 *= ik;
-    }
+    if (r == k) dr = piv;
     __builtin_amdgcn_wave_barrier();
 }
 
 // Cholesky factor and inverse of the 16x16 diagonal block at (o, o) of Sm (lower
 // triangle read) on one wave: writes Ub(o.., o..) = L^{-1} (zeros above the diagonal).
-// The one-block kernels (k_prep, k_xchol) run this cold every iteration, so the code
-// is a rolled loop and the per-step latency chain is short: lane = 4 r + cg holds
-// row r, columns 4 i + cg (i = 0..3) of the working matrix in a0..a3 (shifted one
-// column group per outer step, so the pivot column is always a0) and of the
-// right-hand side of L U = I in R0..R3.  Step k: pivot by readlane, l_r by a DPP
-// quad broadcast, then one LDS round trip hands out column k of L (lds_l, 32 slots,
-// the upper 16 zero) and row k of U (lds_u, 16 slots).
+// The one-block kernels run this cold every iteration, so the code is a rolled loop and
+// the per-step latency chain is short: lane = 4 r + cg holds row r, columns 4 i + cg
+// (i = 0..3) of the working matrix in a0..a3 (shifted one column group per outer step,
+// so the pivot column is always a0) and of the unit inverse W (L = L1 D^{1/2}, W = L1^{-1})
+// in R0..R3.  Step k: pivot by readlane, a_rk by a DPP quad broadcast, one LDS round trip
+// hands out column k (lds_l, 32 slots, the upper 16 zero) and row k of W (lds_u, 16 slots);
+// at the end each row r scales W_r by 1/sqrt(d_r).
 template <int LDP>
 __device__ __forceinline__ void chol_inv16_p(const double *Sm, int o, double *Ub, double *lds_l, double *lds_u,
                                              int lane) {
@@ -368,17 +374,19 @@ __device__ __forceinline__ void chol_inv16_p(const double *Sm, int o, double *Ub
     double a0 = srow[0], a1 = srow[4], a2 = srow[8], a3 = srow[12];
     double R0 = (cg == r) ? 1.0 : 0.0, R1 = (4 + cg == r) ? 1.0 : 0.0;
     double R2 = (8 + cg == r) ? 1.0 : 0.0, R3 = (12 + cg == r) ? 1.0 : 0.0;
+    double dr = 1.0;
     if (lane < 16) lds_l[16 + lane] = 0.0;
 #pragma unroll 1
     for (int kk = 0; kk < 4; ++kk) {
-        chol16_step<0>(a0, a1, a2, a3, R0, R1, R2, R3, kk, r, cg, lds_l, lds_u);
-        chol16_step<1>(a0, a1, a2, a3, R0, R1, R2, R3, kk, r, cg, lds_l, lds_u);
-        chol16_step<2>(a0, a1, a2, a3, R0, R1, R2, R3, kk, r, cg, lds_l, lds_u);
-        chol16_step<3>(a0, a1, a2, a3, R0, R1, R2, R3, kk, r, cg, lds_l, lds_u);
+        chol16_step<0>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u);
+        chol16_step<1>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u);
+        chol16_step<2>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u);
+        chol16_step<3>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u);
         a0 = a1; a1 = a2; a2 = a3; a3 = 0.0;
     }
+    const double ik = rsqrt_f64(dr);                     // 1 / L_rr
     double *urow = Ub + (o + r) * LDP + o + cg;
-    urow[0] = R0; urow[4] = R1; urow[8] = R2; urow[12] = R3;
+    urow[0] = R0 * ik; urow[4] = R1 * ik; urow[8] = R2 * ik; urow[12] = R3 * ik;
 }
 __device__ __forceinline__ void chol_inv16(const double (*Sm)[KP + 1], int o, double (*Ub)[KP + 1],
                                            double *lds_l, double *lds_u, int lane) {

@@ -39,8 +39,8 @@ rep("""        for (int g = 0; g < 4; ++g) Sd[(q + 4 * g) * LD + c16] = T[tJ][g]
         __syncthreads();""", """        for (int g = 0; g < 4; ++g) Sd[(q + 4 * g) * LD + c16] = T[tJ][g];
         __syncthreads();
         PH_MARK(3);""")
-rep("""        chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane, hook);
-        __syncthreads();""", """        chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane, hook);
+rep("""        chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
+        __syncthreads();""", """        chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
         __syncthreads();
         PH_MARK(6);""")
 rep("""        double vj[4];
