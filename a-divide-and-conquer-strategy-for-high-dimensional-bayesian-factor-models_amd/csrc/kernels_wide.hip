@@ -142,94 +142,145 @@ __device__ __forceinline__ d2 row_normals(const Dims &d, const double *inj, bool
 }
 
 // ============================================================================
-// k_zdraw: per (shard m, 64 rows), one wave per 16 rows i.                  dc:101-107,121-123
+// k_zdraw: per (shard m, 16 ZD_RT rows i), the KW/16 output tiles of each product dealt
+// over the block's 4 waves (KW/64 tiles each, for ZD_RT 16-row tiles).     dc:101-107,121-123
 //   V' = W' - sr A X'        (= bz / s1r: Zmsg'(Y_i - sr L X_i) by the identity W = Y (w o L))
-//   Z' = M1 V' + U eps'      (M1 = s1r T, U from k_prep; KW x 16 as MT = KW/16 MFMA tiles)
+//   Z' = M1 V' + U eps'      (M1 = s1r T, U from k_prep)
 //   S' = W' - s1r A Z'       (the shard's X message, dc:121-123)
-// The f64 C/D layout of each product (row = q + 4g of tile mt) is directly the B
-// operand of the next one (k-step 4 mt + g), so nothing crosses LDS; the A
-// operands (A_m, M1, U) stream from L2.
+// The f64 C/D layout of a product (row = q + 4g of tile mt) is the B operand of the next
+// one (k-step 4 mt + g); V' and Z' pass between the waves through LDS (16 rows x KW),
+// the A operands (A_m, M1, U) stream from L2, each load serving the block's ZD_RT row tiles
+// (one wave per 16 rows with every tile left the MFMA pipe idle 80 % of the time at c4).
 // ============================================================================
+#ifndef DCFM_ZD_RT
+#define DCFM_ZD_RT 4
+#endif
+constexpr int ZD_RT = DCFM_ZD_RT;   // 16-row tiles per block: the A operands (A_m, M1, U) serve 4 (c4: 138 -> 81 us vs 1)
 template <int KW>
 __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W, const double *__restrict__ A,
                                                const double *__restrict__ ZM, const double *__restrict__ X,
                                                double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
                                                int64_t iter) {
-    constexpr int MT = KW / 16;
-    const int nrb = d.NP >> 6;
+    constexpr int MW = KW / 64, RT = ZD_RT;         // output tiles per wave, row tiles per block
+    __shared__ double Vs[RT][KW][16], Zs[RT][KW][16];
+    const int nrb = d.NP / (16 * RT);
     const int w = xcd_remap(blockIdx.x, gridDim.x);
     const int m = w / nrb, rb = w % nrb;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int c = lane & 15, q = lane >> 4;
     const int mg = d.shard0 + m;
-    const int i = rb * 64 + wave * 16 + c;
-    const bool live = i < d.n;
+    const int mt0 = wave * MW;
     const double *Am = A + (size_t)m * KW * KW;
     const double *M1 = ZM + (size_t)m * 4 * KW * KW, *U = M1 + 2 * KW * KW;
-    const double *Wi = W + ((size_t)m * d.NP + i) * KW;
-    const double *Xi = X + (size_t)i * KW;
-    // --- A X'
-    d4 av[MT];
+    int iv[RT];
+    bool live[RT];
+    const double *Wi[RT], *Xi[RT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) av[mt] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int h = 0; h < RT; ++h) {
+        iv[h] = (rb * RT + h) * 16 + c;
+        live[h] = iv[h] < d.n;
+        Wi[h] = W + ((size_t)m * d.NP + iv[h]) * KW;
+        Xi[h] = X + (size_t)iv[h] * KW;
+    }
+    // --- A X' for this wave's tiles
+    d4 av[RT][MW];
+#pragma unroll
+    for (int h = 0; h < RT; ++h)
+#pragma unroll
+        for (int u = 0; u < MW; ++u) av[h][u] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 2
     for (int t = 0; t < KW / 8; ++t) {
         const int kk = 8 * t + 2 * q;
-        const d2 xv = *reinterpret_cast<const d2 *>(Xi + kk);
+        d2 xv[RT];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-            const d2 a2 = *reinterpret_cast<const d2 *>(Am + (size_t)(16 * mt + c) * KW + kk);
-            av[mt] = mfma16x16x4(a2.x, xv.x, av[mt]);
-            av[mt] = mfma16x16x4(a2.y, xv.y, av[mt]);
-        }
-    }
-    // --- V' = W' - sr (A X')
+        for (int h = 0; h < RT; ++h) xv[h] = *reinterpret_cast<const d2 *>(Xi[h] + kk);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+        for (int u = 0; u < MW; ++u) {
+            const d2 a2 = *reinterpret_cast<const d2 *>(Am + (size_t)(16 * (mt0 + u) + c) * KW + kk);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) av[mt][g] = Wi[16 * mt + q + 4 * g] - d.sr * av[mt][g];
-    // --- Z' = M1 V' + U eps'      eps[i][kk] of dc:104, kk = 16 mt2 + 4 g + q
-    const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K;
-    d4 az[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) az[mt] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int mt2 = 0; mt2 < MT; ++mt2)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int kk = 16 * mt2 + 4 * g + q;
-            double e = 0.0;
-            if (live && kk < d.K) e = nz[kk];
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                const size_t o = (size_t)(16 * mt + c) * KW + kk;
-                az[mt] = mfma16x16x4(M1[o], av[mt2][g], az[mt]);
-                az[mt] = mfma16x16x4(U[o], e, az[mt]);
+            for (int h = 0; h < RT; ++h) {
+                av[h][u] = mfma16x16x4(a2.x, xv[h].x, av[h][u]);
+                av[h][u] = mfma16x16x4(a2.y, xv[h].y, av[h][u]);
             }
         }
+    }
+    // --- V' = W' - sr (A X') -> LDS
+#pragma unroll
+    for (int h = 0; h < RT; ++h)
+#pragma unroll
+        for (int u = 0; u < MW; ++u)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int k = 16 * (mt0 + u) + q + 4 * g;
+                Vs[h][k][c] = Wi[h][k] - d.sr * av[h][u][g];
+            }
+    __syncthreads();
+    // --- Z' = M1 V' + U eps'      eps[i][kk] of dc:104, kk = 4 t + q
+    d4 az[RT][MW];
+#pragma unroll
+    for (int h = 0; h < RT; ++h)
+#pragma unroll
+        for (int u = 0; u < MW; ++u) az[h][u] = d4{0.0, 0.0, 0.0, 0.0};
+    const size_t nzb = ((size_t)(iter - dr.first_iter) * d.g + mg) * d.n;
+#pragma unroll 2
+    for (int t = 0; t < KW / 4; ++t) {
+        const int kk = 4 * t + q;
+        double vb[RT], e[RT];
+#pragma unroll
+        for (int h = 0; h < RT; ++h) {
+            vb[h] = Vs[h][kk][c];
+            e[h] = (live[h] && kk < d.K) ? dr.NZ[(nzb + iv[h]) * d.K + kk] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < MW; ++u) {
+            const size_t o = (size_t)(16 * (mt0 + u) + c) * KW + kk;
+            const double m1 = M1[o], uu = U[o];
+#pragma unroll
+            for (int h = 0; h < RT; ++h) {
+                az[h][u] = mfma16x16x4(m1, vb[h], az[h][u]);
+                az[h][u] = mfma16x16x4(uu, e[h], az[h][u]);
+            }
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < RT; ++h)
+#pragma unroll
+        for (int u = 0; u < MW; ++u)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) Zs[h][16 * (mt0 + u) + q + 4 * g][c] = az[h][u][g];
+    __syncthreads();
     // --- S' = W' - s1r (A Z')
-    d4 as[MT];
+    d4 as[RT][MW];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) as[mt] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int h = 0; h < RT; ++h)
 #pragma unroll
-    for (int mt2 = 0; mt2 < MT; ++mt2)
+        for (int u = 0; u < MW; ++u) as[h][u] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 2
+    for (int t = 0; t < KW / 4; ++t) {
+        const int kk = 4 * t + q;
+        double zb[RT];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int kk = 16 * mt2 + 4 * g + q;
+        for (int h = 0; h < RT; ++h) zb[h] = Zs[h][kk][c];
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
-                as[mt] = mfma16x16x4(Am[(size_t)(16 * mt + c) * KW + kk], az[mt2][g], as[mt]);
+        for (int u = 0; u < MW; ++u) {
+            const double a1 = Am[(size_t)(16 * (mt0 + u) + c) * KW + kk];
+#pragma unroll
+            for (int h = 0; h < RT; ++h) as[h][u] = mfma16x16x4(a1, zb[h], as[h][u]);
         }
-    double *Zr = Z + ((size_t)m * d.NP + i) * KW;
-    double *Sr = Sp + ((size_t)m * d.NP + i) * KW;
+    }
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int h = 0; h < RT; ++h) {
+        double *Zr = Z + ((size_t)m * d.NP + iv[h]) * KW;
+        double *Sr = Sp + ((size_t)m * d.NP + iv[h]) * KW;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int k = 16 * mt + q + 4 * g;
-            if (live) Zr[k] = (k < d.K) ? az[mt][g] : 0.0;
-            Sr[k] = live ? Wi[k] - d.s1r * as[mt][g] : 0.0;
-        }
+        for (int u = 0; u < MW; ++u)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int k = 16 * (mt0 + u) + q + 4 * g;
+                if (live[h]) Zr[k] = (k < d.K) ? az[h][u][g] : 0.0;
+                Sr[k] = live[h] ? Wi[h][k] - d.s1r * as[h][u][g] : 0.0;
+            }
+    }
 }
 
 // ============================================================================
@@ -676,7 +727,7 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
                                            d.nranks > 1 ? b.xa_all : b.xa, b.XM));
 }
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
-    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_zdraw<KW>, dim3((d.NP / 64) * d.G), dim3(256), 0, s, d, b.W, b.A,
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_zdraw<KW>, dim3((d.NP / (16 * ZD_RT)) * d.G), dim3(256), 0, s, d, b.W, b.A,
                                            b.ZM, b.X, b.Z, b.Sp, dr, iter));
 }
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
