@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void k_gram(Dims d, const double *__restrict__
 template <int KW>
 __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__ A, double *__restrict__ ZM) {
     constexpr int NB = KW / tile::TS, NT = tile::ntiles(NB);
-    __shared__ double Ts[NT * tile::TSZ], Us[NT * tile::TSZ], dinv[KW];
+    __shared__ double Ts[NT * tile::TSZ], Us[NT * tile::TSZ], lds_l[32], lds_u[16];
     const int m = blockIdx.x, N = d.K, nb = (N + tile::TS - 1) / tile::TS, t = threadIdx.x;
     const double *Am = A + (size_t)m * KW * KW;
     for (int e = t; e < tile::ntiles(nb) * tile::TS * tile::TS; e += 256) {
@@ -98,8 +98,8 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
         Ts[tile::tix(I, J) * tile::TSZ + c * tile::TLD + r] = v;
     }
     __syncthreads();
-    tile::potrf(Ts, dinv, nb);
-    tile::trtri(Ts, dinv, Us, nb);
+    tile::potrf_inv(Ts, Us, nb, lds_l, lds_u);
+    tile::trtri(Ts, Us, nb);
     double *Zm = ZM + (size_t)m * 4 * KW * KW;
     tile::uut_store(Us, nb, N, d.s1r, Zm, KW, Zm + (size_t)2 * KW * KW);
 }
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 template <int KW>
 __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict__ xa_all, double *__restrict__ XM) {
     constexpr int NB = KW / tile::TS, NT = tile::ntiles(NB);
-    __shared__ double Ts[NT * tile::TSZ], Us[NT * tile::TSZ], dinv[KW];
+    __shared__ double Ts[NT * tile::TSZ], Us[NT * tile::TSZ], lds_l[32], lds_u[16];
     const int N = d.K, nb = (N + tile::TS - 1) / tile::TS, t = threadIdx.x;
     for (int e = t; e < tile::ntiles(nb) * tile::TS * tile::TS; e += 256) {
         int I, J;
@@ -126,8 +126,8 @@ __global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict_
         Ts[tile::tix(I, J) * tile::TSZ + c * tile::TLD + r] = v;
     }
     __syncthreads();
-    tile::potrf(Ts, dinv, nb);
-    tile::trtri(Ts, dinv, Us, nb);
+    tile::potrf_inv(Ts, Us, nb, lds_l, lds_u);
+    tile::trtri(Ts, Us, nb);
     tile::uut_store(Us, nb, N, d.sr, XM, KW, XM + (size_t)KW * KW);
 }
 

@@ -366,7 +366,8 @@ __device__ __forceinline__ void chol16_step(double &a0, double &a1, double &a2, 
 // in R0..R3.  Step k: pivot by readlane, a_rk by a DPP quad broadcast, one LDS round trip
 // hands out column k (lds_l, 32 slots, the upper 16 zero) and row k of W (lds_u, 16 slots);
 // at the end each row r scales W_r by 1/sqrt(d_r).
-template <int LDP>
+// COLMAJ: Ub is written column-major (element (r, c) at c LDP + r; tile_linalg.h layout)
+template <int LDP, bool COLMAJ = false>
 __device__ __forceinline__ void chol_inv16_p(const double *Sm, int o, double *Ub, double *lds_l, double *lds_u,
                                              int lane) {
     const int r = lane >> 2, cg = lane & 3;
@@ -385,8 +386,13 @@ __device__ __forceinline__ void chol_inv16_p(const double *Sm, int o, double *Ub
         a0 = a1; a1 = a2; a2 = a3; a3 = 0.0;
     }
     const double ik = rsqrt_f64(dr);                     // 1 / L_rr
-    double *urow = Ub + (o + r) * LDP + o + cg;
-    urow[0] = R0 * ik; urow[4] = R1 * ik; urow[8] = R2 * ik; urow[12] = R3 * ik;
+    if (COLMAJ) {
+        double *ucol = Ub + (o + cg) * LDP + o + r;
+        ucol[0] = R0 * ik; ucol[4 * LDP] = R1 * ik; ucol[8 * LDP] = R2 * ik; ucol[12 * LDP] = R3 * ik;
+    } else {
+        double *urow = Ub + (o + r) * LDP + o + cg;
+        urow[0] = R0 * ik; urow[4] = R1 * ik; urow[8] = R2 * ik; urow[12] = R3 * ik;
+    }
 }
 __device__ __forceinline__ void chol_inv16(const double (*Sm)[KP + 1], int o, double (*Ub)[KP + 1],
                                            double *lds_l, double *lds_u, int lane) {
