@@ -339,7 +339,8 @@ __device__ __forceinline__ void chol16_step(double &a0, double &a1, double &a2, 
                                             double &R2, double &R3, double &dr, int kk, int r, int cg,
                                             double *lds_l, double *lds_u) {
     const int k = 4 * kk + J;
-    if (cg == J) lds_l[r] = (r > k) ? a0 : 0.0;                 // a[r][k], zero on and above the pivot
+    const double v = quad_bcast<J>(a0);                         // a[r][k]
+    lds_l[r] = (r > k) ? v : 0.0;       // the quad's 4 lanes store the same value: no exec-mask branch
     if (r == k) {
         lds_u[cg] = R0; lds_u[4 + cg] = R1; lds_u[8 + cg] = R2; lds_u[12 + cg] = R3;
     }
@@ -348,12 +349,11 @@ __device__ __forceinline__ void chol16_step(double &a0, double &a1, double &a2, 
     const double l0 = pl[0], l1 = pl[4], l2 = pl[8], l3 = pl[12];
     const double u0 = lds_u[cg], u1 = lds_u[4 + cg], u2 = lds_u[8 + cg], u3 = lds_u[12 + cg];
     __builtin_amdgcn_sched_barrier(0);                          // the reads are in flight during the chain
-    const double v = quad_bcast<J>(a0);                         // a[r][k]
     const double piv = readlane_d(a0, 4 * k + J);
     const double f = (r > k) ? v * rcp_f64(piv) : 0.0;
     a0 = fma(-f, l0, a0); a1 = fma(-f, l1, a1); a2 = fma(-f, l2, a2); a3 = fma(-f, l3, a3);
     R0 = fma(-f, u0, R0); R1 = fma(-f, u1, R1); R2 = fma(-f, u2, R2); R3 = fma(-f, u3, R3);
-    if (r == k) dr = piv;
+    dr = (r == k) ? piv : dr;
     __builtin_amdgcn_wave_barrier();
 }
 
