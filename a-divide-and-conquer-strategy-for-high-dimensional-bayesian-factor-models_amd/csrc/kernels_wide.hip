@@ -534,57 +534,6 @@ __global__ __launch_bounds__(64) void k_lambda_w(
 }
 
 // ============================================================================
-// k_ss: residual sums and ps / omega of 16 loading rows per block      dc:169-171
-//   SS_j = yy_j - 2 lambda_j . C_j + lambda_j E lambda_j'   (identity; no third Y pass)
-// T = Lambda_m(rows) E_m as fp64 MFMA (A = 16 loading rows, B = E read directly),
-// 16x16 output tiles dealt over the 4 waves, then row dot products with lambda.
-// ============================================================================
-template <int KW>
-__global__ __launch_bounds__(256) void k_ss(Dims d, const double *__restrict__ Lam, const double *__restrict__ C,
-                                            const double *__restrict__ E, const double *__restrict__ yy,
-                                            double *__restrict__ ps, double *__restrict__ omega, DrawsDev dr,
-                                            int64_t iter) {
-    __shared__ double sred[4][16], slc[16];
-    const int m = blockIdx.y, mg = d.shard0 + m, j0 = 16 * blockIdx.x;
-    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c16 = lane & 15, q = lane >> 4;
-    const int K = d.K, nk = (K + 3) >> 2, nct = (K + 15) >> 4;
-    const double *Lm = Lam + ((size_t)m * d.PP + j0) * KW;            // rows j0.. (pad rows are zero)
-    const double *Em = E + (size_t)m * KW * KW;
-    double xe[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int ct = wave; ct < nct; ct += 4) {
-        d4 T = {0.0, 0.0, 0.0, 0.0};
-        for (int s4 = 0; s4 < nk; ++s4)
-            T = mfma16x16x4(Lm[(size_t)c16 * KW + 4 * s4 + q], Em[(size_t)(4 * s4 + q) * KW + 16 * ct + c16], T);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) xe[g] += rowsum16(T[g] * Lm[(size_t)(q + 4 * g) * KW + 16 * ct + c16]);
-    }
-    if (c16 == 0) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) sred[wave][q + 4 * g] = xe[g];
-    }
-    {   // lambda_j . C_j: row = t >> 4, 16 lanes over k
-        const int rr = t >> 4, l = t & 15;
-        const size_t ro = ((size_t)m * d.PP + j0 + rr) * KW;
-        double lc = 0.0;
-        for (int k = l; k < K; k += 16) lc = fma(Lam[ro + k], C[ro + k], lc);
-        lc = rowsum16(lc);
-        if (l == 0) slc[rr] = lc;
-    }
-    __syncthreads();
-    if (t < 16) {
-        const int j = j0 + t;
-        if (j < d.P) {
-            const double xEx = (sred[0][t] + sred[1][t]) + (sred[2][t] + sred[3][t]);
-            const double SS = yy[(size_t)m * d.PP + j] - 2.0 * slc[t] + xEx;
-            const double G = dr.Gps[((size_t)(iter - dr.first_iter) * d.g + mg) * d.P + j];
-            const double psn = (1.0 / (d.bs + 0.5 * SS)) * G;     // dc:170
-            ps[(size_t)m * d.PP + j] = psn;
-            omega[(size_t)m * d.PP + j] = 1.0 / psn;              // dc:171 (Q1)
-        }
-    }
-}
-
-// ============================================================================
 // block = (shard m, 32 columns); 8 row groups x 4 independent accumulators each.
 template <int KW>
 __global__ __launch_bounds__(256) void k_colsum(Dims d, const double *__restrict__ cpart, double *__restrict__ sloc) {

@@ -83,6 +83,31 @@ __device__ __forceinline__ void stepD(double &a0, double &a1, double &a2, double
     dr = (r == k) ? piv : dr;
 }
 
+
+// variant E: every lane stores its row of W each step into a 16 x 16 image (no branch)
+template <int J>
+__device__ __forceinline__ void stepE(double &a0, double &a1, double &a2, double &a3, double &R0, double &R1,
+                                      double &R2, double &R3, double &dr, int kk, int r, int cg,
+                                      double *lds_l, double *lds_w) {
+    const int k = 4 * kk + J;
+    const double v = quad_bcast<J>(a0);
+    lds_l[r] = (r > k) ? v : 0.0;
+    double *wr = lds_w + r * 16 + cg;
+    wr[0] = R0; wr[4] = R1; wr[8] = R2; wr[12] = R3;
+    __builtin_amdgcn_wave_barrier();
+    const double *pl = lds_l + 4 * kk + cg;
+    const double l0 = pl[0], l1 = pl[4], l2 = pl[8], l3 = pl[12];
+    const double *wk = lds_w + k * 16 + cg;
+    const double u0 = wk[0], u1 = wk[4], u2 = wk[8], u3 = wk[12];
+    __builtin_amdgcn_sched_barrier(0);
+    const double piv = readlane_d(a0, 4 * k + J);
+    const double f = (r > k) ? v * rcp_f64(piv) : 0.0;
+    a0 = fma(-f, l0, a0); a1 = fma(-f, l1, a1); a2 = fma(-f, l2, a2); a3 = fma(-f, l3, a3);
+    R0 = fma(-f, u0, R0); R1 = fma(-f, u1, R1); R2 = fma(-f, u2, R2); R3 = fma(-f, u3, R3);
+    dr = (r == k) ? piv : dr;
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <int V>
 __device__ __forceinline__ void cholX(const double *Sm, double *Ub, double *lds_l, double *lds_u, int lane) {
     constexpr int LDP = 17;
@@ -95,7 +120,12 @@ __device__ __forceinline__ void cholX(const double *Sm, double *Ub, double *lds_
     if (lane < 16) lds_l[16 + lane] = 0.0;
 #pragma unroll 1
     for (int kk = 0; kk < 4; ++kk) {
-        if (V == 3) {
+        if (V == 4) {
+            stepE<0>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u);
+            stepE<1>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u);
+            stepE<2>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u);
+            stepE<3>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u);
+        } else if (V == 3) {
             stepD<0>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u);
             stepD<1>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u);
             stepD<2>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u);
@@ -120,7 +150,7 @@ __device__ __forceinline__ void cholX(const double *Sm, double *Ub, double *lds_
 
 __global__ __launch_bounds__(64) void bench(double *sink, unsigned long long *cyc, int reps) {
     constexpr int LD = 17;
-    __shared__ double Sd[16 * LD], Ud[16 * LD], lds_l[32], lds_u[16], X[64];
+    __shared__ double Sd[16 * LD], Ud[16 * LD], lds_l[32], lds_u[256], X[64];
     const int lane = threadIdx.x, r = lane >> 2, cg = lane & 3;
     double acc = 0.0;
     for (int e = lane; e < 16 * 16; e += 64) {
@@ -199,7 +229,7 @@ __global__ __launch_bounds__(64) void bench(double *sink, unsigned long long *cy
         __builtin_amdgcn_wave_barrier();
         cholX<1>(Sd, U1, lds_l, lds_u, lane);
         __builtin_amdgcn_wave_barrier();
-        cholX<3>(Sd, U3, lds_l, lds_u, lane);
+        cholX<4>(Sd, U3, lds_l, lds_u, lane);
         __syncthreads();
         double md = 0.0;
         for (int e = lane; e < 256; e += 64) {
@@ -221,7 +251,7 @@ __global__ __launch_bounds__(64) void bench(double *sink, unsigned long long *cy
     if (lane == 0) cyc[blockIdx.x * 8 + 6] = (t1 - t0) / reps;
     t0 = stamp();
     for (int it = 0; it < reps; ++it) {
-        cholX<3>(Sd, Ud, lds_l, lds_u, lane);
+        cholX<4>(Sd, Ud, lds_l, lds_u, lane);
         __builtin_amdgcn_wave_barrier();
         acc += Ud[lane];
     }
@@ -246,7 +276,7 @@ int main() {
         for (int b = 0; b < n; ++b) for (int i = 0; i < 8; ++i) s[i] += h[b * 8 + i];
         printf("%s: chol_inv16 %.0f cyc | fma %.1f | lds rt %.1f | rcp_f64 %.1f | rsqrt_f64 %.1f | readlane+add %.1f (cycles per op)\n",
                pass ? "1024 waves" : "1 wave", s[0] / n, s[1] / n / 100, s[2] / n / 100, s[3] / n / 100, s[4] / n / 100, s[5] / n / 100);
-        printf("   variant B (branch-light) %.0f cyc | variant D (bpermute) %.0f cyc\n", s[6] / n, s[7] / n);
+        printf("   variant B (branch-light) %.0f cyc | variant E (W image) %.0f cyc\n", s[6] / n, s[7] / n);
     }
     return 0;
 }
