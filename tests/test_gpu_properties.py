@@ -86,3 +86,39 @@ def test_statistical_parity_with_oracle(dcfm):
     eg, ec = np.mean(errs_gpu), np.mean(errs_cpu)
     spread = max(np.std(errs_gpu), np.std(errs_cpu), 0.01)
     assert abs(eg - ec) < 4 * spread + 0.03, (errs_gpu, errs_cpu)
+
+
+def test_statistical_parity_with_oracle_p960(dcfm):
+    """north_star check 2 at a larger shape (p = 960, n = 300, g = 8, K = 10): the GPU chain's
+    posterior-mean covariance has the oracle chain's Frobenius AND operator-norm error against
+    the synthetic truth, within Monte Carlo error.  Paired design: every replicate runs both
+    chains on the same data and initial state with independent draws (Philox vs NumPy), so
+    d_r = err_gpu,r - err_cpu,r has mean 0 under parity; the bar is 3 standard errors of the
+    mean difference (floored at 1 % of the error itself, the replicates being few)."""
+    n, p, g, K = 300, 960, 8, 10
+    burnin, mcmc, thin = 100, 300, 3
+    R = 4
+    diffs = {"fro_rel": [], "op_rel": []}
+    base = {"fro_rel": [], "op_rel": []}
+    for rep in range(R):
+        c = make_case(n, p, g, K, seed=70 + rep, k0=6)
+        truth = oracle.synth.truth_in_output_space(c["Sigma0"], c["Y"], c["keep"], c["init"].varind)
+        tnorm = float(np.max(np.abs(np.linalg.eigvalsh(truth))))
+        smp = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], burnin, mcmc, thin, seed=2000 + rep)
+        try:
+            smp.set_data(c["Yd"])
+            smp.set_state({k: v for k, v in state_dict(c["st"]).items() if k != "eta"})
+            smp.run(1, burnin + mcmc)
+            Sg = smp.get_sigma()
+        finally:
+            smp.close()
+        Sc = V.full(V.run_chain(c["Yd"], c["st"].copy(), c["rho"], c["hyper"], c["src"].iteration, 1,
+                                burnin + mcmc, burnin, mcmc, thin))
+        eg, ec = oracle.synth.cov_errors(Sg, truth), oracle.synth.cov_errors(Sc, truth)
+        for key, a, b in (("fro_rel", eg["fro_rel"], ec["fro_rel"]), ("op_rel", eg["op"] / tnorm, ec["op"] / tnorm)):
+            diffs[key].append(a - b)
+            base[key].append(b)
+    for key in diffs:
+        d = np.asarray(diffs[key])
+        se = max(float(np.std(d, ddof=1)) / np.sqrt(R), 0.01 * float(np.mean(base[key])))
+        assert abs(float(np.mean(d))) < 3 * se, (key, diffs[key], base[key])
