@@ -34,6 +34,15 @@ namespace dcfm {
 constexpr int KP = 32;         // padded factor width of the narrow (K <= 32) kernels
 constexpr int KP_MAX = 128;    // widest supported padding (K <= 128, config c4 has K = 100)
 constexpr int ASM_TILE = 128;  // covariance-assembly output tile
+// Wide paths (KW >= 64) keep E_m = eta_m' eta_m in the loading-row kernel's layout: the
+// upper 16x16 tiles (Kc <= I) of the KW/16 x KW/16 tile grid, tile t = etile(KW/16, Kc, I) in
+// the fp64 MFMA C/D layout, pair g2 = g / 2 of lane l = c + 16 q at (2t + g2) 128 + 2l + (g & 1)
+// for element (16 Kc + q + 4g, 16 I + c) -- one contiguous 16-byte read per lane and pair.
+__host__ __device__ constexpr int etile(int nbw, int Kc, int I) { return Kc * nbw - Kc * (Kc - 1) / 2 + (I - Kc); }
+__host__ __device__ constexpr int etile_index(int nbw, int R, int Cc) {
+    return (2 * etile(nbw, R >> 4, Cc >> 4) + ((R & 15) >> 3)) * 128 + 2 * ((Cc & 15) + 16 * (R & 3)) +
+           (((R & 15) >> 2) & 1);
+}
 constexpr int ASM_KC = 16;            // k_assemble's k chunk (kext, LDB are multiples)
 
 struct Dims {

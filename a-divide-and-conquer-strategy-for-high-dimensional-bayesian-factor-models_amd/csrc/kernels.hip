@@ -835,6 +835,15 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
             for (int tb = 0; tb < 2; ++tb) red[wave][2 * rho + ta][2 * r + tb] = acc[ta][tb][g];
     }
     __syncthreads();
+    if (KW > KP && isE) {   // wide: E_m in the loading-row kernel's tile layout (etile_index), upper tiles
+        double *Em = E + (size_t)m * KW * KW;
+        for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+            const int a = e >> 5, b = e & 31, R = 32 * te + a, Cc = 32 * kt + b;
+            if ((R >> 4) <= (Cc >> 4))
+                Em[etile_index(KW / 16, R, Cc)] = (red[0][a][b] + red[1][a][b]) + (red[2][a][b] + red[3][a][b]);
+        }
+        return;
+    }
     double *out = isE ? (E + (size_t)m * KW * KW + (size_t)(32 * te) * KW + 32 * kt)
                       : (C + ((size_t)m * d.PP + c0) * KW + 32 * kt);
     for (int e = threadIdx.x; e < 32 * 32; e += 256) {

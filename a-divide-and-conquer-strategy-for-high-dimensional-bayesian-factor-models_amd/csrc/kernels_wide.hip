@@ -383,15 +383,16 @@ __global__ __launch_bounds__(64) void k_lambda_w(
         pr[h] = (plam_src ? plam_src : psi)[rowoff + re];
     }
     const double yyj = yy[(size_t)m * d.PP + j], Gps = dr.Gps[drow];   // dc:169-170
-    d4 T[NT];
+    d4 T[NT];   // E_m's upper tiles, stored by k_cpass in this layout (etile_index): 16-byte reads
     static_for<NB>([&](auto KC) {
         constexpr int Kc = decltype(KC)::value;
         static_for<NB>([&](auto IC) {
             constexpr int I = decltype(IC)::value;
             if constexpr (I >= Kc) {
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    T[utix<NB>(Kc, I)][g] = Em[(size_t)(16 * Kc + q + 4 * g) * KW + 16 * I + c16];
+                constexpr int tw = etile(KW / 16, Kc, I);
+                const d2 e0 = *reinterpret_cast<const d2 *>(Em + (2 * tw) * 128 + 2 * lane);
+                const d2 e1 = *reinterpret_cast<const d2 *>(Em + (2 * tw + 1) * 128 + 2 * lane);
+                T[utix<NB>(Kc, I)] = d4{e0.x, e0.y, e1.x, e1.y};
             }
         });
     });
