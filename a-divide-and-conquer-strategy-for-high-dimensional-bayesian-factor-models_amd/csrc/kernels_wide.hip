@@ -432,22 +432,29 @@ __global__ __launch_bounds__(64) void k_lambda_w(
         __syncthreads();
         chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
         __syncthreads();
-        double v = 0.0;
-        if (lane < 16) {
+        double u[4], bq[4];
 #pragma unroll
-            for (int c = 0; c < 16; ++c) v = fma(Ud[lane * LD + c], vb[16 * J + c], v);   // U is lower
+        for (int s4 = 0; s4 < 4; ++s4) {
+            u[s4] = Ud[c16 * LD + 4 * s4 + q];                                 // A operand of U_JJ
+            bq[s4] = vb[16 * J + 4 * s4 + q];                                  // b_J, same in every column
         }
-        double u[4];
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) u[s4] = Ud[c16 * LD + 4 * s4 + q];     // A operand of U_JJ
 #pragma unroll
         for (int g = 0; g < 4; ++g) T[tJ][g] = Ud[(q + 4 * g) * LD + c16];      // U_JJ kept (back solve)
-        __syncthreads();
-        if (lane < 16) vb[16 * J + lane] = v;                                  // v_J (dc:143)
-        __syncthreads();
+        // v_J = U_JJ b_J (dc:143) as a product whose 16 columns all hold it: lane (c16, q) gets
+        // v[q + 4g] in element g, the layout the panel's forward-solve update reads (two chains)
+        d4 va = {0.0, 0.0, 0.0, 0.0}, vc = {0.0, 0.0, 0.0, 0.0};
+        va = mfma16x16x4(u[0], bq[0], va);
+        vc = mfma16x16x4(u[1], bq[1], vc);
+        va = mfma16x16x4(u[2], bq[2], va);
+        vc = mfma16x16x4(u[3], bq[3], vc);
         double vj[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) vj[g] = vb[16 * J + q + 4 * g];
+        for (int g = 0; g < 4; ++g) vj[g] = va[g] + vc[g];
+        __syncthreads();                                                       // b_J read by every lane
+        if (c16 == 0) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) vb[16 * J + q + 4 * g] = vj[g];        // v_J for the back solve
+        }
         static_for<NB>([&](auto IC) {                     // panel R_{J,I} = U_JJ T_{J,I}
             constexpr int I = decltype(IC)::value;
             if constexpr (I > J) {
