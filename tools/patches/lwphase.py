@@ -43,11 +43,9 @@ rep("""        chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
         __syncthreads();""", """        chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
         __syncthreads();
         PH_MARK(6);""")
-rep("""        double vj[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) vj[g] = vb[16 * J + q + 4 * g];""", """        double vj[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) vj[g] = vb[16 * J + q + 4 * g];
+rep("""            for (int g = 0; g < 4; ++g) vb[16 * J + q + 4 * g] = vj[g];        // v_J for the back solve
+        }""", """            for (int g = 0; g < 4; ++g) vb[16 * J + q + 4 * g] = vj[g];        // v_J for the back solve
+        }
         PH_MARK(1);""")
 rep("""        static_for<NB>([&](auto KC) {                     // trailing T_{Kc,I} -= R_{J,Kc}' R_{J,I}""", """        PH_MARK(2);
         static_for<NB>([&](auto KC) {                     // trailing T_{Kc,I} -= R_{J,Kc}' R_{J,I}""")
