@@ -408,7 +408,15 @@ __global__ __launch_bounds__(64) void k_lambda_w(
         vb[r] = tl ? psj * cr[h] : 0.0;                                  // blam (dc:141)
     }
     __syncthreads();
-    // ---- Q_j tiles: ps_j eta2 + diag(Plam_j) (dc:141), identity padding
+    // ---- Q_j tiles: ps_j eta2 + diag(Plam_j) (dc:141), identity padding.  Plam_j only meets
+    //      the diagonal tiles (a compile-time fact: an LDS read per element of every tile made
+    //      this a chain of 112 dependent LDS round trips)
+    double pl[NB][4];
+    static_for<NB>([&](auto JC) {
+        constexpr int J = decltype(JC)::value;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) pl[J][g] = ein[4][16 * J + q + 4 * g];
+    });
     static_for<NB>([&](auto KC) {
         constexpr int Kc = decltype(KC)::value;
         static_for<NB>([&](auto IC) {
@@ -417,8 +425,13 @@ __global__ __launch_bounds__(64) void k_lambda_w(
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const int r = 16 * Kc + q + 4 * g, c = 16 * I + c16;
-                    double val = (r == c) ? 1.0 : 0.0;
-                    if (r < K && c < K) val = psj * T[utix<NB>(Kc, I)][g] + (r == c ? ein[4][r] : 0.0);
+                    double val = psj * T[utix<NB>(Kc, I)][g];
+                    if constexpr (I == Kc) {
+                        if (r == c) val += pl[Kc][g];
+                        val = (r < K && c < K) ? val : (r == c ? 1.0 : 0.0);
+                    } else {
+                        val = (r < K && c < K) ? val : 0.0;
+                    }
                     T[utix<NB>(Kc, I)][g] = val;
                 }
             }
