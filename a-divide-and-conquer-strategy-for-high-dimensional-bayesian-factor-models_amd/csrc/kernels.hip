@@ -309,6 +309,15 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
         wv[t] = *reinterpret_cast<const d2 *>(Wi + 8 * t);
         xv[t] = *reinterpret_cast<const d2 *>(Xi + 8 * t);
     }
+    // the block's share of the shard's operators, in flight during the draws below (stored to
+    // LDS after them: a store per load made the compiler wait for each load in turn)
+    constexpr int NU = 4 * KP * KP / ZTHREADS;
+    double zv[NU];
+    {
+        const double *Zm = ZM + (size_t)m * 4 * KP * KP;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) zv[u] = Zm[threadIdx.x + ZTHREADS * u];
+    }
     if (d.inject) {   // eps[i][kk], kk = 8t + 2q + e   (dc:104 normrnd; injected draw buffer)
         const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K;
 #pragma unroll
@@ -337,12 +346,11 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
             for (int g = 0; g < 4; ++g) wr[mt][g] = Wr[16 * mt + q + 4 * g];
     }
     {
-        const double *Zm = ZM + (size_t)m * 4 * KP * KP;
 #pragma unroll
-        for (int u = 0; u < 4 * KP * KP / ZTHREADS; ++u) {
+        for (int u = 0; u < NU; ++u) {
             const int e = threadIdx.x + ZTHREADS * u;
             const int mat = e / (KP * KP), rem = e % (KP * KP);
-            Ms[mat][rem / KP][rem % KP] = Zm[e];
+            Ms[mat][rem / KP][rem % KP] = zv[u];
         }
     }
     __syncthreads();
@@ -351,16 +359,22 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
     for (int mt = 0; mt < 2; ++mt) zw[mt] = zx[mt] = ze[mt] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
+        double mo[2][3][2];   // this chunk's operator values, read before its 12 MFMAs
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int mat = 0; mat < 3; ++mat)
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) mo[e][mat][mt] = Ms[mat][16 * mt + c][8 * t + 2 * q + e];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const int kk = 8 * t + 2 * q + e;
             const double we = e ? wv[t].y : wv[t].x, xe = e ? xv[t].y : xv[t].x;
             const double ee = e ? ev[t].y : ev[t].x;
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
-                zw[mt] = mfma16x16x4(Ms[0][16 * mt + c][kk], we, zw[mt]);
-                zx[mt] = mfma16x16x4(Ms[1][16 * mt + c][kk], xe, zx[mt]);
-                ze[mt] = mfma16x16x4(Ms[2][16 * mt + c][kk], ee, ze[mt]);
+                zw[mt] = mfma16x16x4(mo[e][0][mt], we, zw[mt]);
+                zx[mt] = mfma16x16x4(mo[e][1][mt], xe, zx[mt]);
+                ze[mt] = mfma16x16x4(mo[e][2][mt], ee, ze[mt]);
             }
         }
     }
