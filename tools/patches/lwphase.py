@@ -78,4 +78,10 @@ extern "C" int dcfm_debug_phases(unsigned long long *out, int reset) {
     return 0;
 }
 """
+rep("""    const double yyj = yy[(size_t)m * d.PP + j], Gps = dr.Gps[drow];   // dc:169-170
+    d4 T[NT];""", """    const double yyj = yy[(size_t)m * d.PP + j], Gps = dr.Gps[drow];   // dc:169-170
+    { double sink = zr[0] + Gr[0] + trr[0] + cr[0] + pr[0] + yyj + Gps + psj;
+      asm volatile("" :: "v"(sink)); }
+    PH_MARK(5);
+    d4 T[NT];""")
 p.write_text(s)
