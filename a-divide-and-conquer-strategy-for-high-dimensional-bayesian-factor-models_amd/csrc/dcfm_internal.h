@@ -87,8 +87,10 @@ struct Bufs {
 constexpr int XSUM_BLOCKS = 8;
 // blocks of the A sum: G / chunk, chunk = a power of two dividing G, grown while more than
 // XSUM_BLOCKS chunks remain — so each chunk is a subtree of the canonical tree (TreeSum) and
-// the tree over the chunk sums is T(0, G)
+// the tree over the chunk sums is T(0, G).  G <= XSUM_BLOCKS: one block sums every shard
+// (tree8 with zero padding is T(0, G)), without the chunk-sum hand-off round
 __host__ __device__ inline int xsum_blocks(int G) {
+    if (G <= XSUM_BLOCKS) return 1;
     int chunk = 1;
     while (G / chunk > XSUM_BLOCKS && (G / chunk) % 2 == 0) chunk *= 2;
     return G / chunk;

@@ -77,7 +77,8 @@ __device__ __forceinline__ void prep_gram(const Dims &d, const double *__restric
     };
     const int nt = d.PP >> 3;
     int tt = wave;
-    for (; tt + 12 < nt; tt += 16) {       // 4 chunks' loads in flight (latency-bound otherwise)
+    for (; tt + 12 < nt; tt += 16) {       // 4 chunks' loads in flight (latency-bound otherwise;
+                                           // one round of 10 measured slower: c3 -1.5%)
         d2 wj[4];
         double l[4][4];
 #pragma unroll
@@ -184,28 +185,31 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 
 // ============================================================================
 // k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA, Y pass 1
-// one wave = (shard m, 32 rows i = 2 M-tiles) x 32 k (even / odd k N-tiles) of
+// one wave = (shard m, 16 MT rows i = MT M-tiles) x 32 k (even / odd k N-tiles) of
 // column tile kt (KW/32 tiles, adjacent in the 1-D grid so the wide layouts re-read Y from L2),
 // reduction over j in chunks of 8: lane (r, q) holds Y[i0+r][8t+2q .. +1] (16 B);
 // k-step 2t uses element 0, 2t+1 element 1; the B operand (w_j L[j][2r], w_j L[j][2r+1])
 // uses the same j <-> (q, e) map.  Register prefetch 3 chunks ahead (ring of 4).
+// MT = 1 (64-row blocks, twice the blocks) where the launch would not fill the chip (a few
+// shards per rank): each element's reduction order is the same for both, so the choice
+// changes no bit of W.
 // ============================================================================
-template <int KW>
+template <int KW, int MT = 2>
 __device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restrict__ Y,
                                            const double *__restrict__ Lam, const double *__restrict__ omega,
                                            double *__restrict__ W, int w, int kt) {
-    const int nrb = d.NP >> 7;                       // 128-row blocks per shard
+    const int nrb = d.NP / (64 * MT);                // row blocks per shard
     const int m = w / nrb, rb = w % nrb;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int i0 = rb * 128 + wave * 32;
+    const int i0 = rb * 64 * MT + wave * 16 * MT;
     const int r = lane & 15, q = lane >> 4;
     const double *Y0 = Y + ((size_t)m * d.NP + i0 + r) * d.PP + 2 * q;
-    const double *Y1 = Y0 + (size_t)16 * d.PP;
+    const double *Y1 = Y0 + (size_t)16 * (MT - 1) * d.PP;
     const double *L = Lam + (size_t)m * d.PP * KW + 32 * kt + 2 * r;
     const double *wp = omega + (size_t)m * d.PP + 2 * q;
-    d4 acc[2][2];
+    d4 acc[MT][2];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < MT; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
     const int nch = d.PP >> 3;
@@ -214,7 +218,7 @@ __device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restri
     {                                                                               \
         const int j = 8 * (t);                                                      \
         y0 = *reinterpret_cast<const d2 *>(Y0 + j);                                 \
-        y1 = *reinterpret_cast<const d2 *>(Y1 + j);                                 \
+        if (MT == 2) y1 = *reinterpret_cast<const d2 *>(Y1 + j);                    \
         ww = *reinterpret_cast<const d2 *>(wp + j);                                 \
         l0 = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q) * KW);           \
         l1 = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q + 1) * KW);       \
@@ -225,12 +229,16 @@ __device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restri
         const double b10 = ww.y * l1.x, b11 = ww.y * l1.y;                          \
         acc[0][0] = mfma16x16x4(y0.x, b00, acc[0][0]);                              \
         acc[0][1] = mfma16x16x4(y0.x, b01, acc[0][1]);                              \
-        acc[1][0] = mfma16x16x4(y1.x, b00, acc[1][0]);                              \
-        acc[1][1] = mfma16x16x4(y1.x, b01, acc[1][1]);                              \
+        if (MT == 2) {                                                              \
+            acc[MT - 1][0] = mfma16x16x4(y1.x, b00, acc[MT - 1][0]);                \
+            acc[MT - 1][1] = mfma16x16x4(y1.x, b01, acc[MT - 1][1]);                \
+        }                                                                           \
         acc[0][0] = mfma16x16x4(y0.y, b10, acc[0][0]);                              \
         acc[0][1] = mfma16x16x4(y0.y, b11, acc[0][1]);                              \
-        acc[1][0] = mfma16x16x4(y1.y, b10, acc[1][0]);                              \
-        acc[1][1] = mfma16x16x4(y1.y, b11, acc[1][1]);                              \
+        if (MT == 2) {                                                              \
+            acc[MT - 1][0] = mfma16x16x4(y1.y, b10, acc[MT - 1][0]);                \
+            acc[MT - 1][1] = mfma16x16x4(y1.y, b11, acc[MT - 1][1]);                \
+        }                                                                           \
     }
     // ring of 4 register buffers: chunk t + 3 is requested while chunk t multiplies, so three
     // chunks (6 KB per wave) are in flight behind the MFMAs (nch is a multiple of 4: PP % 32 == 0)
@@ -252,7 +260,7 @@ __device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restri
 #undef WP_MMA
     // D row = q + 4g (row i), col = r (k = 2r + tb)
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
+    for (int a = 0; a < MT; ++a) {
         double *Wt = W + ((size_t)m * d.NP + i0 + 16 * a) * KW + 32 * kt + 2 * r;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -753,8 +761,10 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
 // ============================================================================
 // k_cpass: [C_m | E_m] = [Y_m | eta_m]' eta_m    fp64 MFMA, Y pass 2      dc:133,138,141
 // block = (shard m, 32-column tile of [Y | eta]) x (32-column tile kt of eta, the
-// fastest index of the 1-D grid); its 4 waves split the reduction over rows i, partial 32x32 tiles
-// summed in LDS in a fixed order.
+// fastest index of the 1-D grid); its CP_WAVES waves split the reduction over rows i, partial
+// 32x32 tiles summed in LDS in a fixed order (the canonical tree).  The wave count fixes the
+// summation order, so it cannot follow the shard count per rank (N ranks reproduce one rank's
+// bits); 8 waves measured g = 8 share 18.2 -> 16.8 us but c3 45.5 -> 49.8 us: 4 it is.
 // Lane (r, q) loads 16 B: Y[i][c0+2r .. +1] and eta[i][2r .. +1] (formed on the
 // fly from X and Z), i = 4s + q, so the MFMA tiles are even/odd columns x
 // even/odd k.  Register double-buffered prefetch, 4 k-steps per batch (a ring of 3: same
@@ -809,12 +819,14 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
     }
 }
 
+template <int KW> constexpr int cp_waves() { return 4; }
 template <int KW>
-__global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict__ Y,
-                                               const double *__restrict__ X,
-                                               const double *__restrict__ Z,
-                                               double *__restrict__ C, double *__restrict__ E) {
-    __shared__ double red[4][32][33];
+__global__ __launch_bounds__(64 * cp_waves<KW>()) void k_cpass(Dims d, const double *__restrict__ Y,
+                                                              const double *__restrict__ X,
+                                                              const double *__restrict__ Z,
+                                                              double *__restrict__ C, double *__restrict__ E) {
+    constexpr int NWV = cp_waves<KW>();
+    __shared__ double red[NWV][32][33];
     // 1-D grid, the KW/32 eta column tiles of one [Y | eta] tile adjacent (same XCD,
     // so the Y tile is fetched once and re-read from L2)
     const int nt = (d.PP + KW) >> 5, nkt = KW / 32;
@@ -830,7 +842,7 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
     const double *Zp = Z + (size_t)m * d.NP * KW + 32 * kt + 2 * r;
     const double *Xa = X + 32 * te + 2 * r;
     const double *Za = Z + (size_t)m * d.NP * KW + 32 * te + 2 * r;
-    const int nsw = d.NP >> 4;                 // k-steps (4 rows each) per wave
+    const int nsw = d.NP / (4 * NWV);          // k-steps (4 rows each) per wave
     d4 acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -849,20 +861,26 @@ __global__ __launch_bounds__(256) void k_cpass(Dims d, const double *__restrict_
             for (int tb = 0; tb < 2; ++tb) red[wave][2 * rho + ta][2 * r + tb] = acc[ta][tb][g];
     }
     __syncthreads();
+    auto tsum = [&](int a, int b) {
+        if constexpr (NWV == 8)
+            return ((red[0][a][b] + red[1][a][b]) + (red[2][a][b] + red[3][a][b])) +
+                   ((red[4][a][b] + red[5][a][b]) + (red[6][a][b] + red[7][a][b]));
+        else
+            return (red[0][a][b] + red[1][a][b]) + (red[2][a][b] + red[3][a][b]);
+    };
     if (KW > KP && isE) {   // wide: E_m in the loading-row kernel's tile layout (etile_index), upper tiles
         double *Em = E + (size_t)m * KW * KW;
-        for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+        for (int e = threadIdx.x; e < 32 * 32; e += 64 * NWV) {
             const int a = e >> 5, b = e & 31, R = 32 * te + a, Cc = 32 * kt + b;
-            if ((R >> 4) <= (Cc >> 4))
-                Em[etile_index(KW / 16, R, Cc)] = (red[0][a][b] + red[1][a][b]) + (red[2][a][b] + red[3][a][b]);
+            if ((R >> 4) <= (Cc >> 4)) Em[etile_index(KW / 16, R, Cc)] = tsum(a, b);
         }
         return;
     }
     double *out = isE ? (E + (size_t)m * KW * KW + (size_t)(32 * te) * KW + 32 * kt)
                       : (C + ((size_t)m * d.PP + c0) * KW + 32 * kt);
-    for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+    for (int e = threadIdx.x; e < 32 * 32; e += 64 * NWV) {
         const int a = e >> 5, b = e & 31;
-        out[(size_t)a * KW + b] = (red[0][a][b] + red[1][a][b]) + (red[2][a][b] + red[3][a][b]);
+        out[(size_t)a * KW + b] = tsum(a, b);
     }
 }
 
@@ -1457,7 +1475,7 @@ __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsu
                     for (int U = 0; U < 8; ++U)
                         v[u][U] = (U < chunk) ? ld_agent(b.A + (size_t)(m0 + U) * KP * KP + t + 256 * u) : 0.0;
 #pragma unroll
-                for (int u = 0; u < NU; ++u) vs[u] = tree8(v[u]);   // chunk is a power of two
+                for (int u = 0; u < NU; ++u) vs[u] = tree8(v[u]);   // chunk a power of two, or G <= 8
             } else {                                               // groups of 8 (subtrees), then their tree
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
@@ -1471,12 +1489,26 @@ __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsu
                     vs[u] = ts.total();
                 }
             }
+            if (nxs > 1) {   // several chunks: publish, the last arrival goes on
 #pragma unroll
-            for (int u = 0; u < NU; ++u) st_agent(b.xpart + (size_t)j * KP * KP + t + 256 * u, vs[u]);
-            if (!last_arrival(b.ticket, (unsigned)nxs, smem)) return;
+                for (int u = 0; u < NU; ++u) st_agent(b.xpart + (size_t)j * KP * KP + t + 256 * u, vs[u]);
+                if (!last_arrival(b.ticket, (unsigned)nxs, smem)) return;
+            }
             double xs[NU];
-            {   // canonical tree over the nxs <= 8 chunk sums (for a non-power-of-two G the chunks
-                // are single shards and nxs = G may exceed 8: groups of 8 into a TreeSum)
+            if (nxs <= 8) {   // canonical tree over the chunk sums: every load in flight at once
+                              // (a round trip per u cost ~1.3 us each); tree8 with zeros past nxs
+                              // is TreeSum's order for any nxs <= 8
+                double v[NU][8];
+#pragma unroll
+                for (int u = 0; u < NU; ++u)
+#pragma unroll
+                    for (int U = 0; U < 8; ++U)
+                        v[u][U] = (U < nxs) ? (U == j ? vs[u] : ld_agent(b.xpart + (size_t)U * KP * KP + t + 256 * u))
+                                            : 0.0;
+#pragma unroll
+                for (int u = 0; u < NU; ++u) xs[u] = tree8(v[u]);
+            } else {   // a non-power-of-two G: the chunks are single shards and nxs = G exceeds
+                       // 8: groups of 8 into a TreeSum
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
                     TreeSum<double, 8> ts;
@@ -1505,9 +1537,10 @@ __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsu
         }
         blk -= nxs;
     }
-    if (wpass) {
+    if (wpass) {   // 1: 128-row blocks, 2: 64-row blocks (wcol_wpass_mode)
         const int nw = gridDim.x - (int)(blockIdx.x - blk);
-        wpass_tile<KP>(d, b.Y, b.Lam, b.omega, b.W, xcd_remap(blk, nw), 0);
+        if (wpass == 2) wpass_tile<KP, 1>(d, b.Y, b.Lam, b.omega, b.W, xcd_remap(blk, nw), 0);
+        else wpass_tile<KP, 2>(d, b.Y, b.Lam, b.omega, b.W, xcd_remap(blk, nw), 0);
     }
 }
 
@@ -1786,9 +1819,11 @@ void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
 // k_wcol launch (K <= 32)
 void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_epoch,
                  hipStream_t s) {
-    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / 128) * d.G : 0);
+    // W pass tiles: 64-row blocks while 128-row blocks would leave CUs idle
+    const int wmode = (d.NP / 128) * d.G < 256 ? 2 : 1;
+    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / (64 * (3 - wmode))) * d.G : 0);
     if (nb == 0) return;
-    hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, ops ? 1 : 0, colsum ? 1 : 0, wpass ? 1 : 0,
+    hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, ops ? 1 : 0, colsum ? 1 : 0, wpass ? wmode : 0,
                        ops_epoch, d.nranks == 1 ? 1 : 0);
 }
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
@@ -1837,7 +1872,7 @@ void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(((d.PP + d.kp) / 32) * d.G * (d.kp / 32));
     switch (d.kp) {
-    case 32: hipLaunchKernelGGL(k_cpass<32>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
+    case 32: hipLaunchKernelGGL(k_cpass<32>, grid, dim3(64 * cp_waves<32>()), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
     case 64: hipLaunchKernelGGL(k_cpass<64>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
     default: hipLaunchKernelGGL(k_cpass<128>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
     }
