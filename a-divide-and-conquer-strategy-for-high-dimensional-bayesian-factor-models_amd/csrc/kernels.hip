@@ -295,17 +295,20 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
 // ============================================================================
 constexpr int ZDRAW_SMEM = 4 * KP * (KP + 1);
 constexpr int ZROWS = 128, ZTHREADS = 512;     // rows and threads per k_zdraw block
+// ZT threads = ZT / 4 rows per block: 256 (64-row blocks) where 128-row ones would leave CUs
+// idle (a few shards per rank); rows are independent, so the choice changes no bit
+template <int ZT = ZTHREADS>
 __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restrict__ W,
                                            const double *__restrict__ ZM, const double *__restrict__ X,
                                            double *__restrict__ Z, double *__restrict__ Sp, const DrawsDev &dr,
                                            int64_t iter, int w, double *smem) {
     double (*Ms)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);   // M1, M2, U, NA
-    const int nrb = d.NP / ZROWS;
+    const int nrb = d.NP / (ZT / 4);
     const int m = w / nrb, rb = w % nrb;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = lane & 15, q = lane >> 4;
     const int mg = d.shard0 + m;
-    const int i0 = rb * ZROWS + wave * 16;
+    const int i0 = rb * (ZT / 4) + wave * 16;
     const int i = i0 + c;
     const bool live = i < d.n;
     // this wave's operands first (in flight while the block stages the operators)
@@ -319,12 +322,12 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
     }
     // the block's share of the shard's operators, in flight during the draws below (stored to
     // LDS after them: a store per load made the compiler wait for each load in turn)
-    constexpr int NU = 4 * KP * KP / ZTHREADS;
+    constexpr int NU = 4 * KP * KP / ZT;
     double zv[NU];
     {
         const double *Zm = ZM + (size_t)m * 4 * KP * KP;
 #pragma unroll
-        for (int u = 0; u < NU; ++u) zv[u] = Zm[threadIdx.x + ZTHREADS * u];
+        for (int u = 0; u < NU; ++u) zv[u] = Zm[threadIdx.x + ZT * u];
     }
     if (d.inject) {   // eps[i][kk], kk = 8t + 2q + e   (dc:104 normrnd; injected draw buffer)
         const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K;
@@ -356,7 +359,7 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
     {
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
-            const int e = threadIdx.x + ZTHREADS * u;
+            const int e = threadIdx.x + ZT * u;
             const int mat = e / (KP * KP), rem = e % (KP * KP);
             Ms[mat][rem / KP][rem % KP] = zv[u];
         }
@@ -414,13 +417,14 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
         }
 }
 
-__global__ __launch_bounds__(ZTHREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_zdraw(Dims d, const double *__restrict__ W,
+template <int ZT>
+__global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(4))) void k_zdraw(Dims d, const double *__restrict__ W,
                                                const double *__restrict__ ZM,
                                                const double *__restrict__ X,
                                                double *__restrict__ Z, double *__restrict__ Sp,
                                                DrawsDev dr, int64_t iter) {
     __shared__ double smem[ZDRAW_SMEM];
-    zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blockIdx.x, gridDim.x), smem);
+    zdraw_tile<ZT>(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blockIdx.x, gridDim.x), smem);
 }
 
 // ============================================================================
@@ -1813,8 +1817,11 @@ void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s) {
 }
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     if (d.kp != KP) return wide::launch_zdraw(d, b, dr, iter, s);
-    hipLaunchKernelGGL(k_zdraw, dim3((d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp,
-                       dr, iter);
+    if ((d.NP / ZROWS) * d.G < 256)   // 64-row blocks (zdraw_tile)
+        hipLaunchKernelGGL(k_zdraw<256>, dim3((d.NP / 64) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z, b.Sp, dr, iter);
+    else
+        hipLaunchKernelGGL(k_zdraw<ZTHREADS>, dim3((d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM, b.X, b.Z,
+                           b.Sp, dr, iter);
 }
 // k_wcol launch (K <= 32)
 void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_epoch,
