@@ -776,13 +776,14 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
 // ============================================================================
 // IS_E: the A operand is eta itself, columns te*32.. (Yp = nullptr; Xa/Za point at
 // them); SAME_T: te == kt, so the A operand is the B operand (no extra loads).
-template <int KW, bool IS_E, bool SAME_T>
+// PS: the block computes only the k columns of parity par (acc[.][0]); same per-element order
+template <int KW, bool IS_E, bool SAME_T, bool PS = false>
 __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restrict__ Yp,
                                            const double *__restrict__ Xp,
                                            const double *__restrict__ Zp,
                                            const double *__restrict__ Xa,
                                            const double *__restrict__ Za, int s0, int nsw,
-                                           int q, d4 (&acc)[2][2]) {
+                                           int q, d4 (&acc)[2][2], int par = 0) {
     constexpr bool EXTRA = IS_E && !SAME_T;
     d2 yA[4], xA[4], zA[4], yB[4], xB[4], zB[4];
     auto load = [&](int s, d2 (&y)[4], d2 (&x)[4], d2 (&z)[4]) {
@@ -807,10 +808,16 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
             const double e0 = eta_of(d.sr, d.s1r, x[u].x, z[u].x);
             const double e1 = eta_of(d.sr, d.s1r, x[u].y, z[u].y);
             const double a0 = (IS_E && SAME_T) ? e0 : y[u].x, a1 = (IS_E && SAME_T) ? e1 : y[u].y;
-            acc[0][0] = mfma16x16x4(a0, e0, acc[0][0]);
-            acc[0][1] = mfma16x16x4(a0, e1, acc[0][1]);
-            acc[1][0] = mfma16x16x4(a1, e0, acc[1][0]);
-            acc[1][1] = mfma16x16x4(a1, e1, acc[1][1]);
+            if constexpr (PS) {
+                const double ep = par ? e1 : e0;
+                acc[0][0] = mfma16x16x4(a0, ep, acc[0][0]);
+                acc[1][0] = mfma16x16x4(a1, ep, acc[1][0]);
+            } else {
+                acc[0][0] = mfma16x16x4(a0, e0, acc[0][0]);
+                acc[0][1] = mfma16x16x4(a0, e1, acc[0][1]);
+                acc[1][0] = mfma16x16x4(a1, e0, acc[1][0]);
+                acc[1][1] = mfma16x16x4(a1, e1, acc[1][1]);
+            }
         }
     };
     const int nb = nsw >> 2;
@@ -824,7 +831,9 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
 }
 
 template <int KW> constexpr int cp_waves() { return 4; }
-template <int KW>
+// PS (K <= 32, where the launch would leave CUs idle): each block computes one parity of its
+// 32 k columns (twice the blocks, the pair adjacent: Y from L2); per-element order unchanged
+template <int KW, bool PS = false>
 __global__ __launch_bounds__(64 * cp_waves<KW>()) void k_cpass(Dims d, const double *__restrict__ Y,
                                                               const double *__restrict__ X,
                                                               const double *__restrict__ Z,
@@ -834,7 +843,9 @@ __global__ __launch_bounds__(64 * cp_waves<KW>()) void k_cpass(Dims d, const dou
     // 1-D grid, the KW/32 eta column tiles of one [Y | eta] tile adjacent (same XCD,
     // so the Y tile is fetched once and re-read from L2)
     const int nt = (d.PP + KW) >> 5, nkt = KW / 32;
-    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int par = PS ? (w & 1) : 0;
+    if (PS) w >>= 1;
     const int kt = w % nkt, m = (w / nkt) / nt, tile = (w / nkt) % nt;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c0 = tile * 32;
@@ -852,17 +863,22 @@ __global__ __launch_bounds__(64 * cp_waves<KW>()) void k_cpass(Dims d, const dou
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-    if (!isE) cpass_wave<KW, false, false>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc);
-    else if (te == kt) cpass_wave<KW, true, true>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc);
-    else cpass_wave<KW, true, false>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc);
+    if (!isE) cpass_wave<KW, false, false, PS>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc, par);
+    else if (te == kt) cpass_wave<KW, true, true, PS>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc, par);
+    else cpass_wave<KW, true, false, PS>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc, par);
     // D row rho = q + 4g -> column c0 + 2 rho + ta;  D col r -> k = 2r + tb
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
         const int rho = q + 4 * g;
 #pragma unroll
-        for (int ta = 0; ta < 2; ++ta)
+        for (int ta = 0; ta < 2; ++ta) {
+            if (PS) {
+                red[wave][2 * rho + ta][2 * r + par] = acc[ta][0][g];
+            } else {
 #pragma unroll
-            for (int tb = 0; tb < 2; ++tb) red[wave][2 * rho + ta][2 * r + tb] = acc[ta][tb][g];
+                for (int tb = 0; tb < 2; ++tb) red[wave][2 * rho + ta][2 * r + tb] = acc[ta][tb][g];
+            }
+        }
     }
     __syncthreads();
     auto tsum = [&](int a, int b) {
@@ -882,6 +898,13 @@ __global__ __launch_bounds__(64 * cp_waves<KW>()) void k_cpass(Dims d, const dou
     }
     double *out = isE ? (E + (size_t)m * KW * KW + (size_t)(32 * te) * KW + 32 * kt)
                       : (C + ((size_t)m * d.PP + c0) * KW + 32 * kt);
+    if (PS) {   // this block's parity of the columns
+        for (int e = threadIdx.x; e < 32 * 16; e += 64 * NWV) {
+            const int a = e >> 4, b = 2 * (e & 15) + par;
+            out[(size_t)a * KW + b] = tsum(a, b);
+        }
+        return;
+    }
     for (int e = threadIdx.x; e < 32 * 32; e += 64 * NWV) {
         const int a = e >> 5, b = e & 31;
         out[(size_t)a * KW + b] = tsum(a, b);
@@ -1879,7 +1902,13 @@ void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(((d.PP + d.kp) / 32) * d.G * (d.kp / 32));
     switch (d.kp) {
-    case 32: hipLaunchKernelGGL(k_cpass<32>, grid, dim3(64 * cp_waves<32>()), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
+    case 32:
+        if (grid.x < 512)   // a few shards per rank: split the k columns by parity (k_cpass PS)
+            hipLaunchKernelGGL((k_cpass<32, true>), dim3(2 * grid.x), dim3(64 * cp_waves<32>()), 0, s, d, b.Y, b.X, b.Z,
+                               b.C, b.E);
+        else
+            hipLaunchKernelGGL((k_cpass<32, false>), grid, dim3(64 * cp_waves<32>()), 0, s, d, b.Y, b.X, b.Z, b.C, b.E);
+        break;
     case 64: hipLaunchKernelGGL(k_cpass<64>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
     default: hipLaunchKernelGGL(k_cpass<128>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
     }
