@@ -417,8 +417,10 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
         }
 }
 
+// ZT = 256 holds twice the operator staging registers per thread: 2 waves per SIMD (it runs
+// only where the launch leaves SIMDs idle anyway) instead of a 128-VGPR cap that spilled
 template <int ZT>
-__global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(4))) void k_zdraw(Dims d, const double *__restrict__ W,
+__global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(ZT == ZTHREADS ? 4 : 2))) void k_zdraw(Dims d, const double *__restrict__ W,
                                                const double *__restrict__ ZM,
                                                const double *__restrict__ X,
                                                double *__restrict__ Z, double *__restrict__ Sp,
@@ -1416,8 +1418,10 @@ __device__ __forceinline__ bool last_arrival(unsigned *ticket, unsigned count, d
 constexpr int ZX_SMEM = ZDRAW_SMEM > XCHOL_SMEM ? ZDRAW_SMEM : XCHOL_SMEM;
 // block 0: the X operators from the ranks' shard sums of A (several ranks, fused chain);
 // blocks [1, 1 + ndel): the previous iteration's delta / tau chain from the gathered column
-// sums (8 shards per block, one wave each), beside the Z pass; the rest: k_zdraw tiles
-__global__ __launch_bounds__(ZTHREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_zxchol(
+// sums (ZT / 64 shards per block, one wave each), beside the Z pass; the rest: k_zdraw tiles
+// (ZT as k_zdraw: 256 where 128-row tiles would leave CUs idle)
+template <int ZT>
+__global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(ZT == ZTHREADS ? 4 : 2))) void k_zxchol(
         Dims d, const double *__restrict__ W, const double *__restrict__ ZM, const double *__restrict__ X,
         double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr, int64_t iter,
         const double *__restrict__ xa_all, double *__restrict__ XM, int ndel, const double *__restrict__ sall,
@@ -1425,16 +1429,16 @@ __global__ __launch_bounds__(ZTHREADS) __attribute__((amdgpu_waves_per_eu(4))) v
     __shared__ double smem[ZX_SMEM];
     const int blk = blockIdx.x;
     if (blk > ndel) {
-        zdraw_tile(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blk - 1 - ndel, gridDim.x - 1 - ndel), smem);
+        zdraw_tile<ZT>(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blk - 1 - ndel, gridDim.x - 1 - ndel), smem);
         return;
     }
     if (blk > 0) {
-        const int m = (blk - 1) * (ZTHREADS / 64) + (threadIdx.x >> 6);
+        const int m = (blk - 1) * (ZT / 64) + (threadIdx.x >> 6);
         if (m < d.g)
             delta_shard(d, sall, da.delta_in, da.tau_in, da.delta_out, da.tau_out, dr, da.iter, m, threadIdx.x & 63);
         return;
     }
-    for (int e = threadIdx.x; e < KP * KP; e += ZTHREADS) {   // the ranks' shard sums, canonical tree
+    for (int e = threadIdx.x; e < KP * KP; e += ZT) {   // the ranks' shard sums, canonical tree
         xprec_store(d, smem, e, tree_sum(xa_all + e, d.nranks, (size_t)d.xstride));
     }
     __syncthreads();
@@ -1860,13 +1864,20 @@ void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t ite
                    const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
                    int64_t delta_iter) {
     if (d.kp != KP) return;
-    // delta blocks padded so that the zdraw tiles' first block sits on XCD 0 (xcd_remap)
-    const int ndel = delta_in ? ((d.g + 7) / 8 + 1 + 7) / 8 * 8 - 1 : 0;
+    // delta blocks (zw shards each) padded so that the zdraw tiles' first block sits on XCD 0 (xcd_remap)
+    const bool small = (d.NP / ZROWS) * d.G < 256;   // 64-row tiles (k_zdraw)
+    const int zw = small ? 4 : ZTHREADS / 64;
+    const int ndel = delta_in ? ((d.g + zw - 1) / zw + 1 + 7) / 8 * 8 - 1 : 0;
     DeltaArgs da;
     da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
     da.iter = delta_iter;
-    hipLaunchKernelGGL(k_zxchol, dim3(1 + ndel + (d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM, b.X, b.Z,
-                       b.Sp, dr, iter, d.nranks > 1 ? b.xa_all : b.xa, b.XM, ndel, b.sall, da);
+    const double *xs = d.nranks > 1 ? b.xa_all : b.xa;
+    if (small)
+        hipLaunchKernelGGL(k_zxchol<256>, dim3(1 + ndel + (d.NP / 64) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z,
+                           b.Sp, dr, iter, xs, b.XM, ndel, b.sall, da);
+    else
+        hipLaunchKernelGGL(k_zxchol<ZTHREADS>, dim3(1 + ndel + (d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM,
+                           b.X, b.Z, b.Sp, dr, iter, xs, b.XM, ndel, b.sall, da);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
     const int total = d.NP * d.kp;
