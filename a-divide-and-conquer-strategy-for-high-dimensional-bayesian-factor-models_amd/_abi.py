@@ -21,6 +21,9 @@ DCFM_ERR_RCCL = 4
 DCFM_ERR_NUMERIC = 5
 DCFM_ERR_ALLOC = 6
 DCFM_FLAG_INJECT_DRAWS = 0x1
+DCFM_FLAG_UNFUSED = 0x2        # K <= 32 through the side-stream layout (same results)
+DCFM_FLAG_ONE_STREAM = 0x4     # every launch on one stream
+DCFM_FLAG_FLAT_PRIORITY = 0x8  # default priority for every stream
 
 KERNEL_IDS = {
     "k_prep": 0, "k_wpass": 1, "k_zdraw": 2, "k_xred": 3, "k_xdraw": 4, "k_cpass": 5,

@@ -72,6 +72,7 @@ struct dcfm_handle {
     hipEvent_t lp_ready = nullptr, lp_done = nullptr;
     hipEvent_t e_lam = nullptr, e_prep = nullptr, e_xchol = nullptr, e_batch = nullptr,
                e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
+    bool fused = false;           // K <= 32 fused launch chain (else the side-stream layout), fixed at create
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
     unsigned long long wc_ops = 0;   // k_wcol launches with the operator roles (hand-off counter epoch)
     bool asm_pending[2] = {false, false};
@@ -408,16 +409,12 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     HIPC(h, hipSetDevice(c.device));
     // Stream priorities: the sweep chain (main, side) at the greatest priority, the draws
     // a batch ahead and the covariance assembly at the least, so the dispatcher hands
-    // freed CUs to the latency-critical chain first (DCFM_STREAM_PRIO=0: all default).
+    // freed CUs to the latency-critical chain first (DCFM_FLAG_FLAT_PRIORITY: all default).
     int prio_lo = 0, prio_hi = 0;
-    {
-        const char *pe = std::getenv("DCFM_STREAM_PRIO");
-        if (!(pe && pe[0] == '0')) HIPC(h, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    }
+    if (!(c.flags & DCFM_FLAG_FLAT_PRIORITY)) HIPC(h, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     HIPC(h, hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi));
-    {   // DCFM_SERIALIZE=1: one stream for everything (isolated per-kernel timings)
-        const char *ser = std::getenv("DCFM_SERIALIZE");
-        if (ser && ser[0] == '1') {
+    {   // DCFM_FLAG_ONE_STREAM: one stream for everything (isolated per-kernel timings)
+        if (c.flags & DCFM_FLAG_ONE_STREAM) {
             h->side = h->sasm = h->sdraw = h->stream;
         } else {
             HIPC(h, hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_hi));
@@ -459,9 +456,10 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     d.as_ = c.as_; d.bs = c.bs; d.df = c.df; d.ad1 = c.ad1; d.bd1 = c.bd1; d.ad2 = c.ad2; d.bd2 = c.bd2;
     d.seed = c.seed;
     d.inject = (c.flags & DCFM_FLAG_INJECT_DRAWS) ? 1 : 0;
+    // K <= 32 runs the fused launch chain unless DCFM_FLAG_UNFUSED asks for the side-stream layout
+    h->fused = d.kp == KP && !(c.flags & DCFM_FLAG_UNFUSED);
     // fused narrow chain on several ranks: column sums and the A sum travel in one message
-    const bool packed = nranks > 1 && d.kp == KP &&
-                        !([] { const char *e = std::getenv("DCFM_NOFUSE"); return e && e[0] == '1'; }());
+    const bool packed = nranks > 1 && h->fused;
     d.sgap = packed ? KP * KP : 0;
     d.xstride = packed ? d.G * KP + KP * KP : d.kp * d.kp;
     h->B = c.asm_batch > 0 ? c.asm_batch : 32;
@@ -528,7 +526,9 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         b.T1 = h->Tb[c.rank + 1];
     }
     ALLOC(b.Sigma, (size_t)(tri(b.T1) - tri(b.T0)) * ASM_TILE * ASM_TILE);
-    if (!d.inject) {
+    // the generated fused chain: k_xdraw draws the loading-row variates into b.ldraw each iteration
+    if (h->fused && !d.inject) ALLOC(b.ldraw, (size_t)lam_gen_doubles(d));
+    if (!d.inject && !h->fused) {   // k_draws batches of the side-stream layouts
         const size_t K = c.K, n = c.n, P = c.P;
         const size_t nz = K * n * g, nx = K * n, nl = K * P * g, gpsi = P * K * g, gdel = K * g, gps = P * g;
         const size_t per_it = nz + nx + nl + gpsi + gdel + gps;
@@ -1033,8 +1033,8 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     // K <= 32: the per-shard operators ride in the fused launches on the main stream
     // (k_wcol, k_zxchol / k_xdraw); K > 32 (or DCFM_NOFUSE=1): prep and the X
     // operators run on the side stream
-    static const bool nofuse = [] { const char *e = std::getenv("DCFM_NOFUSE"); return e && e[0] == '1'; }();
-    const bool fused = d.kp == KP && !nofuse;
+    const bool fused = h->fused;
+    const bool lamgen = fused && !d.inject;   // k_xdraw draws k_lambda's variates (b.ldraw)
     // fused (K <= 32): per iteration t, k_wcol = [Z operators and shard sum of A of t, column
     // sums of t-1] beside the W pass of t.  One rank: the last chunk also factors Xprec, then
     // k_zdraw and k_xdraw = [delta chain of t-1] beside the X draw.  Several ranks: the
@@ -1088,8 +1088,9 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         return sl;
     };
     // Generated draws (Philox, counter-addressed): the fused K <= 32 chain (any rank count) draws
-    // every variate in place (Z / X normals, k_lambda's normals and gammas, the delta gammas);
-    // the other paths read k_draws buffers generated a batch ahead on the draw stream
+    // its variates where they are consumed (Z / X normals, the delta gammas) or in the launch
+    // before (k_lambda's normals and gammas: extra blocks of k_xdraw, whose row blocks leave most
+    // CUs idle); the other paths read k_draws buffers generated a batch ahead on the draw stream
     const bool gen_draws = !d.inject && !fused;
     int slot = -1;
     int64_t batch0 = first_iter, batch_n = 0;
@@ -1164,20 +1165,20 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             KTimer t(h, DCFM_K_XDRAW, s);
             if (delta_pending)
                 launch_xdraw_wc(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
-                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, s);
+                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, s, lamgen);
             else
-                launch_xdraw_wc(d, b, dr, it, nullptr, nullptr, nullptr, nullptr, 0, s);
+                launch_xdraw_wc(d, b, dr, it, nullptr, nullptr, nullptr, nullptr, 0, s, lamgen);
             HIPC(h, hipGetLastError());
             if (delta_pending) after_delta();
             delta_pending = false;
         } else {
             KTimer t(h, DCFM_K_XDRAW, s);
-            launch_xdraw(d, b, dr, it, s, fused && d.nranks == 1);
+            launch_xdraw(d, b, dr, it, s, fused && d.nranks == 1, lamgen);
         }
         { KTimer t(h, DCFM_K_CPASS, s);  launch_cpass(d, b, s); }
         {
             KTimer t(h, DCFM_K_LAMBDA, s);
-            launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, fused && !d.inject);
+            launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, lamgen);
         }
         h->plam_valid = false;
         if (fused) {

@@ -69,8 +69,30 @@ struct DrawsDev {
     int64_t first_iter, n_iter;
 };
 
+// loading-row variates of one iteration in k_lambda's layout (local shard m, loading row j):
+// NL [G][P][K] (dc:142 zlam), Gpsi [G][P][K] (dc:150), Gps [G][P] (dc:170)
+struct LamDraws { const double *NL, *Gpsi, *Gps; };
+// k_xdraw's extra blocks that generate them for the generated fused chain (K <= 32): block
+// segments [0, b_ps) ps gammas, [b_ps, b_psi) psi gammas, [b_psi, b_total) normal pairs,
+// one variate (pair) per thread of LAM_GEN_THREADS
+constexpr int LAM_GEN_THREADS = 1024;
+struct LamGen { double *NL, *Gpsi, *Gps; int b_ps, b_psi, b_total; };
+inline int lam_gen_doubles(const Dims &d) { return 2 * d.G * d.P * d.K + d.G * d.P; }
+inline LamGen lam_gen_plan(const Dims &d, double *base) {
+    const int T = LAM_GEN_THREADS, GP = d.G * d.P;
+    LamGen g;
+    g.NL = base;
+    g.Gpsi = base + (size_t)GP * d.K;
+    g.Gps = base + 2 * (size_t)GP * d.K;
+    g.b_ps = (GP + T - 1) / T;
+    g.b_psi = g.b_ps + (GP * d.K + T - 1) / T;
+    g.b_total = g.b_psi + (GP * ((d.K + 1) / 2) + T - 1) / T;
+    return g;
+}
+
 struct Bufs {
     double *Y, *yy, *Lam, *omega, *ps, *psi, *Plam, *X, *Z, *delta, *tau;
+    double *ldraw;                     // LamDraws of the generated fused chain (lam_gen_plan), else null
     double *W, *A, *ZM, *Sp, *xin, *xall, *C, *E, *cpart, *sloc, *sall;
     double *Lb[2], *wsum[2], *Sigma;
     double *xa, *xa_all, *XM;          // per-rank sum of A, gathered sums, X-draw operators
@@ -131,15 +153,18 @@ void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass
 void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
                    const double *delta_in = nullptr, const double *tau_in = nullptr, double *delta_out = nullptr,
                    double *tau_out = nullptr, int64_t delta_iter = 0);
-// one rank, K <= 32: k_xdraw plus, when delta_in != null, the delta chain of delta_iter
+// one rank, K <= 32: k_xdraw plus, when delta_in != null, the delta chain of delta_iter, and
+// (lamgen) the iteration's loading-row variates into b.ldraw
 void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
-                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s);
+                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s,
+                     bool lamgen);
 void launch_asum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
-                  bool from_shards = false);
+                  bool from_shards = false, bool lamgen = false);
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s);
-// gen: K <= 32 draws its variates in place (one rank's fused chain) instead of reading dr
+// gen: K <= 32 reads the variates k_xdraw generated into b.ldraw (the generated fused chain)
+// instead of the draw buffers dr (injected draws, k_draws batches)
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, const double *plam_src, hipStream_t s, bool gen = false);
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s);

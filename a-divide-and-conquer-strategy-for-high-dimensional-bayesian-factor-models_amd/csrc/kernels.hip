@@ -616,6 +616,40 @@ __device__ __forceinline__ void draws_block(const Dims &d, const DrawsDev &dr, i
                         const_cast<double *>(dr.NL) + ((size_t)mg * d.P + j) * K);
     }
 }
+// The loading-row variates of one iteration (dc:142 zlam, dc:150 psi gammas, dc:170 ps
+// gamma) into k_lambda's buffer layout, at the counters every other path draws them from
+// (k_draws, dcfm_rng_fill): one thread per ps gamma, per psi gamma and per normal pair, the
+// rejection-sampled ps gammas first.  Runs as extra blocks of k_xdraw (latency-bound, most
+// CUs idle) so the loading-row kernel reads its variates instead of drawing them.
+__device__ __forceinline__ void lam_draws_block(const Dims &d, const LamGen &lg, int64_t iter, int blk) {
+    const Rng rng(d.seed);
+    const uint32_t it = (uint32_t)iter;
+    const int t = threadIdx.x;
+    if (blk < lg.b_ps) {
+        const int x = blk * LAM_GEN_THREADS + t;            // (m, j)
+        if (x >= d.G * d.P) return;
+        const int m = x / d.P, j = x - m * d.P;
+        lg.Gps[x] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, (uint32_t)(d.shard0 + m), (uint32_t)j, 0u, it);
+        return;
+    }
+    if (blk < lg.b_psi) {
+        const int x = (blk - lg.b_ps) * LAM_GEN_THREADS + t;   // (m, j, k)
+        if (x >= d.G * d.P * d.K) return;
+        const int mj = x / d.K, k = x - mj * d.K, m = mj / d.P, j = mj - m * d.P;
+        lg.Gpsi[x] = rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)k, it);
+        return;
+    }
+    const int kp2 = (d.K + 1) / 2;
+    const int x = (blk - lg.b_psi) * LAM_GEN_THREADS + t;      // (m, j, pair)
+    if (x >= d.G * d.P * kp2) return;
+    const int mj = x / kp2, q = x - mj * kp2, m = mj / d.P, j = mj - m * d.P;
+    double n0, n1;
+    rng.normal2(SITE_LAMBDA, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)q, it, n0, n1);
+    double *o = lg.NL + (size_t)mj * d.K + 2 * q;
+    o[0] = n0;
+    if (2 * q + 1 < d.K) o[1] = n1;
+}
+
 // hand-off between blocks of one launch (k_wcol, k_xdraw): payload by agent-scope stores,
 // s_waitcnt vmcnt(0), then a relaxed fetch-add on a monotonic 64-bit counter; consumers poll
 // it (s_sleep) up to the launch's target and read the payload with agent-scope loads
@@ -669,9 +703,16 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
                                                 double *__restrict__ X, DrawsDev dr, int64_t iter, int xroles,
                                                 const double *__restrict__ xa, unsigned long long *xm_ctr,
                                                 unsigned long long xm_target, int ndel,
-                                                const double *__restrict__ sall, DeltaArgs da) {
+                                                const double *__restrict__ sall, DeltaArgs da, LamGen lg) {
     __shared__ double smem[XD_SMEM];
     int blk = blockIdx.x;
+    {   // the loading-row variates of this iteration: blocks after the row blocks (lam_draws_block)
+        const int nlead = ((xroles & 1) ? 1 : 0) + ((xroles & 2) ? ndel : 0) + (d.n + 15) / 16;
+        if (blk >= nlead) {
+            lam_draws_block(d, lg, iter, blk - nlead);
+            return;
+        }
+    }
     if (xroles & 1) {   // producer of XM
         if (blk == 0) {
             for (int e = threadIdx.x; e < KP * KP; e += 1024) xprec_store(d, smem, e, xa[e]);
@@ -915,29 +956,36 @@ __global__ __launch_bounds__(64 * cp_waves<KW>()) void k_cpass(Dims d, const dou
 
 // ============================================================================
 // k_lambda: loading rows.                                   dc:140-145 (+150,156,169-171)
-// One wave = 8 loading rows j; an aligned 8-lane group owns one row: lane l holds rows
-// r_b = l + 8b (b = 0..3) of Q_j = diag(Plam_j) + ps_j E_m in registers, row r_b only
-// up to column 8b + 7 (the lower triangle, compile-time pruned: 80 values per lane, ~1.6x
-// the minimal work instead of ~3.5x for 16 lanes x 2 rows).  Per pair of pivots (k, k+1):
-//   * every lane writes its rows' current column pair (and rhs) to the group's LDS image,
-//   * all lanes read the 2x2 pivot block and the rhs pair from it and form the pivots,
-//   * each row forms its L entries and the coefficients (alpha, beta) of the rank-2 update
-//     q[c] -= alpha Q[c][k] + beta Q[c][k+1] (the L column pair expressed through the
-//     unnormalised image, so one LDS round per step), and the forward solve
-//     L v = ps_j C_j rides along (dc:143 vlam = Llam \ blam).
-// Then Lambda_j = L' \ (v + z) (dc:143-144) from the bottom, the sums over rows below a
-// column as 8-lane DPP reductions; psi_j (dc:150), SS_j = yy_j - 2 x.C_j + x'E x and
-// ps_j, omega_j (dc:169-171), with x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j from the
-// solve itself (x'Q_j x = |L'x|^2 = |w|^2), so E is read once.  Plam_j = psi_j o tau'
-// (dc:176) is formed from the previous iteration's psi and tau unless plam_src is given
-// (first iteration after dcfm_set_state).  The row's variates (drawn in place, or loaded
-// from a draw buffer) are formed first, before the rows of Q_j occupy the registers.
-// psi o lambda^2 of the row -> cpart[m][j][:] (k_colsum sums the rows).
+// One wave = 8 loading rows j of shard m; an aligned 8-lane group owns one row's K x K
+// system: lane l holds rows r_b = l + 8b of the system in registers, row r_b only up to
+// column min(8b + 7, KE - 1) (the lower triangle, compile-time pruned; KE = K rounded up to
+// an instantiated width, rows >= K identity padding).
+//   * Q_j = ps_j E_m + diag(Plam_j) (dc:141) is factored as ps_j (E_m + diag(Plam_j / ps_j)):
+//     L_Q = sqrt(ps_j) L, so E_m enters unscaled (staged once per wave in LDS: 8 dwordx4 global
+//     loads per lane, the 8 groups then read it as LDS broadcasts), the rhs of the forward solve
+//     is sqrt(ps_j) C_j (= L_Q v = b, dc:143 vlam) and Lambda_j = L^{-T} (v + z) / sqrt(ps_j)
+//     (dc:143-144 mlam + ylam).
+//   * Pivots two at a time: each group writes the current column pair of its rows (and the
+//     rhs) to an LDS image; every lane reads the 2x2 pivot block from it and forms the rank-2
+//     update q[c] -= alpha Q[c][k] + beta Q[c][k+1] of its rows from the unnormalised image
+//     (one LDS round per pair).  The image is double-buffered: the next pair's columns are
+//     updated first and written to the other buffer, so the next pivots' LDS round trip and
+//     rsqrt chain overlap the rest of this pair's update, whose image reads are issued a batch
+//     of LAM_PIPE columns ahead of their FMAs.
+//   * Back solve L' x = w from the bottom, the sums over the group's rows as 8-lane DPP sums.
+//   * psi_j (dc:150, tau of the previous iteration), SS_j = yy_j - 2 x.C_j + x'E x with
+//     x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j and ps_j x.C_j = w.v (no third Y pass, no
+//     second read of E or C), ps_j and omega_j (dc:169-171), psi o Lambda^2 -> cpart (dc:156).
+// Plam_j = psi_j o tau' (dc:176) is formed from the previous iteration's psi and tau unless
+// plam_src is given (first iteration after dcfm_set_state).  The row's variates (dc:142, 150,
+// 170) come from a draw buffer: the generated chain's k_xdraw draws them (lam_draws_block),
+// injected draws and the k_draws batches are read in place.
 // ============================================================================
+// DPP moves within the aligned 8-lane group (every source lane of these patterns is valid)
 template <int CTRL>
 __device__ __forceinline__ double dpp8_d(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);
 }
 // sum over the aligned 8-lane group (identical bits in every lane: each stage adds a
@@ -950,271 +998,285 @@ __device__ __forceinline__ double rowsum8(double v) {
 }
 
 constexpr int LAM_ROWS = 8;   // loading rows per wave
-__global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict__ C,
-                                               const double *__restrict__ E,
-                                               const double *__restrict__ yy,
-                                               const double *__restrict__ tau_cur,
+constexpr int LAM_PIPE = 4;   // image columns read ahead of their trailing-update FMAs
+__host__ __device__ constexpr int lam_ncol(int KE, int b) { return 8 * b + 8 < KE ? 8 * b + 8 : KE; }
+
+// pivot pair (k, k+1) from the image: 2x2 Cholesky block, the forward-solve entries and the
+// coefficients the rows' updates need
+struct LamPiv { double i00, i11, l10, v0, v1, t10; };
+__device__ __forceinline__ LamPiv lam_pivots(d2 pk, d2 pk1, d2 bb) {
+    LamPiv p;
+    const double a = pk.x, bq = pk1.x, c2 = pk1.y;
+    p.i00 = rsqrt_f64(a);
+    p.l10 = bq * p.i00;
+    const double d11 = c2 - p.l10 * p.l10;
+    p.i11 = rsqrt_f64(d11);
+    p.v0 = bb.x * p.i00;
+    p.v1 = (bb.y - p.l10 * p.v0) * p.i11;
+    p.t10 = p.l10 * p.i11;
+    return p;
+}
+
+template <int KE>
+__global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict__ C, const double *__restrict__ E,
+                                               const double *__restrict__ yy, const double *__restrict__ tau_cur,
                                                double *__restrict__ Lam, double *__restrict__ psi,
                                                const double *__restrict__ plam_src, double *__restrict__ ps,
-                                               double *__restrict__ omega,
-                                               double *__restrict__ cpart, DrawsDev dr,
-                                               int64_t iter, int gen) {
-    // per system: rows' unnormalised column pair of the current step (+1 row of padding:
-    // the 8 systems' images start 4 banks apart), and the rhs of the forward solve
-    __shared__ __attribute__((aligned(16))) double LS[LAM_ROWS][KP + 1][2];
-    __shared__ __attribute__((aligned(16))) double BS[LAM_ROWS][KP + 2];
-    // per system: v = L^{-1} blam (dc:143) and 1 / L[r][r], written at each pivot step
-    __shared__ __attribute__((aligned(16))) double VS[LAM_ROWS][KP + 2];
-    __shared__ __attribute__((aligned(16))) double IS[LAM_ROWS][KP + 2];
-    const int m = blockIdx.y;
-    const int mg = d.shard0 + m;
+                                               double *__restrict__ omega, double *__restrict__ cpart,
+                                               LamDraws ld) {
+    static_assert(KE % 2 == 0 && KE >= 2 && KE <= KP, "even factor width");
+    constexpr int NB = (KE + 7) / 8;
+    // LDS: double-buffered image [2][8 systems][KP + 1 (bank spread)][2] | rhs image [2][8][KP+2] |
+    // per system v and 1 / L_kk [8][KP+2] each; E_m is staged (row pitch EP) in the image area first
+    constexpr int LSN = 2 * LAM_ROWS * (KP + 1) * 2, BSN = 2 * LAM_ROWS * (KP + 2), VSN = LAM_ROWS * (KP + 2);
+    constexpr int EP = KP + 2;
+    static_assert(KP * EP <= LSN + BSN, "E staging fits the image area");
+    __shared__ __attribute__((aligned(16))) double SM[LSN + BSN + 2 * VSN];
+    double(*LS)[LAM_ROWS][KP + 1][2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 1][2]>(SM);
+    double(*BS)[LAM_ROWS][KP + 2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 2]>(SM + LSN);
+    double *Vs = SM + LSN + BSN, *Is = Vs + VSN;
+    double *Es = SM;
+    const int m = blockIdx.y, mg = d.shard0 + m;
     const int lane = threadIdx.x, grp = lane >> 3, l = lane & 7;
+    Vs += grp * (KP + 2);
+    Is += grp * (KP + 2);
     const int j = blockIdx.x * LAM_ROWS + grp;
     const bool valid = j < d.P;
     const int jj = valid ? j : 0;
-    const uint32_t rowoff = (uint32_t)(m * d.PP + jj) * KP;
-    const uint32_t toff = (uint32_t)mg * KP;
+    const uint32_t rowoff = (uint32_t)(m * d.PP + jj) * KP, toff = (uint32_t)mg * KP;
     bool rv[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) rv[b] = valid && l + 8 * b < d.K;
-    const double psj = valid ? ps[(uint32_t)(m * d.PP + jj)] : 0.0;
-    const double yyj = (valid && l == 0) ? yy[(uint32_t)(m * d.PP + jj)] : 0.0;
+    {   // E_m rows < KE: lane t moves pairs 2t + 128 i
+        const double *Em = E + (uint32_t)m * KP * KP;
+        constexpr int NI = (KE * KP + 127) / 128;
+        d2 e[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) e[i] = *reinterpret_cast<const d2 *>(Em + 2 * lane + 128 * i);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int f = 2 * lane + 128 * i, r = f >> 5, c = f & 31;
+            *reinterpret_cast<d2 *>(Es + r * EP + c) = e[i];
+        }
+    }
+    const double psj = valid ? ps[(uint32_t)(m * d.PP + jj)] : 1.0;
+    const double isj = rsqrt_f64(psj), sj = psj * isj;     // 1 / sqrt(ps_j), sqrt(ps_j)
+    const double ipsj = isj * isj;
     const double *pin = plam_src ? plam_src : psi;
-    // Plam_j (dc:176) and blam = ps_j eta' Y_j (dc:141), loaded ahead of the draw code
-    // (addresses are in range for every lane: jj is clamped and r < KP; the values are
-    // selected after the loads, so no load waits behind a branch)
-    double pv[4], tv[4], cv[4];
+    double dg[4], bv[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-        pv[b] = pin[rowoff + l + 8 * b];
-        tv[b] = tau_cur[toff + l + 8 * b];
-        cv[b] = C[rowoff + l + 8 * b];
+        const double pv = pin[rowoff + l + 8 * b], tv = tau_cur[toff + l + 8 * b], cv = C[rowoff + l + 8 * b];
+        dg[b] = rv[b] ? (plam_src ? pv : pv * tv) * ipsj : 1.0;   // Plam_j / ps_j; identity padding
+        bv[b] = valid ? sj * cv : 0.0;
     }
-    auto plam_of = [&](int b) {
-        const int r = l + 8 * b;
-        const double p = pin[rowoff + r], tr = tau_cur[toff + r];
-        return rv[b] ? (plam_src ? p : p * tr) : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    double q0[lam_ncol(KE, 0)], q1[NB > 1 ? lam_ncol(KE, 1) : 1], q2[NB > 2 ? lam_ncol(KE, 2) : 1],
+        q3[NB > 3 ? lam_ncol(KE, 3) : 1];
+    auto qref = [&](auto NBc) -> auto & {
+        constexpr int b = decltype(NBc)::value;
+        if constexpr (b == 0) return q0;
+        else if constexpr (b == 1) return q1;
+        else if constexpr (b == 2) return q2;
+        else return q3;
     };
-    // ---- the row's variates: z (dc:142), the psi gammas (dc:150), the ps gamma (dc:170),
-    //      formed before the 80-value rows are live (the draw code needs ~60 registers)
-    double z[4], G[4], Gps = 0.0;
-    const uint32_t ti = (uint32_t)(iter - dr.first_iter);
-    const uint32_t drow = (ti * (uint32_t)d.g + (uint32_t)mg) * (uint32_t)d.P + (uint32_t)jj;
-    const uint32_t dk = drow * (uint32_t)d.K;
-    if (!gen) {       // injected, or k_draws buffers (the paths other than the fused chain)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            z[b] = rv[b] ? dr.NL[dk + l + 8 * b] : 0.0;
-            G[b] = rv[b] ? dr.Gpsi[dk + l + 8 * b] : 0.0;
-        }
-        Gps = (valid && l == 0) ? dr.Gps[drow] : 0.0;
-    } else {          // drawn here, at the counters k_draws uses (identical values)
-        const Rng rng(d.seed);
-        const uint32_t it32 = (uint32_t)iter, mg32 = (uint32_t)mg, j32 = (uint32_t)jj;
-        // lane l draws normal pairs l and l + 8 (indices 2l, 2l+1, 2l+16, 2l+17); row r_b
-        // = l + 8b takes element r_b & 1 of pair (l >> 1) + 4b, i.e. pair slot b >> 1 of
-        // lane (l >> 1) + 4 (b & 1) of the group
-        double n0 = 0.0, n1 = 0.0, n2 = 0.0, n3 = 0.0;
-        if (valid) {
-            rng.normal2(SITE_LAMBDA, mg32, j32, (uint32_t)l, it32, n0, n1);
-            rng.normal2(SITE_LAMBDA, mg32, j32, (uint32_t)l + 8u, it32, n2, n3);
-        }
-        const int odd = l & 1;   // lanes l and l ^ 1 read the same source: both elements move
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int src = (grp << 3) | ((l >> 1) + 4 * (b & 1));
-            const double x0 = __shfl((b >> 1) ? n2 : n0, src, 64);
-            const double x1 = __shfl((b >> 1) ? n3 : n1, src, 64);
-            z[b] = rv[b] ? (odd ? x1 : x0) : 0.0;
-        }
-        const double shp = d.df * 0.5 + 0.5;
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-            G[b] = rv[b] ? rng.gamma(shp, SITE_PSI, mg32, j32, (uint32_t)(l + 8 * b), it32) : 0.0;
-        Gps = (valid && l == 0) ? rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, mg32, j32, 0u, it32) : 0.0;
-    }
-    // ---- Q_j rows r_b, columns <= 8b + 7: ps_j * eta2 + diag(Plam_j) (dc:141), identity padding
-    //      (every row's E loads are issued before the first is consumed: one L2 round trip)
-    double plam[4], bv[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        plam[b] = rv[b] ? (plam_src ? pv[b] : pv[b] * tv[b]) : 0.0;
-        bv[b] = valid ? psj * cv[b] : 0.0;
-    }
-    double q0[8], q1[16], q2[24], q3[32];
-    auto load = [&](auto &q, auto NB) {
-        constexpr int b = decltype(NB)::value, nc = 8 * b + 8;
-        const double *Er = E + ((uint32_t)m * KP + l + 8 * b) * KP;
+    static_for<NB>([&](auto NBc) {
+        constexpr int b = decltype(NBc)::value, nc = lam_ncol(KE, b);
+        auto &q = qref(NBc);
+        const double *Er = Es + (l + 8 * b) * EP;
 #pragma unroll
         for (int c = 0; c < nc; c += 2) {
             const d2 e = *reinterpret_cast<const d2 *>(Er + c);
             q[c] = e.x;
             q[c + 1] = e.y;
         }
-    };
-    auto build = [&](auto &q, auto NB) {
-        constexpr int b = decltype(NB)::value, nc = 8 * b + 8;
-        const int r = l + 8 * b;
-#pragma unroll
-        for (int c = 0; c < nc; ++c) q[c] *= psj;
 #pragma unroll
         for (int c = 8 * b; c < nc; ++c)
-            if (c == r) q[c] = rv[b] ? plam[b] + q[c] : 1.0;
-    };
-    load(q0, std::integral_constant<int, 0>{});
-    load(q1, std::integral_constant<int, 1>{});
-    load(q2, std::integral_constant<int, 2>{});
-    load(q3, std::integral_constant<int, 3>{});
-    build(q0, std::integral_constant<int, 0>{});
-    build(q1, std::integral_constant<int, 1>{});
-    build(q2, std::integral_constant<int, 2>{});
-    build(q3, std::integral_constant<int, 3>{});
-    double(*Ls)[2] = LS[grp];
-    double *Bs = BS[grp], *Vs = VS[grp], *Is = IS[grp];
-    // ---- factorisation, two pivots per step, forward solve fused
-    static_for<KP / 2>([&](auto JC) {
-        constexpr int k = 2 * decltype(JC)::value;
-        constexpr int b0 = k / 8;               // the first block with rows >= k
-        auto put = [&](auto &q, auto NB) {
-            constexpr int b = decltype(NB)::value;
-            if constexpr (b >= b0) {
-                const int r = l + 8 * b;
-                d2 v;
-                v.x = q[k];
-                v.y = q[k + 1];
-                *reinterpret_cast<d2 *>(Ls[r]) = v;
-                Bs[r] = bv[b];
-            }
-        };
-        put(q0, std::integral_constant<int, 0>{});
-        put(q1, std::integral_constant<int, 1>{});
-        put(q2, std::integral_constant<int, 2>{});
-        put(q3, std::integral_constant<int, 3>{});
-        __builtin_amdgcn_wave_barrier();
-        const d2 pk = *reinterpret_cast<const d2 *>(Ls[k]);
-        const d2 pk1 = *reinterpret_cast<const d2 *>(Ls[k + 1]);
-        const d2 bb = *reinterpret_cast<const d2 *>(Bs + k);
-        const double a = pk.x, bq = pk1.x, c2 = pk1.y;
-        const double i00 = rsqrt_f64(a);
-        const double l00 = a * i00, l10 = bq * i00;
-        const double d11 = c2 - l10 * l10;
-        const double i11 = rsqrt_f64(d11);
-        const double l11 = d11 * i11;
-        const double v0 = bb.x * i00, v1 = (bb.y - l10 * v0) * i11;
-        const double t10 = l10 * i11;
-        if (l == 0) {
+            if (c == l + 8 * b) q[c] += dg[b];
+    });
+    __builtin_amdgcn_wave_barrier();
+    // image of column pair (0, 1) (overwrites E's staging: every read of it is above)
+    static_for<NB>([&](auto NBc) {
+        constexpr int b = decltype(NBc)::value;
+        auto &q = qref(NBc);
+        d2 v;
+        v.x = q[0];
+        v.y = q[1];
+        *reinterpret_cast<d2 *>(LS[0][grp][l + 8 * b]) = v;
+        BS[0][grp][l + 8 * b] = bv[b];
+    });
+    __builtin_amdgcn_wave_barrier();
+    LamPiv pv = lam_pivots(*reinterpret_cast<const d2 *>(LS[0][grp][0]), *reinterpret_cast<const d2 *>(LS[0][grp][1]),
+                           *reinterpret_cast<const d2 *>(&BS[0][grp][0]));
+    // ---- factorisation (dc:142 Llam = chol(Qlam,'lower')), forward solve fused
+    static_for<KE / 2>([&](auto JC) {
+        constexpr int k = 2 * decltype(JC)::value, cur = decltype(JC)::value & 1, nxt = cur ^ 1;
+        constexpr int cb = k / 8, kk = k % 8;
+        double(*Ls)[2] = LS[cur][grp];
+        const LamPiv p = pv;
+        {   // every lane of the group stores the same values: no exec-mask branch
             d2 v, iv;
-            v.x = v0; v.y = v1; iv.x = i00; iv.y = i11;
+            v.x = p.v0; v.y = p.v1; iv.x = p.i00; iv.y = p.i11;
             *reinterpret_cast<d2 *>(Vs + k) = v;
             *reinterpret_cast<d2 *>(Is + k) = iv;
         }
-        double al[4], be[4];
-        auto piv = [&](auto &q, auto NB) {
-            constexpr int b = decltype(NB)::value;
-            al[b] = 0.0;
-            be[b] = 0.0;
-            if constexpr (b >= b0) {
-                const int r = l + 8 * b;
-                const double lr0 = q[k] * i00;
-                const double lr1 = (q[k + 1] - lr0 * l10) * i11;
-                if (r > k + 1) {
-                    q[k] = lr0;
+        // the rows' L entries of the pair, their update coefficients and forward-solve rhs;
+        // rows k and k+1 get their own entries from the same formulas (l00 = a i00, l10, l11 =
+        // d11 i11), only rows below the pair update their trailing columns
+        double al[4] = {0.0, 0.0, 0.0, 0.0}, be[4] = {0.0, 0.0, 0.0, 0.0};
+        static_for<NB>([&](auto NBc) {
+            constexpr int b = decltype(NBc)::value;
+            if constexpr (b >= cb) {
+                auto &q = qref(NBc);
+                const double lr0 = q[k] * p.i00;
+                const double lr1 = (q[k + 1] - lr0 * p.l10) * p.i11;
+                const double a_ = p.i00 * fma(-lr1, p.t10, lr0), b_ = lr1 * p.i11;
+                bv[b] = fma(-lr1, p.v1, fma(-lr0, p.v0, bv[b]));
+                q[k] = lr0;
+                if constexpr (b > cb) {
                     q[k + 1] = lr1;
-                    al[b] = i00 * fma(-lr1, t10, lr0);
-                    be[b] = lr1 * i11;
-                    bv[b] = fma(-lr1, v1, fma(-lr0, v0, bv[b]));
-                } else if (r == k + 1) {
-                    q[k] = l10;
-                    q[k + 1] = l11;
-                } else if (r == k) {
-                    q[k] = l00;
-                    q[k + 1] = 0.0;
+                    al[b] = a_;
+                    be[b] = b_;
+                } else {
+                    const bool below = l > kk + 1;
+                    q[k + 1] = (l == kk) ? 0.0 : lr1;
+                    al[b] = below ? a_ : 0.0;
+                    be[b] = below ? b_ : 0.0;
                 }
             }
-        };
-        piv(q0, std::integral_constant<int, 0>{});
-        piv(q1, std::integral_constant<int, 1>{});
-        piv(q2, std::integral_constant<int, 2>{});
-        piv(q3, std::integral_constant<int, 3>{});
-        // rank-2 trailing update of every row's columns k+2 .. 8b+7 from the image; the
-        // FMAs are pinned per column (hipcc would otherwise sink each to its consumer)
-        {
-            constexpr int cs = k + 2, ce = KP;
+        });
+        if constexpr (k + 2 < KE) {
+            constexpr int c0 = k + 2, cb2 = c0 / 8;
+            // columns c0, c0+1 first: the next pair's image
+            const d2 i2 = *reinterpret_cast<const d2 *>(Ls[c0]);
+            const d2 i3 = *reinterpret_cast<const d2 *>(Ls[c0 + 1]);
+            static_for<NB>([&](auto NBc) {
+                constexpr int b = decltype(NBc)::value;
+                if constexpr (b >= cb2) {
+                    auto &q = qref(NBc);
+                    q[c0] = fma(-be[b], i2.y, fma(-al[b], i2.x, q[c0]));
+                    q[c0 + 1] = fma(-be[b], i3.y, fma(-al[b], i3.x, q[c0 + 1]));
+                    d2 v;
+                    v.x = q[c0];
+                    v.y = q[c0 + 1];
+                    *reinterpret_cast<d2 *>(LS[nxt][grp][l + 8 * b]) = v;
+                    BS[nxt][grp][l + 8 * b] = bv[b];
+                }
+            });
+            __builtin_amdgcn_wave_barrier();
+            pv = lam_pivots(*reinterpret_cast<const d2 *>(LS[nxt][grp][c0]),
+                            *reinterpret_cast<const d2 *>(LS[nxt][grp][c0 + 1]),
+                            *reinterpret_cast<const d2 *>(&BS[nxt][grp][c0]));
+            // the rest of the rank-2 update, image reads a batch ahead
+            auto upd = [&](int c, d2 ic) {
+                static_for<NB>([&](auto NBc) {
+                    constexpr int b = decltype(NBc)::value;
+                    if constexpr (b >= cb) {
+                        auto &q = qref(NBc);
+                        constexpr int nq = lam_ncol(KE, b);
+                        if (c < nq) {
+                            double &x = q[c < nq ? c : 0];
+                            x = fma(-be[b], ic.y, fma(-al[b], ic.x, x));
+                        }
+                    }
+                });
+            };
+            constexpr int cs = c0 + 2, nbt = (KE - cs + LAM_PIPE - 1) / LAM_PIPE;
+            d2 buf[2][LAM_PIPE];
+            static_for<LAM_PIPE>([&](auto T) {
+                constexpr int c = cs + decltype(T)::value;
+                if constexpr (c < KE) buf[0][decltype(T)::value] = *reinterpret_cast<const d2 *>(Ls[c]);
+            });
+            static_for<nbt>([&](auto Bt) {
+                constexpr int bt = decltype(Bt)::value, cur_b = bt & 1;
+                if constexpr (bt + 1 < nbt) {
+                    static_for<LAM_PIPE>([&](auto T) {
+                        constexpr int c = cs + (bt + 1) * LAM_PIPE + decltype(T)::value;
+                        if constexpr (c < KE) buf[cur_b ^ 1][decltype(T)::value] = *reinterpret_cast<const d2 *>(Ls[c]);
+                    });
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                static_for<LAM_PIPE>([&](auto T) {
+                    constexpr int c = cs + bt * LAM_PIPE + decltype(T)::value;
+                    if constexpr (c < KE) upd(c, buf[cur_b][decltype(T)::value]);
+                });
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            // keep the trailing update eager: without this hipcc sinks each FMA to the step that
+            // consumes it and keeps the image values live
+            static_for<NB>([&](auto NBc) {
+                constexpr int b = decltype(NBc)::value;
+                if constexpr (b >= cb) {
+                    auto &q = qref(NBc);
 #pragma unroll
-            for (int c = cs; c < ce; ++c) {
-                const d2 qc = *reinterpret_cast<const d2 *>(Ls[c]);
-                if (c < 8) q0[c < 8 ? c : 0] = fma(-be[0], qc.y, fma(-al[0], qc.x, q0[c < 8 ? c : 0]));
-                if (c < 16) q1[c < 16 ? c : 0] = fma(-be[1], qc.y, fma(-al[1], qc.x, q1[c < 16 ? c : 0]));
-                if (c < 24) q2[c < 24 ? c : 0] = fma(-be[2], qc.y, fma(-al[2], qc.x, q2[c < 24 ? c : 0]));
-                q3[c] = fma(-be[3], qc.y, fma(-al[3], qc.x, q3[c]));
-            }
-#pragma unroll
-            for (int c = cs; c < ce; ++c) {
-                if (c < 8) asm volatile("" : "+v"(q0[c < 8 ? c : 0]));
-                if (c < 16) asm volatile("" : "+v"(q1[c < 16 ? c : 0]));
-                if (c < 24) asm volatile("" : "+v"(q2[c < 24 ? c : 0]));
-                asm volatile("" : "+v"(q3[c]));
-            }
+                    for (int c = c0; c < lam_ncol(KE, b); ++c) asm volatile("" : "+v"(q[c]));
+                }
+            });
         }
     });
-    // ---- back solve L' x = w, w = v + z (dc:142-144), pivots (c, c-1) from the bottom:
+    // ---- the row's variates (dc:142 zlam, dc:150, dc:170), Plam_j and tau for the epilogue
+    double z[4], G[4], tv[4], pl2[4];
+    const uint32_t dro = (uint32_t)(m * d.P + jj), dk = dro * (uint32_t)d.K;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t di = rv[b] ? dk + l + 8 * b : dk;
+        z[b] = ld.NL[di];
+        G[b] = ld.Gpsi[di];
+        const double p2 = pin[rowoff + l + 8 * b];
+        tv[b] = tau_cur[toff + l + 8 * b];
+        pl2[b] = plam_src ? p2 : p2 * tv[b];
+    }
+    const double Gps = ld.Gps[dro];
+    const double yyj = yy[(uint32_t)(m * d.PP + jj)];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        z[b] = rv[b] ? z[b] : 0.0;
+        G[b] = rv[b] ? G[b] : 0.0;
+        pl2[b] = rv[b] ? pl2[b] : 0.0;
+        tv[b] = rv[b] ? tv[b] : 0.0;
+    }
+    // ---- back solve L' x = w, w = v + z (dc:143-144), pivots (c, c-1) from the bottom:
     //      x_c = (w_c - sum_{r>c} L[r][c] x_r) / L[c][c], the sums over the group's lanes
     double x[4] = {0.0, 0.0, 0.0, 0.0};
-    double ww = 0.0, wv = 0.0;          // |w|^2 and w.v over the lane's rows
-    static_for<KP / 2>([&](auto JC) {
-        constexpr int c = KP - 1 - 2 * decltype(JC)::value;     // odd; c and c-1 in block cb
+    static_for<KE / 2>([&](auto JC) {
+        constexpr int c = KE - 1 - 2 * decltype(JC)::value;     // odd; c and c-1 in block cb
         constexpr int cb = c / 8;
         double pa = 0.0, pb = 0.0;
-        auto part = [&](auto &q, auto NB) {
-            constexpr int b = decltype(NB)::value;
-            if constexpr (b > cb) {                              // every row of the block is > c
-                pa = fma(q[c], x[b], pa);
-                pb = fma(q[c - 1], x[b], pb);
-            } else if constexpr (b == cb) {    // rows l + 8b > c only: x is still 0 for the others
+        static_for<NB>([&](auto NBc) {
+            constexpr int b = decltype(NBc)::value;
+            if constexpr (b >= cb) {   // block cb: rows above c have x = 0 still
+                auto &q = qref(NBc);
                 pa = fma(q[c], x[b], pa);
                 pb = fma(q[c - 1], x[b], pb);
             }
-        };
-        part(q0, std::integral_constant<int, 0>{});
-        part(q1, std::integral_constant<int, 1>{});
-        part(q2, std::integral_constant<int, 2>{});
-        part(q3, std::integral_constant<int, 3>{});
+        });
         pa = rowsum8(pa);
         pb = rowsum8(pb);
-        auto &qc = [&]() -> auto & {
-            if constexpr (cb == 0) return q0;
-            else if constexpr (cb == 1) return q1;
-            else if constexpr (cb == 2) return q2;
-            else return q3;
-        }();
+        auto &qc = qref(std::integral_constant<int, cb>{});
         const d2 vv = *reinterpret_cast<const d2 *>(Vs + c - 1);
         const d2 iv = *reinterpret_cast<const d2 *>(Is + c - 1);
-        double t = 0.0;
-        if (l + 8 * cb == c) {
-            const double wc = vv.y + z[cb];
-            x[cb] = (wc - pa) * iv.y;
-            t = qc[c - 1] * x[cb];                               // L[c][c-1] x_c
-            ww = fma(wc, wc, ww);
-            wv = fma(wc, vv.y, wv);
-        }
-        const double tb = dpp8_d<0x101>(t);                      // row_shl:1: lane c%8 -> c%8 - 1
-        if (l + 8 * cb == c - 1) {
-            const double wc = vv.x + z[cb];
-            x[cb] = (wc - pb - tb) * iv.x;
-            ww = fma(wc, wc, ww);
-            wv = fma(wc, vv.x, wv);
-        }
+        const bool isc = l + 8 * cb == c, isc1 = l + 8 * cb == c - 1;
+        const double xa = (vv.y + z[cb] - pa) * iv.y;
+        x[cb] = isc ? xa : x[cb];
+        const double t = isc ? qc[c - 1] * xa : 0.0;               // L[c][c-1] x_c
+        const double tb = dpp8_d<0x101>(t);                        // row_shl:1: lane c%8 -> c%8 - 1
+        const double xb = (vv.x + z[cb] - pb - tb) * iv.x;
+        x[cb] = isc1 ? xb : x[cb];
     });
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-        if (!rv[b]) x[b] = 0.0;
-    // ---- SS_j = yy_j - 2 x.C_j + x'E x (dc:169 by identity, no Y pass).  x = L'^{-1} w, so
+    // ---- SS_j = yy_j - 2 x.C_j + x'E x (dc:169 by identity, no Y pass).  x = L_Q'^{-1} w, so
     //      x'Q_j x = |w|^2 and x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j: no E re-read;
-    //      ps_j x.C_j = x.blam = x.(L v) = (L'x).v = w.v: no C re-read.
-    double px = 0.0;
+    //      ps_j x.C_j = x.blam = x.(L_Q v) = (L_Q'x).v = w.v: no C re-read.
+    double ww = 0.0, wv = 0.0, px = 0.0;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) px = fma(plam_of(b) * x[b], x[b], px);   // reloaded (L2): not held live
-    double contrib = (ww - px - 2.0 * wv) / psj;
+    for (int b = 0; b < NB; ++b) {
+        const double vr = Vs[l + 8 * b < KE ? l + 8 * b : 0];
+        const double w = vr + z[b];
+        ww = rv[b] ? fma(w, w, ww) : ww;
+        wv = rv[b] ? fma(w, vr, wv) : wv;
+        x[b] = rv[b] ? x[b] * isj : 0.0;                           // Lambda_j = L^{-T} w / sqrt(ps_j)
+        px = fma(pl2[b] * x[b], x[b], px);
+    }
+    double contrib = (ww - px - 2.0 * wv) * ipsj;
     contrib = valid ? contrib : 0.0;
     contrib = rowsum8(contrib);
     // ---- psi (dc:150, tau of the previous iteration, Q11) and the outputs
@@ -1222,17 +1284,16 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const int r = l + 8 * b;
-            const double tr = rv[b] ? tau_cur[toff + r] : 0.0;
-            const double ps_b = rv[b] ? (1.0 / (d.df * 0.5 + 0.5 * (x[b] * x[b] * tr))) * G[b] : 0.0;
+            const double ps_b = rv[b] ? (1.0 / (d.df * 0.5 + 0.5 * (x[b] * x[b] * tv[b]))) * G[b] : 0.0;
             Lam[rowoff + r] = x[b];
-            cpart[rowoff + r] = ps_b * (x[b] * x[b]);           // mat = psijh .* Lambda.^2 (dc:156)
+            cpart[rowoff + r] = ps_b * (x[b] * x[b]);               // mat = psijh .* Lambda.^2 (dc:156)
             if (rv[b]) psi[rowoff + r] = ps_b;
         }
         if (l == 0) {
             const double SS = yyj + contrib;
-            const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;   // dc:170
+            const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;     // dc:170
             ps[(uint32_t)(m * d.PP + j)] = psn;
-            omega[(uint32_t)(m * d.PP + j)] = 1.0 / psn;        // dc:171 (Q1)
+            omega[(uint32_t)(m * d.PP + j)] = 1.0 / psn;            // dc:171 (Q1)
         }
     }
 }
@@ -1890,25 +1951,34 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
     if (d.kp != KP) return wide::launch_xchol(d, b, s);
     hipLaunchKernelGGL(k_xchol, dim3(1), dim3(256), 0, s, d, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
 }
+static LamGen lam_gen_of(const Dims &d, const Bufs &b, bool lamgen) {
+    if (lamgen && b.ldraw) return lam_gen_plan(d, b.ldraw);
+    LamGen g = {};
+    return g;
+}
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
-                  bool from_shards) {
+                  bool from_shards, bool lamgen) {
     if (d.kp != KP) return wide::launch_xdraw(d, b, dr, iter, s);
     DeltaArgs da = {};
+    const LamGen lg = lam_gen_of(d, b, lamgen);
+    const dim3 grid(cdiv(d.n, 16) + lg.b_total);
     if (from_shards)   // one rank: sum the G shard messages here (no k_xred)
-        hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter, 0,
-                           nullptr, nullptr, 0ull, 0, nullptr, da);
+        hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter, 0,
+                           nullptr, nullptr, 0ull, 0, nullptr, da, lg);
     else
-        hipLaunchKernelGGL(k_xdraw, dim3(cdiv(d.n, 16)), dim3(1024), 0, s, d, b.xall, d.nranks, b.XM, b.X, dr,
-                           iter, 0, nullptr, nullptr, 0ull, 0, nullptr, da);
+        hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.xall, d.nranks, b.XM, b.X, dr,
+                           iter, 0, nullptr, nullptr, 0ull, 0, nullptr, da, lg);
 }
 void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
-                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s) {
+                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s,
+                     bool lamgen) {
     const int ndel = delta_in ? (d.g + 15) / 16 : 0;
     DeltaArgs da;
     da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
     da.iter = delta_iter;
-    hipLaunchKernelGGL(k_xdraw, dim3(ndel + cdiv(d.n, 16)), dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter,
-                       delta_in ? 2 : 0, nullptr, nullptr, 0ull, ndel, b.sall, da);
+    const LamGen lg = lam_gen_of(d, b, lamgen);
+    hipLaunchKernelGGL(k_xdraw, dim3(ndel + cdiv(d.n, 16) + lg.b_total), dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X,
+                       dr, iter, delta_in ? 2 : 0, nullptr, nullptr, 0ull, ndel, b.sall, da, lg);
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(((d.PP + d.kp) / 32) * d.G * (d.kp / 32));
@@ -1927,8 +1997,28 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, const double *plam_src, hipStream_t s, bool gen) {
     if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, plam_src, s);
-    hipLaunchKernelGGL(k_lambda, dim3(cdiv(d.P, LAM_ROWS), d.G), dim3(64), 0, s, d, b.C, b.E, b.yy, tau_cur, b.Lam,
-                       b.psi, plam_src, b.ps, b.omega, b.cpart, dr, iter, gen ? 1 : 0);
+    LamDraws ld;
+    if (gen) {   // this iteration's variates, drawn by k_xdraw
+        const LamGen g = lam_gen_plan(d, b.ldraw);
+        ld.NL = g.NL; ld.Gpsi = g.Gpsi; ld.Gps = g.Gps;
+    } else {     // [T][g][P][K] / [T][g][P] draw buffers: this iteration, this rank's first shard
+        const size_t row0 = ((size_t)(iter - dr.first_iter) * d.g + d.shard0) * d.P;
+        ld.NL = dr.NL + row0 * d.K;
+        ld.Gpsi = dr.Gpsi + row0 * d.K;
+        ld.Gps = dr.Gps + row0;
+    }
+    const dim3 grid(cdiv(d.P, LAM_ROWS), d.G);
+#define LAUNCH_LAM(KE)                                                                                       \
+    hipLaunchKernelGGL(k_lambda<KE>, grid, dim3(64), 0, s, d, b.C, b.E, b.yy, tau_cur, b.Lam, b.psi, plam_src, \
+                       b.ps, b.omega, b.cpart, ld)
+    // the factor width rounded up to an instantiated one (rows >= K are identity padding)
+    if (d.K <= 8) LAUNCH_LAM(8);
+    else if (d.K <= 16) LAUNCH_LAM(16);
+    else if (d.K <= 20) LAUNCH_LAM(20);
+    else if (d.K <= 24) LAUNCH_LAM(24);
+    else if (d.K <= 30) LAUNCH_LAM(30);
+    else LAUNCH_LAM(32);
+#undef LAUNCH_LAM
 }
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(d.G, d.kp / 32);

@@ -47,6 +47,12 @@ extern "C" {
 /* dcfm_config.flags */
 #define DCFM_FLAG_INJECT_DRAWS 0x1u  /* read standard variates from dcfm_set_draws
                                         buffers instead of on-device Philox        */
+#define DCFM_FLAG_UNFUSED      0x2u  /* K <= 32 through the per-kernel side-stream layout
+                                        (k_prep / k_xchol on a second stream, k_draws
+                                        batches) instead of the fused launch chain;
+                                        same results (tests, diagnostics)           */
+#define DCFM_FLAG_ONE_STREAM   0x4u  /* every launch on one stream (isolated timings) */
+#define DCFM_FLAG_FLAT_PRIORITY 0x8u /* default priority for every stream          */
 
 typedef struct dcfm_handle dcfm_handle;
 
