@@ -315,6 +315,31 @@ static int numeric_status(dcfm_handle *h) {
                                          "after dcfm_run; set_state / init_state to restart");
     return DCFM_OK;
 }
+// Collective entry points (get_sigma_cols, sigma_error) must take the same path on every rank:
+// a failure only some ranks see (an argument only the root checks, a non-finite local shard)
+// would otherwise leave the others blocked in the collective.  Every rank contributes
+// [invalid, numeric, other] failure counts to an all-reduce first; any failure anywhere
+// fails the call on all ranks (a rank that saw none reports which failure another rank had).
+static int agree(dcfm_handle *h, int code) {
+    if (h->d.nranks == 1) return code;
+    const double f[3] = {code == DCFM_ERR_INVALID ? 1.0 : 0.0, code == DCFM_ERR_NUMERIC ? 1.0 : 0.0,
+                         (code != DCFM_OK && code != DCFM_ERR_INVALID && code != DCFM_ERR_NUMERIC) ? 1.0 : 0.0};
+    double g[3] = {0.0, 0.0, 0.0};
+    const std::string mine = h->err;
+    hipError_t e = hipMemcpyAsync(h->b.agree, f, sizeof f, hipMemcpyHostToDevice, h->stream);
+    if (e != hipSuccess) return fail(h, DCFM_ERR_HIP, "agree: %s", hipGetErrorString(e));
+    if (int rc = coll_allreduce_sum(h, CH_ASM, h->b.agree, 3, h->stream)) return rc;
+    HIPC(h, hipMemcpyAsync(g, h->b.agree, sizeof g, hipMemcpyDeviceToHost, h->stream));
+    HIPC(h, hipStreamSynchronize(h->stream));
+    if (code != DCFM_OK) {
+        h->err = mine;
+        return code;
+    }
+    if (g[0] > 0.0) return fail(h, DCFM_ERR_INVALID, "another rank rejected the collective call's arguments");
+    if (g[1] > 0.0) return fail(h, DCFM_ERR_NUMERIC, "another rank's sampler state is non-finite");
+    if (g[2] > 0.0) return fail(h, DCFM_ERR_HIP, "the collective call failed on another rank");
+    return DCFM_OK;
+}
 static int reset_numeric(dcfm_handle *h) {
     HIPC(h, hipMemset(h->nan_dev, 0, sizeof(int)));
     *h->nan_host = 0;
@@ -381,19 +406,23 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         return fail(nullptr, DCFM_ERR_INVALID, "thin >= 1, mcmc >= 0, burnin >= 0 required");
     if (!(c.bs > 0 && c.bd1 > 0 && c.bd2 > 0 && c.df > 0))
         return fail(nullptr, DCFM_ERR_INVALID, "bs, bd1, bd2, df must be > 0 (dc:62-65)");
-    // on-device gammas are Marsaglia-Tsang for shape >= 1 (philox.h); the smallest shapes the
-    // stream draws are as, df/2 (init, dc:69,73), ad1, ad2 (dc:83) and df/2 + 0.5 (dc:150)
-    if (!(c.flags & DCFM_FLAG_INJECT_DRAWS) && !(c.as_ >= 1.0 && c.df >= 2.0 && c.ad1 >= 1.0 && c.ad2 >= 1.0))
-        return fail(nullptr, DCFM_ERR_UNSUPPORTED,
-                    "on-device gamma draws need shapes >= 1: as >= 1, df >= 2, ad1 >= 1, ad2 >= 1 "
-                    "(got %g, %g, %g, %g); inject the draws for other hyper-parameters", c.as_, c.df, c.ad1, c.ad2);
+    // on-device gammas (philox.h): Marsaglia-Tsang for shape >= 1, boosted below 1, so every
+    // positive hyper-parameter the reference accepts (dc:62-65) is drawn on the device
+    if (!(c.as_ > 0.0 && c.ad1 > 0.0 && c.ad2 > 0.0))
+        return fail(nullptr, DCFM_ERR_INVALID, "as, ad1, ad2 must be > 0 (dc:62-65; got %g, %g, %g)", c.as_, c.ad1,
+                    c.ad2);
     const int nranks = c.nranks < 1 ? 1 : c.nranks;
     if (c.rank < 0 || c.rank >= nranks) return fail(nullptr, DCFM_ERR_INVALID, "bad rank");
-    {   // the canonical shard-sum trees keep their levels in registers (TreeSum<.., 8 | 10>)
+    {   // the fused K <= 32 chain keeps the canonical shard-sum trees' levels in registers
+        // (k_wcol TreeSum<.., 8>, k_xdraw <.., 10>); the other layouts sum with TREE_LEVELS = 16
+        const bool fused = c.K <= KP && !(c.flags & DCFM_FLAG_UNFUSED);
         const int Gl = c.g / nranks, nxs = xsum_blocks(Gl);
-        if (c.g > 1023 || nxs > 255 || Gl / nxs > 255)
-            return fail(nullptr, DCFM_ERR_UNSUPPORTED, "g = %d shards (%d per rank): at most 1023, and a per-rank "
-                        "count whose odd part is below 256", c.g, Gl);
+        if (fused && (c.g > 1023 || nxs > 255 || Gl / nxs > 255))
+            return fail(nullptr, DCFM_ERR_UNSUPPORTED, "g = %d shards (%d per rank): the fused K <= 32 chain takes at "
+                        "most 1023, and a per-rank count whose odd part is below 256 (DCFM_FLAG_UNFUSED lifts "
+                        "this)", c.g, Gl);
+        if (!fused && c.g >= (1 << 16))    // TreeSum's default depth (linalg.h TREE_LEVELS)
+            return fail(nullptr, DCFM_ERR_UNSUPPORTED, "g = %d shards: at most %d", c.g, (1 << 16) - 1);
     }
     if (c.g % nranks)
         return fail(nullptr, DCFM_ERR_UNSUPPORTED, "g = %d not divisible by nranks = %d", c.g, nranks);
@@ -498,6 +527,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         ALLOC(b.xa_all, (size_t)nranks * KP * KP);
     }
     ALLOC(b.XM, 2 * KP * KP);
+    ALLOC(b.agree, 3);
     ALLOC(b.xpart, (size_t)G * KP * KP);  // k_wcol: xsum_blocks(G) <= G chunk sums
     {
         double *tk = nullptr;
@@ -1292,14 +1322,16 @@ int dcfm_get_sigma_cols(dcfm_handle *h, int64_t col0, int64_t ncols, double *out
     if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
     Dims &d = h->d;
     const int root = 0;
-    if (!out && d.rank == root) return fail(h, DCFM_ERR_INVALID, "null output on the root rank");
-    if (col0 < 0 || ncols < 0 || col0 + ncols > d.p)
-        return fail(h, DCFM_ERR_INVALID, "columns [%lld, %lld) outside 0..p = %d", (long long)col0,
+    int code = DCFM_OK;
+    if (!out && d.rank == root) code = fail(h, DCFM_ERR_INVALID, "null output on the root rank");
+    else if (col0 < 0 || ncols < 0 || col0 + ncols > d.p)
+        code = fail(h, DCFM_ERR_INVALID, "columns [%lld, %lld) outside 0..p = %d", (long long)col0,
                     (long long)(col0 + ncols), d.p);
-    if (ncols == 0) return DCFM_OK;
     HIPC(h, hipSetDevice(h->cfg.device));
     sync_all(h);
-    if (int rc = numeric_status(h)) return rc;
+    if (code == DCFM_OK) code = numeric_status(h);
+    if (int rc = agree(h, code)) return rc;     // every rank enters the gather, or none
+    if (ncols == 0) return DCFM_OK;
     const int nr = d.nranks;
     const long long p = d.p, c0 = col0, c1 = col0 + ncols;
     // every rank's packed-window count for this stripe (known to all ranks: no size exchange)
@@ -1423,11 +1455,15 @@ static uint64_t splitmix64(uint64_t &x) {
 
 int dcfm_sigma_error(dcfm_handle *h, const double *U, int32_t r, const double *sdiag, int32_t iters,
                      uint64_t seed, double out[3]) {
-    if (!h || !sdiag || !out || (r > 0 && !U)) return fail(h, DCFM_ERR_INVALID, "null argument");
-    if (r < 0 || r > 32) return fail(h, DCFM_ERR_INVALID, "truth rank r = %d outside 0..32", r);
-    if (iters < 0) return fail(h, DCFM_ERR_INVALID, "iters = %d < 0", iters);
+    if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
+    int code = DCFM_OK;
+    if (!sdiag || !out || (r > 0 && !U)) code = fail(h, DCFM_ERR_INVALID, "null argument");
+    else if (r < 0 || r > 32) code = fail(h, DCFM_ERR_INVALID, "truth rank r = %d outside 0..32", r);
+    else if (iters < 0) code = fail(h, DCFM_ERR_INVALID, "iters = %d < 0", iters);
     HIPC(h, hipSetDevice(h->cfg.device));
     sync_all(h);
+    if (code == DCFM_OK) code = numeric_status(h);
+    if (int rc = agree(h, code)) return rc;     // the all-reduces below run on every rank, or on none
     const Dims &d = h->d;
     const int p = d.p;
     const size_t P = (size_t)p;
@@ -1560,7 +1596,7 @@ int dcfm_get_kernel_stats(dcfm_handle *h, double ms[DCFM_K_COUNT], int64_t launc
 
 int dcfm_rng_fill(int device, uint64_t seed, int kind, double shape, int32_t site, int32_t shard,
                   int64_t iter, int64_t count, double *out) {
-    if (!out || count < 0 || (kind != 0 && kind != 1) || (kind == 1 && !(shape >= 1.0)))
+    if (!out || count < 0 || (kind != 0 && kind != 1) || (kind == 1 && !(shape > 0.0)))
         return fail(nullptr, DCFM_ERR_INVALID, "rng_fill: bad argument");
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return fail(nullptr, DCFM_ERR_HIP, "hipSetDevice: %s", hipGetErrorString(e));

@@ -100,6 +100,7 @@ struct Bufs {
     unsigned *ticket;                  // k_wcol last-arrival ticket (0 between launches)
     unsigned long long *sync;          // hand-off counters (monotonic): [2 + chunk] = k_wcol A_m of the chunk out
     double *msg_all;                   // packed gather target (fused, nranks > 1), else null
+    double *agree;                     // 3 doubles: the failure counts of a collective call (dcfm.hip agree)
     int2 *tiles;
     int ntiles, LDB;
     int T0, T1;                        // owned tile rows of Sigma (block-sharded, see above)

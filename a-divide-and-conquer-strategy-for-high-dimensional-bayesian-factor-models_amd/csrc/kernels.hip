@@ -29,6 +29,7 @@
 #include "dcfm_internal.h"
 #include "philox.h"
 #include "linalg.h"
+#include "lambda.h"
 
 #include <algorithm>
 
@@ -616,43 +617,17 @@ __device__ __forceinline__ void draws_block(const Dims &d, const DrawsDev &dr, i
                         const_cast<double *>(dr.NL) + ((size_t)mg * d.P + j) * K);
     }
 }
-// The loading-row variates of one iteration (dc:142 zlam, dc:150 psi gammas, dc:170 ps
-// gamma) into k_lambda's buffer layout, at the counters every other path draws them from
-// (k_draws, dcfm_rng_fill): one thread per ps gamma, per psi gamma and per normal pair, the
-// rejection-sampled ps gammas first.  Runs as extra blocks of k_xdraw (latency-bound, most
-// CUs idle) so the loading-row kernel reads its variates instead of drawing them.
-__device__ __forceinline__ void lam_draws_block(const Dims &d, const LamGen &lg, int64_t iter, int blk) {
-    const Rng rng(d.seed);
-    const uint32_t it = (uint32_t)iter;
-    const int t = threadIdx.x;
-    if (blk < lg.b_ps) {
-        const int x = blk * LAM_GEN_THREADS + t;            // (m, j)
-        if (x >= d.G * d.P) return;
-        const int m = x / d.P, j = x - m * d.P;
-        lg.Gps[x] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, (uint32_t)(d.shard0 + m), (uint32_t)j, 0u, it);
-        return;
-    }
-    if (blk < lg.b_psi) {
-        const int x = (blk - lg.b_ps) * LAM_GEN_THREADS + t;   // (m, j, k)
-        if (x >= d.G * d.P * d.K) return;
-        const int mj = x / d.K, k = x - mj * d.K, m = mj / d.P, j = mj - m * d.P;
-        lg.Gpsi[x] = rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)k, it);
-        return;
-    }
-    const int kp2 = (d.K + 1) / 2;
-    const int x = (blk - lg.b_psi) * LAM_GEN_THREADS + t;      // (m, j, pair)
-    if (x >= d.G * d.P * kp2) return;
-    const int mj = x / kp2, q = x - mj * kp2, m = mj / d.P, j = mj - m * d.P;
-    double n0, n1;
-    rng.normal2(SITE_LAMBDA, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)q, it, n0, n1);
-    double *o = lg.NL + (size_t)mj * d.K + 2 * q;
-    o[0] = n0;
-    if (2 * q + 1 < d.K) o[1] = n1;
-}
-
 // hand-off between blocks of one launch (k_wcol, k_xdraw): payload by agent-scope stores,
 // s_waitcnt vmcnt(0), then a relaxed fetch-add on a monotonic 64-bit counter; consumers poll
-// it (s_sleep) up to the launch's target and read the payload with agent-scope loads
+// it (s_sleep) up to the launch's target and read the payload with agent-scope loads.
+// Hardware assumption (not the HIP memory model's release / acquire, which on gfx950 costs an
+// L2 write-back + invalidate per hand-off, +25 us per k_wcol in round 1): this is the guide's
+// cross-XCD hand-off recipe -- (1) every payload store is an agent-scope (sc1) atomic store that
+// bypasses the non-coherent per-XCD L2 copy, (2) the storing threads wait for those stores
+// (s_waitcnt vmcnt(0)) and meet at the workgroup barrier before one thread signals, (3) the
+// polled counter is an atomic, (4) every consumer load of the payload is an agent-scope (sc1)
+// load issued after the poll returned.  An ISA without sc1 coherence for relaxed agent-scope
+// atomics would break it; tests/test_gpu_loopback.py and the parity tests run these paths.
 __device__ __forceinline__ void signal_count(unsigned long long *ctr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // this thread's agent-scope stores are done
     __syncthreads();
@@ -954,349 +929,7 @@ __global__ __launch_bounds__(64 * cp_waves<KW>()) void k_cpass(Dims d, const dou
     }
 }
 
-// ============================================================================
-// k_lambda: loading rows.                                   dc:140-145 (+150,156,169-171)
-// One wave = 8 loading rows j of shard m; an aligned 8-lane group owns one row's K x K
-// system: lane l holds rows r_b = l + 8b of the system in registers, row r_b only up to
-// column min(8b + 7, KE - 1) (the lower triangle, compile-time pruned; KE = K rounded up to
-// an instantiated width, rows >= K identity padding).
-//   * Q_j = ps_j E_m + diag(Plam_j) (dc:141) is factored as ps_j (E_m + diag(Plam_j / ps_j)):
-//     L_Q = sqrt(ps_j) L, so E_m enters unscaled (staged once per wave in LDS: 8 dwordx4 global
-//     loads per lane, the 8 groups then read it as LDS broadcasts), the rhs of the forward solve
-//     is sqrt(ps_j) C_j (= L_Q v = b, dc:143 vlam) and Lambda_j = L^{-T} (v + z) / sqrt(ps_j)
-//     (dc:143-144 mlam + ylam).
-//   * Pivots two at a time: each group writes the current column pair of its rows (and the
-//     rhs) to an LDS image; every lane reads the 2x2 pivot block from it and forms the rank-2
-//     update q[c] -= alpha Q[c][k] + beta Q[c][k+1] of its rows from the unnormalised image
-//     (one LDS round per pair).  The image is double-buffered: the next pair's columns are
-//     updated first and written to the other buffer, so the next pivots' LDS round trip and
-//     rsqrt chain overlap the rest of this pair's update, whose image reads are issued a batch
-//     of LAM_PIPE columns ahead of their FMAs.
-//   * Back solve L' x = w from the bottom, the sums over the group's rows as 8-lane DPP sums.
-//   * psi_j (dc:150, tau of the previous iteration), SS_j = yy_j - 2 x.C_j + x'E x with
-//     x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j and ps_j x.C_j = w.v (no third Y pass, no
-//     second read of E or C), ps_j and omega_j (dc:169-171), psi o Lambda^2 -> cpart (dc:156).
-// Plam_j = psi_j o tau' (dc:176) is formed from the previous iteration's psi and tau unless
-// plam_src is given (first iteration after dcfm_set_state).  The row's variates (dc:142, 150,
-// 170) come from a draw buffer: the generated chain's k_xdraw draws them (lam_draws_block),
-// injected draws and the k_draws batches are read in place.
-// ============================================================================
-// DPP moves within the aligned 8-lane group (every source lane of these patterns is valid)
-template <int CTRL>
-__device__ __forceinline__ double dpp8_d(double v) {
-    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
-    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
-    return __hiloint2double(hi, lo);
-}
-// sum over the aligned 8-lane group (identical bits in every lane: each stage adds a
-// commutative pair)
-__device__ __forceinline__ double rowsum8(double v) {
-    v += dpp8_d<0xB1>(v);     // quad_perm [1,0,3,2]
-    v += dpp8_d<0x4E>(v);     // quad_perm [2,3,0,1]
-    v += dpp8_d<0x141>(v);    // row_half_mirror: the other quad of the 8
-    return v;
-}
-
-constexpr int LAM_ROWS = 8;   // loading rows per wave
-constexpr int LAM_PIPE = 4;   // image columns read ahead of their trailing-update FMAs
-__host__ __device__ constexpr int lam_ncol(int KE, int b) { return 8 * b + 8 < KE ? 8 * b + 8 : KE; }
-
-// pivot pair (k, k+1) from the image: 2x2 Cholesky block, the forward-solve entries and the
-// coefficients the rows' updates need
-struct LamPiv { double i00, i11, l10, v0, v1, t10; };
-__device__ __forceinline__ LamPiv lam_pivots(d2 pk, d2 pk1, d2 bb) {
-    LamPiv p;
-    const double a = pk.x, bq = pk1.x, c2 = pk1.y;
-    p.i00 = rsqrt_f64(a);
-    p.l10 = bq * p.i00;
-    const double d11 = c2 - p.l10 * p.l10;
-    p.i11 = rsqrt_f64(d11);
-    p.v0 = bb.x * p.i00;
-    p.v1 = (bb.y - p.l10 * p.v0) * p.i11;
-    p.t10 = p.l10 * p.i11;
-    return p;
-}
-
-template <int KE>
-__global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict__ C, const double *__restrict__ E,
-                                               const double *__restrict__ yy, const double *__restrict__ tau_cur,
-                                               double *__restrict__ Lam, double *__restrict__ psi,
-                                               const double *__restrict__ plam_src, double *__restrict__ ps,
-                                               double *__restrict__ omega, double *__restrict__ cpart,
-                                               LamDraws ld) {
-    static_assert(KE % 2 == 0 && KE >= 2 && KE <= KP, "even factor width");
-    constexpr int NB = (KE + 7) / 8;
-    // LDS: double-buffered image [2][8 systems][KP + 1 (bank spread)][2] | rhs image [2][8][KP+2] |
-    // per system v and 1 / L_kk [8][KP+2] each; E_m is staged (row pitch EP) in the image area first
-    constexpr int LSN = 2 * LAM_ROWS * (KP + 1) * 2, BSN = 2 * LAM_ROWS * (KP + 2), VSN = LAM_ROWS * (KP + 2);
-    constexpr int EP = KP + 2;
-    static_assert(KP * EP <= LSN + BSN, "E staging fits the image area");
-    __shared__ __attribute__((aligned(16))) double SM[LSN + BSN + 2 * VSN];
-    double(*LS)[LAM_ROWS][KP + 1][2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 1][2]>(SM);
-    double(*BS)[LAM_ROWS][KP + 2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 2]>(SM + LSN);
-    double *Vs = SM + LSN + BSN, *Is = Vs + VSN;
-    double *Es = SM;
-    const int m = blockIdx.y, mg = d.shard0 + m;
-    const int lane = threadIdx.x, grp = lane >> 3, l = lane & 7;
-    Vs += grp * (KP + 2);
-    Is += grp * (KP + 2);
-    const int j = blockIdx.x * LAM_ROWS + grp;
-    const bool valid = j < d.P;
-    const int jj = valid ? j : 0;
-    const uint32_t rowoff = (uint32_t)(m * d.PP + jj) * KP, toff = (uint32_t)mg * KP;
-    bool rv[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) rv[b] = valid && l + 8 * b < d.K;
-    {   // E_m rows < KE: lane t moves pairs 2t + 128 i
-        const double *Em = E + (uint32_t)m * KP * KP;
-        constexpr int NI = (KE * KP + 127) / 128;
-        d2 e[NI];
-#pragma unroll
-        for (int i = 0; i < NI; ++i) e[i] = *reinterpret_cast<const d2 *>(Em + 2 * lane + 128 * i);
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int f = 2 * lane + 128 * i, r = f >> 5, c = f & 31;
-            *reinterpret_cast<d2 *>(Es + r * EP + c) = e[i];
-        }
-    }
-    const double psj = valid ? ps[(uint32_t)(m * d.PP + jj)] : 1.0;
-    const double isj = rsqrt_f64(psj), sj = psj * isj;     // 1 / sqrt(ps_j), sqrt(ps_j)
-    const double ipsj = isj * isj;
-    const double *pin = plam_src ? plam_src : psi;
-    double dg[4], bv[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const double pv = pin[rowoff + l + 8 * b], tv = tau_cur[toff + l + 8 * b], cv = C[rowoff + l + 8 * b];
-        dg[b] = rv[b] ? (plam_src ? pv : pv * tv) * ipsj : 1.0;   // Plam_j / ps_j; identity padding
-        bv[b] = valid ? sj * cv : 0.0;
-    }
-    __builtin_amdgcn_wave_barrier();
-    double q0[lam_ncol(KE, 0)], q1[NB > 1 ? lam_ncol(KE, 1) : 1], q2[NB > 2 ? lam_ncol(KE, 2) : 1],
-        q3[NB > 3 ? lam_ncol(KE, 3) : 1];
-    auto qref = [&](auto NBc) -> auto & {
-        constexpr int b = decltype(NBc)::value;
-        if constexpr (b == 0) return q0;
-        else if constexpr (b == 1) return q1;
-        else if constexpr (b == 2) return q2;
-        else return q3;
-    };
-    static_for<NB>([&](auto NBc) {
-        constexpr int b = decltype(NBc)::value, nc = lam_ncol(KE, b);
-        auto &q = qref(NBc);
-        const double *Er = Es + (l + 8 * b) * EP;
-#pragma unroll
-        for (int c = 0; c < nc; c += 2) {
-            const d2 e = *reinterpret_cast<const d2 *>(Er + c);
-            q[c] = e.x;
-            q[c + 1] = e.y;
-        }
-#pragma unroll
-        for (int c = 8 * b; c < nc; ++c)
-            if (c == l + 8 * b) q[c] += dg[b];
-    });
-    __builtin_amdgcn_wave_barrier();
-    // image of column pair (0, 1) (overwrites E's staging: every read of it is above)
-    static_for<NB>([&](auto NBc) {
-        constexpr int b = decltype(NBc)::value;
-        auto &q = qref(NBc);
-        d2 v;
-        v.x = q[0];
-        v.y = q[1];
-        *reinterpret_cast<d2 *>(LS[0][grp][l + 8 * b]) = v;
-        BS[0][grp][l + 8 * b] = bv[b];
-    });
-    __builtin_amdgcn_wave_barrier();
-    LamPiv pv = lam_pivots(*reinterpret_cast<const d2 *>(LS[0][grp][0]), *reinterpret_cast<const d2 *>(LS[0][grp][1]),
-                           *reinterpret_cast<const d2 *>(&BS[0][grp][0]));
-    // ---- factorisation (dc:142 Llam = chol(Qlam,'lower')), forward solve fused
-    static_for<KE / 2>([&](auto JC) {
-        constexpr int k = 2 * decltype(JC)::value, cur = decltype(JC)::value & 1, nxt = cur ^ 1;
-        constexpr int cb = k / 8, kk = k % 8;
-        double(*Ls)[2] = LS[cur][grp];
-        const LamPiv p = pv;
-        {   // every lane of the group stores the same values: no exec-mask branch
-            d2 v, iv;
-            v.x = p.v0; v.y = p.v1; iv.x = p.i00; iv.y = p.i11;
-            *reinterpret_cast<d2 *>(Vs + k) = v;
-            *reinterpret_cast<d2 *>(Is + k) = iv;
-        }
-        // the rows' L entries of the pair, their update coefficients and forward-solve rhs;
-        // rows k and k+1 get their own entries from the same formulas (l00 = a i00, l10, l11 =
-        // d11 i11), only rows below the pair update their trailing columns
-        double al[4] = {0.0, 0.0, 0.0, 0.0}, be[4] = {0.0, 0.0, 0.0, 0.0};
-        static_for<NB>([&](auto NBc) {
-            constexpr int b = decltype(NBc)::value;
-            if constexpr (b >= cb) {
-                auto &q = qref(NBc);
-                const double lr0 = q[k] * p.i00;
-                const double lr1 = (q[k + 1] - lr0 * p.l10) * p.i11;
-                const double a_ = p.i00 * fma(-lr1, p.t10, lr0), b_ = lr1 * p.i11;
-                bv[b] = fma(-lr1, p.v1, fma(-lr0, p.v0, bv[b]));
-                q[k] = lr0;
-                if constexpr (b > cb) {
-                    q[k + 1] = lr1;
-                    al[b] = a_;
-                    be[b] = b_;
-                } else {
-                    const bool below = l > kk + 1;
-                    q[k + 1] = (l == kk) ? 0.0 : lr1;
-                    al[b] = below ? a_ : 0.0;
-                    be[b] = below ? b_ : 0.0;
-                }
-            }
-        });
-        if constexpr (k + 2 < KE) {
-            constexpr int c0 = k + 2, cb2 = c0 / 8;
-            // columns c0, c0+1 first: the next pair's image
-            const d2 i2 = *reinterpret_cast<const d2 *>(Ls[c0]);
-            const d2 i3 = *reinterpret_cast<const d2 *>(Ls[c0 + 1]);
-            static_for<NB>([&](auto NBc) {
-                constexpr int b = decltype(NBc)::value;
-                if constexpr (b >= cb2) {
-                    auto &q = qref(NBc);
-                    q[c0] = fma(-be[b], i2.y, fma(-al[b], i2.x, q[c0]));
-                    q[c0 + 1] = fma(-be[b], i3.y, fma(-al[b], i3.x, q[c0 + 1]));
-                    d2 v;
-                    v.x = q[c0];
-                    v.y = q[c0 + 1];
-                    *reinterpret_cast<d2 *>(LS[nxt][grp][l + 8 * b]) = v;
-                    BS[nxt][grp][l + 8 * b] = bv[b];
-                }
-            });
-            __builtin_amdgcn_wave_barrier();
-            pv = lam_pivots(*reinterpret_cast<const d2 *>(LS[nxt][grp][c0]),
-                            *reinterpret_cast<const d2 *>(LS[nxt][grp][c0 + 1]),
-                            *reinterpret_cast<const d2 *>(&BS[nxt][grp][c0]));
-            // the rest of the rank-2 update, image reads a batch ahead
-            auto upd = [&](int c, d2 ic) {
-                static_for<NB>([&](auto NBc) {
-                    constexpr int b = decltype(NBc)::value;
-                    if constexpr (b >= cb) {
-                        auto &q = qref(NBc);
-                        constexpr int nq = lam_ncol(KE, b);
-                        if (c < nq) {
-                            double &x = q[c < nq ? c : 0];
-                            x = fma(-be[b], ic.y, fma(-al[b], ic.x, x));
-                        }
-                    }
-                });
-            };
-            constexpr int cs = c0 + 2, nbt = (KE - cs + LAM_PIPE - 1) / LAM_PIPE;
-            d2 buf[2][LAM_PIPE];
-            static_for<LAM_PIPE>([&](auto T) {
-                constexpr int c = cs + decltype(T)::value;
-                if constexpr (c < KE) buf[0][decltype(T)::value] = *reinterpret_cast<const d2 *>(Ls[c]);
-            });
-            static_for<nbt>([&](auto Bt) {
-                constexpr int bt = decltype(Bt)::value, cur_b = bt & 1;
-                if constexpr (bt + 1 < nbt) {
-                    static_for<LAM_PIPE>([&](auto T) {
-                        constexpr int c = cs + (bt + 1) * LAM_PIPE + decltype(T)::value;
-                        if constexpr (c < KE) buf[cur_b ^ 1][decltype(T)::value] = *reinterpret_cast<const d2 *>(Ls[c]);
-                    });
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                static_for<LAM_PIPE>([&](auto T) {
-                    constexpr int c = cs + bt * LAM_PIPE + decltype(T)::value;
-                    if constexpr (c < KE) upd(c, buf[cur_b][decltype(T)::value]);
-                });
-                __builtin_amdgcn_sched_barrier(0);
-            });
-            // keep the trailing update eager: without this hipcc sinks each FMA to the step that
-            // consumes it and keeps the image values live
-            static_for<NB>([&](auto NBc) {
-                constexpr int b = decltype(NBc)::value;
-                if constexpr (b >= cb) {
-                    auto &q = qref(NBc);
-#pragma unroll
-                    for (int c = c0; c < lam_ncol(KE, b); ++c) asm volatile("" : "+v"(q[c]));
-                }
-            });
-        }
-    });
-    // ---- the row's variates (dc:142 zlam, dc:150, dc:170), Plam_j and tau for the epilogue
-    double z[4], G[4], tv[4], pl2[4];
-    const uint32_t dro = (uint32_t)(m * d.P + jj), dk = dro * (uint32_t)d.K;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const uint32_t di = rv[b] ? dk + l + 8 * b : dk;
-        z[b] = ld.NL[di];
-        G[b] = ld.Gpsi[di];
-        const double p2 = pin[rowoff + l + 8 * b];
-        tv[b] = tau_cur[toff + l + 8 * b];
-        pl2[b] = plam_src ? p2 : p2 * tv[b];
-    }
-    const double Gps = ld.Gps[dro];
-    const double yyj = yy[(uint32_t)(m * d.PP + jj)];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        z[b] = rv[b] ? z[b] : 0.0;
-        G[b] = rv[b] ? G[b] : 0.0;
-        pl2[b] = rv[b] ? pl2[b] : 0.0;
-        tv[b] = rv[b] ? tv[b] : 0.0;
-    }
-    // ---- back solve L' x = w, w = v + z (dc:143-144), pivots (c, c-1) from the bottom:
-    //      x_c = (w_c - sum_{r>c} L[r][c] x_r) / L[c][c], the sums over the group's lanes
-    double x[4] = {0.0, 0.0, 0.0, 0.0};
-    static_for<KE / 2>([&](auto JC) {
-        constexpr int c = KE - 1 - 2 * decltype(JC)::value;     // odd; c and c-1 in block cb
-        constexpr int cb = c / 8;
-        double pa = 0.0, pb = 0.0;
-        static_for<NB>([&](auto NBc) {
-            constexpr int b = decltype(NBc)::value;
-            if constexpr (b >= cb) {   // block cb: rows above c have x = 0 still
-                auto &q = qref(NBc);
-                pa = fma(q[c], x[b], pa);
-                pb = fma(q[c - 1], x[b], pb);
-            }
-        });
-        pa = rowsum8(pa);
-        pb = rowsum8(pb);
-        auto &qc = qref(std::integral_constant<int, cb>{});
-        const d2 vv = *reinterpret_cast<const d2 *>(Vs + c - 1);
-        const d2 iv = *reinterpret_cast<const d2 *>(Is + c - 1);
-        const bool isc = l + 8 * cb == c, isc1 = l + 8 * cb == c - 1;
-        const double xa = (vv.y + z[cb] - pa) * iv.y;
-        x[cb] = isc ? xa : x[cb];
-        const double t = isc ? qc[c - 1] * xa : 0.0;               // L[c][c-1] x_c
-        const double tb = dpp8_d<0x101>(t);                        // row_shl:1: lane c%8 -> c%8 - 1
-        const double xb = (vv.x + z[cb] - pb - tb) * iv.x;
-        x[cb] = isc1 ? xb : x[cb];
-    });
-    // ---- SS_j = yy_j - 2 x.C_j + x'E x (dc:169 by identity, no Y pass).  x = L_Q'^{-1} w, so
-    //      x'Q_j x = |w|^2 and x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j: no E re-read;
-    //      ps_j x.C_j = x.blam = x.(L_Q v) = (L_Q'x).v = w.v: no C re-read.
-    double ww = 0.0, wv = 0.0, px = 0.0;
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const double vr = Vs[l + 8 * b < KE ? l + 8 * b : 0];
-        const double w = vr + z[b];
-        ww = rv[b] ? fma(w, w, ww) : ww;
-        wv = rv[b] ? fma(w, vr, wv) : wv;
-        x[b] = rv[b] ? x[b] * isj : 0.0;                           // Lambda_j = L^{-T} w / sqrt(ps_j)
-        px = fma(pl2[b] * x[b], x[b], px);
-    }
-    double contrib = (ww - px - 2.0 * wv) * ipsj;
-    contrib = valid ? contrib : 0.0;
-    contrib = rowsum8(contrib);
-    // ---- psi (dc:150, tau of the previous iteration, Q11) and the outputs
-    if (valid) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int r = l + 8 * b;
-            const double ps_b = rv[b] ? (1.0 / (d.df * 0.5 + 0.5 * (x[b] * x[b] * tv[b]))) * G[b] : 0.0;
-            Lam[rowoff + r] = x[b];
-            cpart[rowoff + r] = ps_b * (x[b] * x[b]);               // mat = psijh .* Lambda.^2 (dc:156)
-            if (rv[b]) psi[rowoff + r] = ps_b;
-        }
-        if (l == 0) {
-            const double SS = yyj + contrib;
-            const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;     // dc:170
-            ps[(uint32_t)(m * d.PP + j)] = psn;
-            omega[(uint32_t)(m * d.PP + j)] = 1.0 / psn;            // dc:171 (Q1)
-        }
-    }
-}
+// k_lambda (loading rows, dc:140-145,150,156,169-171): lambda.h
 
 // ============================================================================
 // k_colsum: sloc[m][k] = sum_{j<P} cpart[m][j][k], fixed order            dc:156 sum(mat)

@@ -12,9 +12,10 @@
 //           gammas : 0x80000000 | index << 8 | attempt << 1 | {0: normal, 1: uniform}
 //
 // Standard normal: Box-Muller on two 53-bit uniforms in (0,1].
-// Standard gamma(a >= 1): Marsaglia-Tsang squeeze/rejection (every gamma shape
-// in the reference is >= 1: df/2+0.5 = 2, as+n/2, ad+P*K/2 ...); shapes 1 and 2
-// (the psi site uses 2) as a sum of exponentials.
+// Standard gamma(a >= 1): Marsaglia-Tsang squeeze/rejection (every gamma shape the
+// reference's defaults draw is >= 1: df/2+0.5 = 2, as+n/2, ad+P*K/2 ...); shapes 1 and 2
+// (the psi site uses 2) as a sum of exponentials; a < 1 (other hyper-parameters) by the
+// boost Ga(a) = Ga(a+1) U^(1/a).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -164,10 +165,16 @@ struct Rng {
         return (idx & 1u) ? b : a;
     }
 
-    // standard gamma(shape >= 1): integer shapes 1, 2 inline (the psi site), else
-    // Marsaglia & Tsang (2000)
+    // standard gamma(shape > 0): integer shapes 1, 2 inline (the psi site), shapes >= 1
+    // Marsaglia & Tsang (2000), shapes below 1 by their boost Ga(a) = Ga(a + 1) U^(1/a)
+    // (U from its own counter: attempt bits 1..6 of gamma_mt never reach bit 7)
     __device__ __forceinline__ double gamma(double shape, uint32_t site, uint32_t shard, uint32_t row,
                                             uint32_t idx, uint32_t iter) const {
+        if (shape < 1.0) {
+            const double g1 = gamma_mt(shape + 1.0, site, shard, row, idx, iter);
+            const u32x4 b = raw(site, shard, row, 0x80000000u | ((idx & 0x7FFFFFu) << 8) | 0x80u, iter);
+            return g1 * exp(log_u01(u01_53(b.x, b.y)) / shape);
+        }
         if (shape == 1.0 || shape == 2.0) {
             // integer shape: sum of shape exponentials, -log(u1 [* u2]) — exact, no rejection; one
             // log of the product (>= 2^-106, a normal double) instead of a sum of two logs

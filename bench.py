@@ -185,6 +185,11 @@ def main():
                          "collectives; weak scaling) instead of splitting the shards of one chain")
     ap.add_argument("--err-iters", type=int, default=20,
                     help="Lanczos steps of the on-device truth error after the timed region (0: off)")
+    ap.add_argument("--converged-burnin", type=int, default=1000)
+    ap.add_argument("--converged-mcmc", type=int, default=5000,
+                    help="after the timed region (1 GPU): a separate chain of burnin + mcmc iterations at the "
+                         "same config whose posterior-mean Sigmaout error and split-R-hat / ESS are reported "
+                         "(north_star check 2 at the BASELINE shape; 0: off)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -324,6 +329,40 @@ def main():
                    "note": "after the timed region; chain of warmup+steps iterations, not converged"}
     smp.close()
 
+    # (4) north_star check (2) at this shape: a converged chain (BURNIN 1,000,
+    #     MCMC 5,000, thin 5) from its own init, outside the timed region; its posterior-mean
+    #     Sigmaout against the synthetic truth, with split-R-hat / ESS of the MCMC part's trace
+    converged = None
+    if world == 1 and args.converged_mcmc > 0 and args.err_iters > 0:
+        cb, cm = args.converged_burnin, args.converged_mcmc
+        smc = dcfm.Sampler(n, P, g, K, rho, cb, cm, thin, seed=7, device=device, asm_batch=args.asm_batch)
+        try:
+            Yc, _, _ = synth_data(n, p, factors=True)
+            smc.set_data_raw(Yc, cols)
+            del Yc
+            smc.init_state()
+            smc.run(1, cb)
+            smc.set_trace(cm)
+            smc.synchronize()
+            tc = time.perf_counter()
+            smc.run(cb + 1, cm)
+            smc.synchronize()
+            tc = time.perf_counter() - tc
+            ec0 = smc.sigma_error(U_true, s_true, iters=0)
+            ec1 = smc.sigma_error(U_true, s_true, iters=max(args.err_iters, 40))
+            summ = dcfm.diagnostics.summarize(smc.get_trace()[None])
+            converged = {"burnin": cb, "mcmc": cm, "thin": thin, "saved_samples": smc.saved_samples(),
+                         "fro_rel": round(ec0["fro_rel"], 6), "op": round(ec1["op"], 6),
+                         "op_rel": round(ec1["op"] / float(np.linalg.norm(U_true, 2) ** 2 + 0.0), 6),
+                         "split_rhat": {k: round(v["rhat"], 4) for k, v in summ.items()},
+                         "ess": {k: round(v["ess"], 1) for k, v in summ.items()},
+                         "mcmc_seconds": round(tc, 3),
+                         "note": "separate chain (seed 7) at the bench config, outside the timed region; "
+                                 "split-R-hat / ESS over the MCMC iterations' device trace; op_rel uses "
+                                 "||U U'||_2 as the truth's scale (the diagonal term adds < 1)"}
+        finally:
+            smc.close()
+
     diag = None
     if trace is not None and len(trace) >= 4:
         tr = torch.from_numpy(np.ascontiguousarray(trace))
@@ -410,6 +449,8 @@ def main():
     out["kernels"] = kern
     if sig_err:
         out["sigma_error"] = sig_err
+    if converged:
+        out["sigma_error_converged"] = converged
     out["ingest"] = ingest
     if diag:
         out["diagnostics"] = diag

@@ -81,9 +81,12 @@ def update_eta(st: SamplerState, rho):
     st.eta[...] = np.sqrt(rho) * st.X[:, :, None] + np.sqrt(1 - rho) * st.Z
 
 
-def update_Lambda_psi_delta_ps(st: SamplerState, D: Data, hyper: Hyper, d: IterDraws):
-    """dc:136-172 batched; SS_j by the identity (no residual pass over Y)."""
-    g, n, P = D.Ys.shape
+def loading_systems(st: SamplerState, D: Data, d: IterDraws):
+    """The loading rows' systems of dc:137-144 from the state after the eta update:
+    E (g x K x K, dc:138), C = eta'Y (g x P x K), Q_j = ps_j E + diag(Plam_j) (dc:141),
+    b_j = ps_j C_j, L_j = chol(Q_j, 'lower') (dc:142) and the draws z_j (all g x P x ...).
+    Lambda_j = L_j' \ (L_j \ b_j + z_j) solves Q_j Lambda_j = b_j + L_j z_j exactly."""
+    D = _as_data(D)
     K = st.Lambda.shape[1]
     eta = np.ascontiguousarray(np.moveaxis(st.eta, 2, 0))          # g x n x K
     E = np.swapaxes(eta, 1, 2) @ eta                                 # g x K x K, dc:138
@@ -95,8 +98,20 @@ def update_Lambda_psi_delta_ps(st: SamplerState, D: Data, hyper: Hyper, d: IterD
     b = ps[:, :, None] * C
     L = np.linalg.cholesky(Q)                                        # dc:142
     z = np.moveaxis(d.NL, (0, 1, 2), (2, 1, 0))                      # g x P x K
-    v = np.linalg.solve(L, b[..., None])[..., 0]
-    lam = np.linalg.solve(np.swapaxes(L, -1, -2), (v + z)[..., None])[..., 0]   # g x P x K
+    return E, C, Q, b, L, z
+
+
+def update_Lambda_psi_delta_ps(st: SamplerState, D: Data, hyper: Hyper, d: IterDraws, lam_given=None):
+    """dc:136-172 batched; SS_j by the identity (no residual pass over Y).  ``lam_given``
+    (P x K x g, MATLAB layout) replaces the loading draw: the rest of the update is then
+    applied to that Lambda (stage-wise parity checks of an implementation's later stages)."""
+    g, n, P = D.Ys.shape
+    E, C, Q, b, L, z = loading_systems(st, D, d)
+    if lam_given is None:
+        v = np.linalg.solve(L, b[..., None])[..., 0]
+        lam = np.linalg.solve(np.swapaxes(L, -1, -2), (v + z)[..., None])[..., 0]   # g x P x K
+    else:
+        lam = np.ascontiguousarray(np.moveaxis(np.asarray(lam_given, dtype=np.float64), 2, 0))
     st.Lambda[...] = np.moveaxis(lam, 0, 2)
     # psi (dc:150)
     tau = st.tauh[:, 0, :][None, :, :]

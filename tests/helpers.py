@@ -50,3 +50,62 @@ def sigma_stripe_from_lower(SigLower, c0, c1):
     r = np.arange(SigLower.shape[0])[:, None]
     c = np.arange(c0, c1)[None, :]
     return np.where(r >= c, lo, up)
+
+
+def loading_backward_error(lam_mat, Q, b, L, z):
+    """Per-row backward error of a loading draw (dc:142-144): the exact draw solves
+    Q_j lam_j = b_j + L_j z_j, so || Q_j lam_j - b_j - L_j z_j || / (||Q_j|| ||lam_j|| + ||b_j||
+    + ||L_j|| ||z_j||) is ~ machine epsilon for any backward-stable solve, whatever cond(Q_j).
+    lam_mat: P x K x g (MATLAB layout); the systems g x P x ... (oracle.vectorised.loading_systems).
+    Returns the worst row."""
+    lam = np.moveaxis(np.asarray(lam_mat, dtype=np.float64), 2, 0)          # g x P x K
+    r = np.einsum("mjkl,mjl->mjk", Q, lam) - b - np.einsum("mjkl,mjl->mjk", L, z)
+    nq = np.linalg.norm(Q, axis=(-2, -1), ord=2)
+    nl = np.linalg.norm(L, axis=(-2, -1), ord=2)
+    den = nq * np.linalg.norm(lam, axis=-1) + np.linalg.norm(b, axis=-1) + nl * np.linalg.norm(z, axis=-1)
+    return float(np.max(np.linalg.norm(r, axis=-1) / den))
+
+
+def stagewise_errors(start, got, Yd, rho, hyper, draws, check_lambda=None):
+    """Stage-wise parity of one Gibbs iteration (absolute bars, no comparison of two
+    implementations' rounding): from the oracle state `start` at the iteration's start,
+      * the stages before the loading solve (Z, X, eta; dc:97-134) vs the oracle's, relative;
+      * the loading draw (dc:137-144) as the per-row backward error of got's Lambda against the
+        oracle's systems (Q_j, b_j, L_j, z_j) built from got's eta -- cond(Q_j) reaches ~1e7 at
+        c1/c2, where two restatements' forward errors differ by cond x eps (see
+        tests/test_gpu_parity_configs.py);
+      * every later stage (psi, delta/tau, ps, omega, Plam; dc:149-177) vs the oracle update
+        applied to got's own Lambda, relative (ps, omega per row and relative to the
+        conditioning kappa_j of the residual identity they are computed by).
+    `got` maps state fields to MATLAB-layout arrays (Sampler.get_state, or an oracle state's
+    as_dict()).  Returns ({field: rel err}, lambda backward error, the oracle state after the
+    iteration with got's Lambda)."""
+    from oracle import vectorised as V
+    D = V._as_data(Yd)
+    st = start.copy()
+    V.update_ZX(st, D, rho, draws)
+    V.update_eta(st, rho)
+    errs = {f: rel_err(got[f], getattr(st, f)) for f in ("X", "Z", "eta")}
+    for f in ("X", "Z", "eta"):        # the later stages from got's own inputs
+        getattr(st, f)[...] = np.asarray(got[f], dtype=np.float64).reshape(getattr(st, f).shape)
+    E, C, Q, b, L, z = V.loading_systems(st, D, draws)
+    bw = loading_backward_error(got["Lambda"], Q, b, L, z)
+    # ps_j (dc:169-171) from SS_j = yy_j - 2 lam_j.C_j + lam_j E lam_j': evaluating that sum (the
+    # oracle's and the kernels' identity, or the reference's direct residual) carries the condition
+    # number kappa_j = (yy_j + 2 sum_k |lam_jk C_jk| + sum_kl |lam_jk E_kl lam_jl|) / SS_j (up to
+    # ~1e6 at c2's second iteration, where the |X| excursions make E large), so its rows are
+    # compared relative to kappa_j: a forward-error bound, no second implementation involved
+    lam = np.moveaxis(np.asarray(got["Lambda"], dtype=np.float64), 2, 0)   # g x P x K
+    ss = D.yy - 2.0 * np.einsum("mjk,mjk->mj", lam, C) + np.einsum("mjk,mkl,mjl->mj", lam, E, lam)
+    alc = np.einsum("mjk,mjk->mj", np.abs(lam), np.abs(C))
+    alel = np.einsum("mjk,mkl,mjl->mj", np.abs(lam), np.abs(E), np.abs(lam))
+    kappa = np.maximum(1.0, (D.yy + 2.0 * alc + alel) / np.abs(ss)).T         # P x g
+    V.update_Lambda_psi_delta_ps(st, D, hyper, draws, lam_given=got["Lambda"])
+    V.update_Plam(st)
+    for f in ("psi", "delta", "tauh", "Plam"):
+        errs[f] = rel_err(got[f], getattr(st, f))
+    for f in ("ps", "omega"):
+        a = np.asarray(got[f], dtype=np.float64).reshape(kappa.shape)
+        r = np.asarray(getattr(st, f), dtype=np.float64).reshape(kappa.shape)
+        errs[f] = float(np.max(np.abs(a - r) / np.abs(r) / kappa))
+    return errs, bw, st

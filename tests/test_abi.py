@@ -77,11 +77,16 @@ def test_create_validates_before_touching_a_device(dcfm):
     assert _create(dcfm, thin=0)[0] == _abi.DCFM_ERR_INVALID
     assert _create(dcfm, n=0)[0] == _abi.DCFM_ERR_INVALID
     assert _create(dcfm, bs=0.0)[0] == _abi.DCFM_ERR_INVALID
-    # on-device gamma needs shape >= 1 (no shape < 1 boost): rejected unless draws are injected
-    assert _create(dcfm, df=1.5)[0] == _abi.DCFM_ERR_UNSUPPORTED
-    assert _create(dcfm, as_=0.5)[0] == _abi.DCFM_ERR_UNSUPPORTED
-    assert _create(dcfm, ad2=0.9)[0] == _abi.DCFM_ERR_UNSUPPORTED
-    assert _create(dcfm, ad1=0.5, flags=_abi.DCFM_FLAG_INJECT_DRAWS)[0] != _abi.DCFM_ERR_UNSUPPORTED
+    # every positive hyper-parameter the reference accepts (dc:62-65) is drawn on the device
+    # (gamma shapes below 1 by the boost): past validation, to the device lookup
+    for kw in (dict(df=1.5), dict(as_=0.5), dict(ad2=0.9), dict(ad1=0.5, flags=_abi.DCFM_FLAG_INJECT_DRAWS)):
+        assert _create(dcfm, **kw)[0] not in (_abi.DCFM_ERR_UNSUPPORTED, _abi.DCFM_ERR_INVALID), kw
+    assert _create(dcfm, as_=0.0)[0] == _abi.DCFM_ERR_INVALID
+    assert _create(dcfm, ad2=-1.0)[0] == _abi.DCFM_ERR_INVALID
+    # the register tree of the fused K <= 32 chain caps g; the side-stream layout does not
+    assert _create(dcfm, g=1024, P=2)[0] == _abi.DCFM_ERR_UNSUPPORTED
+    assert _create(dcfm, g=1024, P=2, flags=_abi.DCFM_FLAG_UNFUSED)[0] not in (_abi.DCFM_ERR_UNSUPPORTED,
+                                                                             _abi.DCFM_ERR_INVALID)
 
 
 def test_create_without_gpu_reports_hip_error(dcfm, gpu_available):

@@ -16,32 +16,35 @@ copies of p x p), must match to the north_star bar of 1e-10 normwise relative
 Conditioning.  The reference chain's second iteration is not always well conditioned: with
 quirks Q1 (Omega as a variance) and Q2 (the (R R')^-1 operator) the X / Z draws make
 excursions (|X| ~ 1e3 at c2), E = eta'eta reaches cond ~1e7 and so does Q_j of the loading
-rows (dc:141).  Two restatements of the reference then differ by cond * eps: the faithful
-loop and the vectorised oracle differ by 1.3e-9 in Lambda at c2's iteration 2 (8e-12 at c3,
-7e-14 at c4).  No implementation can meet 1e-10 there, so where the faithful loop is cheap
-enough to run (c1, c2) the bar of iteration 2 is max(1e-10, 10 x the faithful-vs-vectorised
-spread of the same conditional updates from the same state); everything upstream of the
-loading solve (Z, X, eta) and all of iteration 1 keep the strict 1e-10.  c3 and c4 are
-strict throughout (their faithful iterations take 30-80 s; spreads measured 8e-12 / 7e-14).
+rows (dc:141); any two restatements' Lambda then differ by cond x eps (the faithful loop and
+the vectorised oracle by 1.3e-9 at c2).  Where that happens (c1, c2 iteration 2) the bars are
+absolute and stage-wise (tests/helpers.stagewise_errors, the same check that pins the
+vectorised oracle to the faithful loop at c2 / c3 in tests/test_oracle.py): the stages
+before the loading solve (Z, X, eta) at 1e-10 against the oracle; the loading draw by its
+per-row backward error against the oracle's systems Q_j, b_j, L_j, z_j (<= 1e-13); every
+later stage (psi, delta / tau, ps, omega, Plam) at 1e-10 against the oracle update applied to
+the GPU's own Lambda (ps, omega relative to the residual identity's condition number); and
+Sigmaout at 1e-10 against the oracle assembly of the GPU's own Lambda and omega.  No bar is
+defined relative to another implementation.  Iteration 1 everywhere, and c3 / c4
+throughout, keep the direct 1e-10 comparison.
 """
 import numpy as np
 import pytest
 
-from helpers import STATE_CMP, make_case, rel_err, sigma_stripe_from_lower, stacked_draws, state_dict
-from oracle import dc_oracle as F
+from helpers import (STATE_CMP, make_case, rel_err, sigma_stripe_from_lower, stacked_draws, stagewise_errors,
+                     state_dict)
 from oracle import vectorised as V
 
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-10
 CONFIGS = {
-    # name: (n, p, g, K, faithful spread check)
+    # name: (n, p, g, K, stage-wise bars at iteration 2)
     "c1": (100, 1000, 4, 5, True),
     "c2": (500, 5000, 8, 20, True),
     "c3": (1000, 19968, 64, 30, False),
     "c4": (2000, 10000, 8, 100, False),
 }
-UPSTREAM = ("X", "Z", "eta")   # drawn before the loading solve: always strict
 
 
 def _sigma_err(smp, SigL, p, w=2048):
@@ -56,9 +59,12 @@ def _sigma_err(smp, SigL, p, w=2048):
     return worst
 
 
+BW_TOL = 1e-13    # per-row backward error of the loading draw (helpers.loading_backward_error)
+
+
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_baseline_shape_parity(dcfm, name):
-    n, p, g, K, spread_check = CONFIGS[name]
+    n, p, g, K, stagewise = CONFIGS[name]
     burnin, mcmc, thin = 1, 1, 1
     N = burnin + mcmc
     effsamp = mcmc / thin
@@ -73,26 +79,27 @@ def test_baseline_shape_parity(dcfm, name):
         ref = st.copy()
         SigL = None
         for it in range(1, N + 1):
-            tol = {f: TOL for f in STATE_CMP}
-            tol_S = TOL
-            if it > 1 and spread_check:
-                alt = ref.copy()                                   # same state at the iteration's start
-                F.gibbs_iteration(alt, Yd, c["rho"], c["hyper"], c["src"].iteration(it))
+            start = ref.copy()
             smp.run(it, 1)
             SigL = V.run_chain(D, ref, c["rho"], c["hyper"], c["src"].iteration, it, 1,
                                burnin, mcmc, thin, SigLower=SigL)
-            if it > 1 and spread_check:
-                for f in STATE_CMP:
-                    if f not in UPSTREAM:
-                        tol[f] = max(TOL, 10.0 * rel_err(getattr(alt, f), getattr(ref, f)))
-                Salt = V.full(V.assemble_lower(np.zeros_like(SigL), alt, c["rho"], effsamp))
-                tol_S = max(TOL, 10.0 * rel_err(Salt, V.full(SigL)))
             got = smp.get_state()
+            if it > 1 and stagewise:
+                errs, bw, _ = stagewise_errors(start, got, D, c["rho"], c["hyper"], c["src"].iteration(it))
+                for f, e in errs.items():
+                    assert e < TOL, f"{name} iter {it}: stage {f} rel err {e:.3e} (bar {TOL:.0e})"
+                assert bw < BW_TOL, f"{name} iter {it}: loading backward error {bw:.3e} (bar {BW_TOL:.0e})"
+                # the assembly stage (dc:182-195) of the GPU's own Lambda and omega
+                own = ref.copy()
+                own.Lambda[...] = got["Lambda"]
+                own.omega[...] = got["omega"]
+                SigL = V.assemble_lower(np.zeros_like(SigL), own, c["rho"], effsamp)
+                continue
             for f in STATE_CMP:
                 e = rel_err(got[f], getattr(ref, f))
-                assert e < tol[f], f"{name} iter {it}: {f} rel err {e:.3e} (bar {tol[f]:.1e})"
+                assert e < TOL, f"{name} iter {it}: {f} rel err {e:.3e} (bar {TOL:.0e})"
         assert smp.saved_samples() == 1
         e = _sigma_err(smp, SigL, c["p"])
-        assert e < tol_S, f"{name}: Sigmaout rel err {e:.3e} (bar {tol_S:.1e})"
+        assert e < TOL, f"{name}: Sigmaout rel err {e:.3e} (bar {TOL:.0e})"
     finally:
         smp.close()

@@ -56,6 +56,26 @@ def test_malformed_calls_are_rejected(mex):
     assert mex.locks() == 0
 
 
+def test_malformed_calls_under_address_and_ub_sanitizers(tmp_path):
+    """SURVEY §5 (race detection / sanitizers): the gateway and the mock MEX runtime built with
+    -fsanitize=address,undefined (host code only; GPU sanitizers are unavailable on the pool)
+    run the malformed-call suite (tests/mexmock/asan_main.c) with leak checking on: every call
+    is rejected with its error id and no out-of-bounds access, use after free, leak or undefined
+    behaviour is reported."""
+    import os
+    import subprocess
+    exe = tmp_path / "mex_asan"
+    cmd = ["gcc", *mm.FLAGS, "-g", "-O1", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+           "-fno-omit-frame-pointer", str(mm.ROOT / "matlab" / "dcfm_mex.c"),
+           str(mm.ROOT / "tests" / "mexmock" / "mexmock.c"), str(mm.ROOT / "tests" / "mexmock" / "asan_main.c"),
+           f"-L{mm.PKG}", "-ldcfm", f"-Wl,-rpath,{mm.PKG}", "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
+
+
 def test_create_without_gpu_reports_the_hip_error(mex, gpu_available):
     if gpu_available:
         pytest.skip("a GPU is present")

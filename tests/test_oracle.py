@@ -140,6 +140,30 @@ def test_faithful_vs_vectorised_at_c1_shape():
     assert rel_err(S2, S1) < 1e-12
 
 
+@pytest.mark.parametrize("name,n,p,g,K,iters", [("c2", 500, 5000, 8, 20, 2), ("c3", 1000, 19968, 64, 30, 1)])
+def test_faithful_vs_vectorised_at_baseline_shapes(name, n, p, g, K, iters):
+    """The vectorised oracle the BASELINE-shape GPU parity tests compare against is pinned to
+    the faithful per-row loop (the reference's loop structure, dc:97-177) AT those shapes, with
+    absolute bars: every iteration starts both restatements from the same state, and
+    tests/helpers.stagewise_errors checks the stages before the loading solve and after it at
+    1e-12 relative and the loading draw by its per-row backward error (<= 1e-14) -- at c2's
+    second iteration cond(Q_j) ~ 1e7 makes the two restatements' Lambda differ by ~1e-9 in
+    forward error while both solve their systems to machine precision."""
+    from helpers import stagewise_errors
+    c = make_case(n, p, g, K, seed=29, k0=10, dense_truth=False)
+    D = V.Data(c["Yd"])
+    st = c["st"].copy()
+    for it in range(1, iters + 1):
+        d = c["src"].iteration(it)
+        faithful = st.copy()
+        F.gibbs_iteration(faithful, c["Yd"], c["rho"], c["hyper"], d)
+        errs, bw, _ = stagewise_errors(st, faithful.as_dict(), D, c["rho"], c["hyper"], d)
+        for f, e in errs.items():
+            assert e < 1e-12, (name, it, f, e)
+        assert bw < 1e-14, (name, it, bw)
+        V.gibbs_iteration(st, D, c["rho"], c["hyper"], d)
+
+
 def test_posterior_mean_recovers_truth():
     """End-to-end statistical sanity of the oracle chain's Sigmaout against the synthetic truth.
 

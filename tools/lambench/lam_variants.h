@@ -1,6 +1,7 @@
 // Dev harness variants of the loading-row kernel (tools/lambench).  Not product code.
 #pragma once
 #include "linalg.h"
+#include "lambda.h"
 
 namespace dcfm {
 namespace lv {
@@ -919,11 +920,321 @@ __global__ __launch_bounds__(64) void k_lam_n3(Dims d, const double *__restrict_
     }
 }
 
+template <int KE>
+__global__ __launch_bounds__(64) void k_lam_n5(Dims d, const double *__restrict__ C, const double *__restrict__ E,
+                                               const double *__restrict__ yy, const double *__restrict__ tau_cur,
+                                               double *__restrict__ Lam, double *__restrict__ psi,
+                                               const double *__restrict__ plam_src, double *__restrict__ ps,
+                                               double *__restrict__ omega, double *__restrict__ cpart,
+                                               LamDraws ld) {
+    static_assert(KE % 2 == 0 && KE >= 2 && KE <= KP, "even factor width");
+    constexpr int NB = (KE + 7) / 8;
+    // LDS: double-buffered image [2][8 systems][KP + 1 (bank spread)][2] | rhs image [2][8][KP+2] |
+    // per system v and 1 / L_kk [8][KP+2] each; E_m is staged (row pitch EP) in the image area first
+    constexpr int LSN = 2 * LAM_ROWS * (KP + 1) * 2, BSN = 2 * LAM_ROWS * (KP + 2), VSN = LAM_ROWS * (KP + 2);
+    constexpr int EP = KP + 2;
+    static_assert(KP * EP <= LSN + BSN, "E staging fits the image area");
+    __shared__ __attribute__((aligned(16))) double SM[LSN + BSN + 2 * VSN];
+    double(*LS)[LAM_ROWS][KP + 1][2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 1][2]>(SM);
+    double(*BS)[LAM_ROWS][KP + 2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 2]>(SM + LSN);
+    double *Vs = SM + LSN + BSN, *Is = Vs + VSN;
+    double *Es = SM;
+    const int m = blockIdx.y, mg = d.shard0 + m;
+    const int lane = threadIdx.x, grp = lane >> 3, l = lane & 7;
+    Vs += grp * (KP + 2);
+    Is += grp * (KP + 2);
+    const int j = blockIdx.x * LAM_ROWS + grp;
+    const bool valid = j < d.P;
+    const int jj = valid ? j : 0;
+    const uint32_t rowoff = (uint32_t)(m * d.PP + jj) * KP, toff = (uint32_t)mg * KP;
+    bool rv[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) rv[b] = valid && l + 8 * b < d.K;
+    {   // E_m rows < KE: lane t moves pairs 2t + 128 i
+        const double *Em = E + (uint32_t)m * KP * KP;
+        constexpr int NI = (KE * KP + 127) / 128;
+        d2 e[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) e[i] = *reinterpret_cast<const d2 *>(Em + 2 * lane + 128 * i);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int f = 2 * lane + 128 * i, r = f >> 5, c = f & 31;
+            *reinterpret_cast<d2 *>(Es + r * EP + c) = e[i];
+        }
+    }
+    const double psj = valid ? ps[(uint32_t)(m * d.PP + jj)] : 1.0;
+    const double isj = rsqrt_f64(psj), sj = psj * isj;     // 1 / sqrt(ps_j), sqrt(ps_j)
+    const double ipsj = isj * isj;
+    const double *pin = plam_src ? plam_src : psi;
+    double dg[4], bv[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const double pv = pin[rowoff + l + 8 * b], tv = tau_cur[toff + l + 8 * b], cv = C[rowoff + l + 8 * b];
+        dg[b] = rv[b] ? (plam_src ? pv : pv * tv) * ipsj : 1.0;   // Plam_j / ps_j; identity padding
+        bv[b] = valid ? sj * cv : 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    double q0[lam_ncol(KE, 0)], q1[NB > 1 ? lam_ncol(KE, 1) : 1], q2[NB > 2 ? lam_ncol(KE, 2) : 1],
+        q3[NB > 3 ? lam_ncol(KE, 3) : 1];
+    auto qref = [&](auto NBc) -> auto & {
+        constexpr int b = decltype(NBc)::value;
+        if constexpr (b == 0) return q0;
+        else if constexpr (b == 1) return q1;
+        else if constexpr (b == 2) return q2;
+        else return q3;
+    };
+    static_for<NB>([&](auto NBc) {
+        constexpr int b = decltype(NBc)::value, nc = lam_ncol(KE, b);
+        auto &q = qref(NBc);
+        const double *Er = Es + (l + 8 * b) * EP;
+#pragma unroll
+        for (int c = 0; c < nc; c += 2) {
+            const d2 e = *reinterpret_cast<const d2 *>(Er + c);
+            q[c] = e.x;
+            q[c + 1] = e.y;
+        }
+#pragma unroll
+        for (int c = 8 * b; c < nc; ++c)
+            if (c == l + 8 * b) q[c] += dg[b];
+    });
+    __builtin_amdgcn_wave_barrier();
+    // image of column pair (0, 1) (overwrites E's staging: every read of it is above)
+    static_for<NB>([&](auto NBc) {
+        constexpr int b = decltype(NBc)::value;
+        auto &q = qref(NBc);
+        d2 v;
+        v.x = q[0];
+        v.y = q[1];
+        *reinterpret_cast<d2 *>(LS[0][grp][l + 8 * b]) = v;
+        BS[0][grp][l + 8 * b] = bv[b];
+    });
+    __builtin_amdgcn_wave_barrier();
+    LamPiv pv = lam_pivots(*reinterpret_cast<const d2 *>(LS[0][grp][0]), *reinterpret_cast<const d2 *>(LS[0][grp][1]),
+                           *reinterpret_cast<const d2 *>(&BS[0][grp][0]));
+    // ---- factorisation (dc:142 Llam = chol(Qlam,'lower')), forward solve fused
+    static_for<KE / 2>([&](auto JC) {
+        constexpr int k = 2 * decltype(JC)::value, cur = decltype(JC)::value & 1, nxt = cur ^ 1;
+        constexpr int cb = k / 8, kk = k % 8;
+        double(*Ls)[2] = LS[cur][grp];
+        const LamPiv p = pv;
+        {   // every lane of the group stores the same values: no exec-mask branch
+            d2 v, iv;
+            v.x = p.v0; v.y = p.v1; iv.x = p.i00; iv.y = p.i11;
+            *reinterpret_cast<d2 *>(Vs + k) = v;
+            *reinterpret_cast<d2 *>(Is + k) = iv;
+        }
+        // the rows' L entries of the pair, their update coefficients and forward-solve rhs;
+        // rows k and k+1 get their own entries from the same formulas (l00 = a i00, l10, l11 =
+        // d11 i11), only rows below the pair update their trailing columns
+        double al[4] = {0.0, 0.0, 0.0, 0.0}, be[4] = {0.0, 0.0, 0.0, 0.0};
+        static_for<NB>([&](auto NBc) {
+            constexpr int b = decltype(NBc)::value;
+            if constexpr (b >= cb) {
+                auto &q = qref(NBc);
+                const double lr0 = q[k] * p.i00;
+                const double lr1 = (q[k + 1] - lr0 * p.l10) * p.i11;
+                const double a_ = p.i00 * fma(-lr1, p.t10, lr0), b_ = lr1 * p.i11;
+                bv[b] = fma(-lr1, p.v1, fma(-lr0, p.v0, bv[b]));
+                q[k] = lr0;
+                if constexpr (b > cb) {
+                    q[k + 1] = lr1;
+                    al[b] = a_;
+                    be[b] = b_;
+                } else {
+                    const bool below = l > kk + 1;
+                    q[k + 1] = (l == kk) ? 0.0 : lr1;
+                    al[b] = below ? a_ : 0.0;
+                    be[b] = below ? b_ : 0.0;
+                }
+            }
+        });
+        if constexpr (k + 2 < KE) {
+            constexpr int c0 = k + 2, cb2 = c0 / 8;
+            // columns c0, c0+1 first: the next pair's image
+            const d2 i2 = *reinterpret_cast<const d2 *>(Ls[c0]);
+            const d2 i3 = *reinterpret_cast<const d2 *>(Ls[c0 + 1]);
+            static_for<NB>([&](auto NBc) {
+                constexpr int b = decltype(NBc)::value;
+                if constexpr (b >= cb2) {
+                    auto &q = qref(NBc);
+                    q[c0] = fma(-be[b], i2.y, fma(-al[b], i2.x, q[c0]));
+                    q[c0 + 1] = fma(-be[b], i3.y, fma(-al[b], i3.x, q[c0 + 1]));
+                    d2 v;
+                    v.x = q[c0];
+                    v.y = q[c0 + 1];
+                    *reinterpret_cast<d2 *>(LS[nxt][grp][l + 8 * b]) = v;
+                    BS[nxt][grp][l + 8 * b] = bv[b];
+                }
+            });
+            __builtin_amdgcn_wave_barrier();
+            // next pivot pair: reads issued now, its chain computed in stages inside the batches below
+            const d2 npk = *reinterpret_cast<const d2 *>(LS[nxt][grp][c0]);
+            const d2 npk1 = *reinterpret_cast<const d2 *>(LS[nxt][grp][c0 + 1]);
+            const d2 nbb = *reinterpret_cast<const d2 *>(&BS[nxt][grp][c0]);
+            LamPiv np;
+            auto stage = [&](int st) {
+                if (st == 0) np.i00 = rsqrt_f64(npk.x);
+                if (st == 1) {
+                    np.l10 = npk1.x * np.i00;
+                    np.i11 = rsqrt_f64(npk1.y - np.l10 * np.l10);
+                }
+                if (st == 2) {
+                    np.v0 = nbb.x * np.i00;
+                    np.v1 = (nbb.y - np.l10 * np.v0) * np.i11;
+                    np.t10 = np.l10 * np.i11;
+                }
+            };
+            // the rest of the rank-2 update, image reads a batch ahead
+            auto upd = [&](int c, d2 ic) {
+                static_for<NB>([&](auto NBc) {
+                    constexpr int b = decltype(NBc)::value;
+                    if constexpr (b >= cb) {
+                        auto &q = qref(NBc);
+                        constexpr int nq = lam_ncol(KE, b);
+                        if (c < nq) {
+                            double &x = q[c < nq ? c : 0];
+                            x = fma(-be[b], ic.y, fma(-al[b], ic.x, x));
+                        }
+                    }
+                });
+            };
+            constexpr int cs = c0 + 2, nbt = (KE - cs + LAM_PIPE - 1) / LAM_PIPE;
+            d2 buf[2][LAM_PIPE];
+            static_for<LAM_PIPE>([&](auto T) {
+                constexpr int c = cs + decltype(T)::value;
+                if constexpr (c < KE) buf[0][decltype(T)::value] = *reinterpret_cast<const d2 *>(Ls[c]);
+            });
+            static_for<nbt>([&](auto Bt) {
+                constexpr int bt = decltype(Bt)::value, cur_b = bt & 1;
+                if constexpr (bt + 1 < nbt) {
+                    static_for<LAM_PIPE>([&](auto T) {
+                        constexpr int c = cs + (bt + 1) * LAM_PIPE + decltype(T)::value;
+                        if constexpr (c < KE) buf[cur_b ^ 1][decltype(T)::value] = *reinterpret_cast<const d2 *>(Ls[c]);
+                    });
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (bt < 3) stage(bt);
+                static_for<LAM_PIPE>([&](auto T) {
+                    constexpr int c = cs + bt * LAM_PIPE + decltype(T)::value;
+                    if constexpr (c < KE) upd(c, buf[cur_b][decltype(T)::value]);
+                });
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            static_for<3>([&](auto St) {
+                if constexpr (decltype(St)::value >= nbt) stage(decltype(St)::value);
+            });
+            pv = np;
+            // keep the trailing update eager: without this hipcc sinks each FMA to the step that
+            // consumes it and keeps the image values live
+            static_for<NB>([&](auto NBc) {
+                constexpr int b = decltype(NBc)::value;
+                if constexpr (b >= cb) {
+                    auto &q = qref(NBc);
+#pragma unroll
+                    for (int c = c0; c < lam_ncol(KE, b); ++c) asm volatile("" : "+v"(q[c]));
+                }
+            });
+        }
+    });
+    // ---- the row's variates (dc:142 zlam, dc:150, dc:170), Plam_j and tau for the epilogue
+    double z[4], G[4], tv[4], pl2[4];
+    const uint32_t dro = (uint32_t)(m * d.P + jj), dk = dro * (uint32_t)d.K;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t di = rv[b] ? dk + l + 8 * b : dk;
+        z[b] = ld.NL[di];
+        G[b] = ld.Gpsi[di];
+        const double p2 = pin[rowoff + l + 8 * b];
+        tv[b] = tau_cur[toff + l + 8 * b];
+        pl2[b] = plam_src ? p2 : p2 * tv[b];
+    }
+    const double Gps = ld.Gps[dro];
+    const double yyj = yy[(uint32_t)(m * d.PP + jj)];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        z[b] = rv[b] ? z[b] : 0.0;
+        G[b] = rv[b] ? G[b] : 0.0;
+        pl2[b] = rv[b] ? pl2[b] : 0.0;
+        tv[b] = rv[b] ? tv[b] : 0.0;
+    }
+    // ---- back solve L' x = w, w = v + z (dc:143-144), pivots (c, c-1) from the bottom:
+    //      x_c = (w_c - sum_{r>c} L[r][c] x_r) / L[c][c], the sums over the group's lanes
+    double x[4] = {0.0, 0.0, 0.0, 0.0};
+    static_for<KE / 2>([&](auto JC) {
+        constexpr int c = KE - 1 - 2 * decltype(JC)::value;     // odd; c and c-1 in block cb
+        constexpr int cb = c / 8;
+        double pa = 0.0, pb = 0.0;
+        static_for<NB>([&](auto NBc) {
+            constexpr int b = decltype(NBc)::value;
+            if constexpr (b >= cb) {   // block cb: rows above c have x = 0 still
+                auto &q = qref(NBc);
+                pa = fma(q[c], x[b], pa);
+                pb = fma(q[c - 1], x[b], pb);
+            }
+        });
+        pa = rowsum8(pa);
+        pb = rowsum8(pb);
+        auto &qc = qref(std::integral_constant<int, cb>{});
+        const d2 vv = *reinterpret_cast<const d2 *>(Vs + c - 1);
+        const d2 iv = *reinterpret_cast<const d2 *>(Is + c - 1);
+        const bool isc = l + 8 * cb == c, isc1 = l + 8 * cb == c - 1;
+        const double xa = (vv.y + z[cb] - pa) * iv.y;
+        x[cb] = isc ? xa : x[cb];
+        const double t = isc ? qc[c - 1] * xa : 0.0;               // L[c][c-1] x_c
+        const double tb = dpp8_d<0x101>(t);                        // row_shl:1: lane c%8 -> c%8 - 1
+        const double xb = (vv.x + z[cb] - pb - tb) * iv.x;
+        x[cb] = isc1 ? xb : x[cb];
+    });
+    // ---- SS_j = yy_j - 2 x.C_j + x'E x (dc:169 by identity, no Y pass).  x = L_Q'^{-1} w, so
+    //      x'Q_j x = |w|^2 and x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j: no E re-read;
+    //      ps_j x.C_j = x.blam = x.(L_Q v) = (L_Q'x).v = w.v: no C re-read.
+    double ww = 0.0, wv = 0.0, px = 0.0;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const double vr = Vs[l + 8 * b < KE ? l + 8 * b : 0];
+        const double w = vr + z[b];
+        ww = rv[b] ? fma(w, w, ww) : ww;
+        wv = rv[b] ? fma(w, vr, wv) : wv;
+        x[b] = rv[b] ? x[b] * isj : 0.0;                           // Lambda_j = L^{-T} w / sqrt(ps_j)
+        px = fma(pl2[b] * x[b], x[b], px);
+    }
+    double contrib = (ww - px - 2.0 * wv) * ipsj;
+    contrib = valid ? contrib : 0.0;
+    contrib = rowsum8(contrib);
+    // ---- psi (dc:150, tau of the previous iteration, Q11) and the outputs
+    if (valid) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int r = l + 8 * b;
+            const double ps_b = rv[b] ? (1.0 / (d.df * 0.5 + 0.5 * (x[b] * x[b] * tv[b]))) * G[b] : 0.0;
+            Lam[rowoff + r] = x[b];
+            cpart[rowoff + r] = ps_b * (x[b] * x[b]);               // mat = psijh .* Lambda.^2 (dc:156)
+            if (rv[b]) psi[rowoff + r] = ps_b;
+        }
+        if (l == 0) {
+            const double SS = yyj + contrib;
+            const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;     // dc:170
+            ps[(uint32_t)(m * d.PP + j)] = psn;
+            omega[(uint32_t)(m * d.PP + j)] = 1.0 / psn;            // dc:171 (Q1)
+        }
+    }
+}
+
 }  // namespace lv
 
 template <class Run>
 void run_variants(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *tau, Run &&run) {
     const dim3 grid((d.P + 7) / 8, d.G);
+    {
+        const size_t row0 = ((size_t)(iter - dr.first_iter) * d.g + d.shard0) * d.P;
+        LamDraws ld{dr.NL + row0 * d.K, dr.Gpsi + row0 * d.K, dr.Gps + row0};
+        if (d.K <= 30)
+            run("n5 staged pivots KE=30", [&] {
+                hipLaunchKernelGGL((lv::k_lam_n5<30>), grid, dim3(64), 0, nullptr, d, b.C, b.E, b.yy, tau, b.Lam,
+                                   b.psi, nullptr, b.ps, b.omega, b.cpart, ld);
+            });
+    }
+    if (getenv("LAM_ONLY_NEW")) return;
     run("n1 (draws from buffers)", [&] {
         hipLaunchKernelGGL(lv::k_lam_n1<0>, grid, dim3(64), 0, nullptr, d, b.C, b.E, b.yy, tau, b.Lam, b.psi,
                            nullptr, b.ps, b.omega, b.cpart, dr, iter);

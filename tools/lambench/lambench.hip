@@ -110,9 +110,9 @@ int main(int argc, char **argv) {
         return o;
     };
     const char *names[5] = {"Lam", "psi", "ps", "omega", "cpart"};
-    // reference: the library kernel, draws in place
+    // reference: the library kernel, variates from the draw buffers
     reset();
-    launch_lambda(d, b, dr, iter, tau, nullptr, nullptr, true);
+    launch_lambda(d, b, dr, iter, tau, nullptr, nullptr, false);
     CK(hipDeviceSynchronize());
     auto ref = outputs();
     hipEvent_t e0, e1;
@@ -147,8 +147,7 @@ int main(int argc, char **argv) {
         fflush(stdout);
     };
     printf("shape g=%d P=%d n=%d K=%d (%d rows)\n", g, P, n, K, g * P);
-    run("lib k_lambda gen=1", [&] { launch_lambda(d, b, dr, iter, tau, nullptr, nullptr, true); });
-    run("lib k_lambda gen=0", [&] { launch_lambda(d, b, dr, iter, tau, nullptr, nullptr, false); });
+    run("lib k_lambda", [&] { launch_lambda(d, b, dr, iter, tau, nullptr, nullptr, false); });
     run_variants(d, b, dr, iter, tau, run);
     return 0;
 }
