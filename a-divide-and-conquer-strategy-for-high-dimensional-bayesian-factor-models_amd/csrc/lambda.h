@@ -135,9 +135,11 @@ __global__ __launch_bounds__(64) void k_lambda(Dims d, const double *__restrict_
     bool rv[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) rv[b] = valid && l + 8 * b < d.K;
-    {   // E_m rows < KE: lane t moves pairs 2t + 128 i
+    {   // E_m rows < 8 NB (every row a lane of the group holds, identity-padding rows >= K included:
+        // E is zero there; an unstaged row would leave stale LDS in registers that the back solve
+        // multiplies by x = 0, and NaN * 0 is NaN): lane t moves pairs 2t + 128 i
         const double *Em = E + (uint32_t)m * KP * KP;
-        constexpr int NI = (KE * KP + 127) / 128;
+        constexpr int NI = (8 * NB * KP + 127) / 128;
         d2 e[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) e[i] = *reinterpret_cast<const d2 *>(Em + 2 * lane + 128 * i);

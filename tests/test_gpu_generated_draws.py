@@ -40,7 +40,7 @@ def _draws(dcfm, seed, n, P, g, K, first, T, hyper):
     return dict(NZ=NZ, NX=NX, NL=NL, Gpsi=Gpsi, Gdelta=Gdelta, Gps=Gps)
 
 
-@pytest.mark.parametrize("n,p,g,K", [(40, 60, 4, 5), (50, 96, 8, 30), (36, 64, 2, 32)])
+@pytest.mark.parametrize("n,p,g,K", [(40, 60, 4, 5), (50, 96, 8, 30), (36, 64, 2, 32), (44, 80, 4, 20), (30, 52, 4, 13)])
 def test_generated_equals_injected_at_the_counters(dcfm, n, p, g, K):
     seed, burnin, mcmc, thin = 77, 1, 3, 1
     N = burnin + mcmc

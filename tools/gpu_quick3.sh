@@ -10,3 +10,7 @@ tail -1 gpurun_out/smoke_$TAG.log
 timeout -k 10 400 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail gpurun_out/bench_$TAG.err; exit 1; }
 timeout -k 10 300 python3 -u bench.py --g 8 --thin 100000 --steps 2000 --warmup 100 --no-cpu-baseline > gpurun_out/bench_${TAG}_g8.json 2> gpurun_out/bench_${TAG}_g8.err || { echo "g8 bench failed"; tail gpurun_out/bench_${TAG}_g8.err; exit 1; }
 python3 tools/show_bench.py gpurun_out/bench_$TAG.json gpurun_out/bench_${TAG}_g8.json
+# kernel trace of the g = 8 share (strong-scaling floor): per-kernel durations vs the iteration
+export TMPDIR=/tmp
+( cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}_g8 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --g 8 --thin 100000 --steps 2000 --warmup 100 --no-cpu-baseline --no-profile --converged-mcmc 0 > $GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}_g8.log 2>&1 ) || { echo "g8 trace failed"; exit 1; }
+echo "g8 trace ok"
