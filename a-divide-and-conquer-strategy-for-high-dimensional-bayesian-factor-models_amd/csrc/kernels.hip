@@ -1300,7 +1300,10 @@ __global__ __launch_bounds__(256) void k_save(Dims d, const double *__restrict__
 // the tiles at c3) start their accumulators FROM the old Sigma values, loaded with the
 // first panel chunk, and stage the row panel scaled by rho / effsamp: the epilogue is
 // plain stores, so the read half of the read-modify-write never waits at the end of the
-// tile.  Tiles with same-shard pairs (and the diagonal) keep the epilogue update.
+// tile.  Tiles with same-shard pairs (and the diagonal) keep the epilogue update.  Sigma is
+// streamed with nontemporal loads / stores (read and written once per flush): it no longer
+// evicts the Lb panels the XCD's co-resident tiles share from L2 (driver flush 1,176 -> 1,137 us;
+// a second register set prefetching the panels two chunks ahead measured no gain).
 // 4 waves in 2x2, each 64x64 = 4x4 tiles of v_mfma_f64_16x16x4.  The k extent
 // (batch x K) runs in chunks of 16 through double-buffered LDS, stored k-major
 // with a 144-double pitch: an MFMA operand read (16 consecutive rows x 4 k) is a
@@ -1356,7 +1359,7 @@ __device__ __forceinline__ void assemble_tile(const Dims &d, const double *__res
 #pragma unroll
             for (int v = 0; v < 4; ++v)
 #pragma unroll
-                for (int g = 0; g < 4; ++g) acc[u][v][g] = St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r];
+                for (int g = 0; g < 4; ++g) acc[u][v][g] = __builtin_nontemporal_load(&St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r]);
     } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -1391,7 +1394,7 @@ __device__ __forceinline__ void assemble_tile(const Dims &d, const double *__res
 #pragma unroll
             for (int v = 0; v < 4; ++v)
 #pragma unroll
-                for (int g = 0; g < 4; ++g) St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r] = acc[u][v][g];
+                for (int g = 0; g < 4; ++g) __builtin_nontemporal_store(acc[u][v][g], &St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r]);
         return;
     }
     // epilogue: lower-triangle read-modify-write of the tile (tile-packed, row-major inside),
@@ -1410,7 +1413,7 @@ __device__ __forceinline__ void assemble_tile(const Dims &d, const double *__res
             for (int v = 0; v < 4; ++v) {
                 const int b = b0 + 16 * v + r;
                 const bool live = a < p && b <= a;
-                old[g][v] = live ? St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r] : 0.0;
+                old[g][v] = live ? __builtin_nontemporal_load(&St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r]) : 0.0;
             }
         }
 #pragma unroll
@@ -1425,7 +1428,7 @@ __device__ __forceinline__ void assemble_tile(const Dims &d, const double *__res
                     const double coef = (sb[v] == sa) ? 1.0 : d.rho;
                     double val = coef * acc[u][v][g] * inv_eff;
                     if (a == b) val += dg;
-                    St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r] = old[g][v] + val;
+                    __builtin_nontemporal_store(old[g][v] + val, &St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r]);
                 }
             }
         }

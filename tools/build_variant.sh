@@ -7,7 +7,7 @@ SRC=a-divide-and-conquer-strategy-for-high-dimensional-bayesian-factor-models_am
 OBJ=build/obj_$NAME
 mkdir -p $OBJ
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -I/opt/rocm/include -Iinclude $*"
-for f in kernels kernels_wide sigma_err dcfm; do
+for f in kernels kernels_wide sigma_err ingest trace init dcfm; do
   hipcc $FLAGS -c $SRC/$f.hip -o $OBJ/$f.o &
 done
 wait

@@ -1,5 +1,5 @@
 """Dev aid: per-phase shader cycles per block of k_lambda_t at the c4 shape (needs the variant
-built with tools/patches/ltphase.py; run with DCFM_LIB=build/libdcfm_ltphase.so)."""
+built from a dev patch (git history: tools/patches/ltphase.py); run with DCFM_LIB=build/libdcfm_ltphase.so)."""
 import ctypes as C
 import sys
 from pathlib import Path

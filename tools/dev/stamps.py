@@ -1,5 +1,5 @@
 """Dev aid: per-role block timelines of one k_wcol launch at c3, or g shards from argv[1] (needs a variant built with
-tools/patches/stamps.py; run with DCFM_LIB=build/libdcfm_stamps.so)."""
+a dev patch (git history: tools/patches/stamps.py); run with DCFM_LIB=build/libdcfm_stamps.so)."""
 import ctypes as C
 import sys
 from pathlib import Path
