@@ -75,6 +75,7 @@ struct dcfm_handle {
     bool fused = false;           // K <= 32 fused launch chain (else the side-stream layout), fixed at create
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
     unsigned long long wc_ops = 0;   // k_wcol launches with the operator roles (hand-off counter epoch)
+    unsigned long long xm_ops = 0;   // k_xdraw launches with the X-operator role (several ranks; its counter's epoch)
     bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
     int lb = 0;                   // Lb buffer being filled
@@ -487,10 +488,11 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     d.inject = (c.flags & DCFM_FLAG_INJECT_DRAWS) ? 1 : 0;
     // K <= 32 runs the fused launch chain unless DCFM_FLAG_UNFUSED asks for the side-stream layout
     h->fused = d.kp == KP && !(c.flags & DCFM_FLAG_UNFUSED);
-    // fused narrow chain on several ranks: column sums and the A sum travel in one message
+    // fused narrow chain on several ranks: column sums, the A sum and the X message travel in
+    // ONE message per iteration (Dims::sgap / xstride)
     const bool packed = nranks > 1 && h->fused;
-    d.sgap = packed ? KP * KP : 0;
-    d.xstride = packed ? d.G * KP + KP * KP : d.kp * d.kp;
+    d.sgap = packed ? KP * KP + d.NP * KP : 0;
+    d.xstride = packed ? d.G * KP + KP * KP + d.NP * KP : d.kp * d.kp;
     h->B = c.asm_batch > 0 ? c.asm_batch : 32;
 
     Bufs &b = h->b;
@@ -513,16 +515,18 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     ALLOC(b.A, G * KP * KP);
     ALLOC(b.ZM, G * 4 * KP * KP);
     ALLOC(b.Sp, G * NP * KP);
-    ALLOC(b.xin, NP * KP);
-    if (nranks > 1) { ALLOC(b.xall, (size_t)nranks * NP * KP); } else b.xall = b.xin;
-    if (d.sgap) {   // packed message [sloc | xa] and its gather (dcfm_internal.h, Dims::sgap)
-        const size_t msg = (size_t)G * KP + KP * KP;
+    if (d.sgap) {   // packed message [sloc | xa | xin] and its gather (dcfm_internal.h, Dims::sgap)
+        const size_t msg = (size_t)d.xstride;
         ALLOC(b.sloc, msg);
         b.xa = b.sloc + (size_t)G * KP;
+        b.xin = b.xa + KP * KP;
         ALLOC(b.msg_all, (size_t)nranks * msg);
         b.sall = b.msg_all;
         b.xa_all = b.msg_all + (size_t)G * KP;
+        b.xall = b.xa_all + KP * KP;
     } else {
+        ALLOC(b.xin, NP * KP);
+        if (nranks > 1) { ALLOC(b.xall, (size_t)nranks * NP * KP); } else b.xall = b.xin;
         ALLOC(b.xa, KP * KP);
         ALLOC(b.xa_all, (size_t)nranks * KP * KP);
     }
@@ -534,7 +538,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         ALLOC(tk, 1);
         b.ticket = reinterpret_cast<unsigned *>(tk);
         double *sy = nullptr;
-        ALLOC(sy, 2 + 256);               // zeroed: the hand-off counters start at 0 (<= 255 chunks)
+        ALLOC(sy, SYNC_ZM + G);           // zeroed: the hand-off counters start at 0 (<= 255 chunks, G shards)
         b.sync = reinterpret_cast<unsigned long long *>(sy);
     }
     ALLOC(b.C, G * PP * KP);
@@ -1061,16 +1065,15 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     const size_t nkg = (size_t)d.g * KW;
     const int64_t end_iter = first_iter + n_iter;
     // K <= 32: the per-shard operators ride in the fused launches on the main stream
-    // (k_wcol, k_zxchol / k_xdraw); K > 32 (or DCFM_NOFUSE=1): prep and the X
-    // operators run on the side stream
+    // (k_wcol, k_xdraw); K > 32 (or DCFM_FLAG_UNFUSED): prep and the X operators run on the
+    // side stream
     const bool fused = h->fused;
     const bool lamgen = fused && !d.inject;   // k_xdraw draws k_lambda's variates (b.ldraw)
     // fused (K <= 32): per iteration t, k_wcol = [Z operators and shard sum of A of t, column
-    // sums of t-1] beside the W pass of t.  One rank: the last chunk also factors Xprec, then
-    // k_zdraw and k_xdraw = [delta chain of t-1] beside the X draw.  Several ranks: the
-    // [column sums | A sum] all-gather, k_zxchol = [X operators, delta chain of t-1] beside the
-    // Z draw, then k_xred, the X message gather and k_xdraw.  The last iteration's chain runs
-    // after the loop (k_delta).
+    // sums of t-1] beside the W pass of t, whose tiles draw Z; one rank: the last chunk also
+    // factors Xprec.  Several ranks: k_xred and ONE all-gather of [column sums | A sum | X
+    // message].  Then k_xdraw = [X operators (several ranks), delta chain of t-1, loading-row
+    // variates of t] beside the X draw.  The last iteration's chain runs after the loop (k_delta).
     const bool wc = fused && d.nranks == 1;
     bool delta_pending = false;           // k_lambda of it - 1 ran, its delta chain not yet queued
     auto after_delta = [&]() {            // iteration it - 1 is complete
@@ -1135,39 +1138,22 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             if (it + batch_n < end_iter && gen_batch(it + batch_n, slot) < 0) return rc_gen;   // next batch
         }
         const DrawsDev &dr = d.inject ? h->dr : h->gen[gen_draws ? slot : 0];
-        if (wc) {
+        if (wc) {   // k_wcol: + the Z draw of the W tiles' rows
+            KTimer t(h, DCFM_K_WPASS, s);
+            h->wc_ops += 1;
+            launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s);
+        } else if (fused) {   // several ranks: k_wcol (W pass + Z draw, no X factorisation), k_xred
+                              // (the local X message), then ONE all-gather of [column sums of it - 1
+                              // | local A sum | X message]; k_xdraw factors Xprec from the ranks' A
+                              // sums, runs the delta chain of it - 1 and draws X
             {
                 KTimer t(h, DCFM_K_WPASS, s);
                 h->wc_ops += 1;
-                launch_wcol(d, b, true, delta_pending, true, h->wc_ops, s);
+                launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s);
             }
-            { KTimer t(h, DCFM_K_ZDRAW, s); launch_zdraw(d, b, dr, it, s); }
-        } else if (fused) {   // several ranks: k_wcol (no X factorisation), ONE all-gather of
-                              // [column sums of it - 1 | local A sum], then k_zxchol = X operators
-                              // + delta chain of it - 1 + Z draw; the X message gather
-            {
-                KTimer t(h, DCFM_K_WPASS, s);
-                h->wc_ops += 1;
-                launch_wcol(d, b, true, delta_pending, true, h->wc_ops, s);
-            }
-            {
-                KTimer t(h, DCFM_K_COMM, s);
-                if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)) return rc;
-            }
-            {
-                KTimer t(h, DCFM_K_ZDRAW, s);
-                if (delta_pending)
-                    launch_zxchol(d, b, dr, it, s, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
-                                  b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1);
-                else
-                    launch_zxchol(d, b, dr, it, s);
-            }
-            HIPC(h, hipGetLastError());
-            if (delta_pending) after_delta();
-            delta_pending = false;
             { KTimer t(h, DCFM_K_XRED, s); launch_xred(d, b, s); }
             KTimer t(h, DCFM_K_COMM, s);
-            if (int rc = coll_allgather(h, CH_MAIN, b.xin, b.xall, (size_t)d.NP * KW, s)) return rc;
+            if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)) return rc;
         } else {
             // side stream: A_m, R_m, Rx from this iteration's incoming Lambda, omega (dc:98-100,112-118)
             HIPC(h, hipStreamWaitEvent(ss, h->e_lam, 0));
@@ -1191,13 +1177,25 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             }
             HIPC(h, hipStreamWaitEvent(s, h->e_xchol, 0));
         }
-        if (wc) {   // + the X factorisation and the delta chain of it - 1
+        if (wc) {   // + the delta chain of it - 1
             KTimer t(h, DCFM_K_XDRAW, s);
             if (delta_pending)
                 launch_xdraw_wc(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
                                 b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, s, lamgen);
             else
                 launch_xdraw_wc(d, b, dr, it, nullptr, nullptr, nullptr, nullptr, 0, s, lamgen);
+            HIPC(h, hipGetLastError());
+            if (delta_pending) after_delta();
+            delta_pending = false;
+        } else if (fused) {   // several ranks: + the X factorisation and the delta chain of it - 1
+            KTimer t(h, DCFM_K_XDRAW, s);
+            h->xm_ops += 1;
+            if (delta_pending)
+                launch_xdraw_mr(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, h->xm_ops, s,
+                                lamgen);
+            else
+                launch_xdraw_mr(d, b, dr, it, nullptr, nullptr, nullptr, nullptr, 0, h->xm_ops, s, lamgen);
             HIPC(h, hipGetLastError());
             if (delta_pending) after_delta();
             delta_pending = false;
@@ -1255,7 +1253,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     }
     if (delta_pending) {   // the last iteration's column sums (+ their gather) and delta chain
         KTimer t(h, DCFM_K_DELTA, s);
-        launch_wcol(d, b, false, true, false, 0, s);
+        launch_wcol(d, b, h->dr, end_iter - 1, false, true, false, 0, s);
         if (d.nranks > 1)
             if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)) return rc;
         const DrawsDev &dr = d.inject ? h->dr : h->gen[0];   // gammas drawn in place unless injected

@@ -10,11 +10,13 @@
 //                        iteration, after which Plam = psi o tau is formed on the fly)
 //   X      [NP][KW]      replicated;    Z [G][NP][KW]
 //   delta, tau [2][g][KW] replicated on every rank, double-buffered per iteration
-//   W      [G][NP][KW]   W_m = Y_m (omega o Lambda_m)                    (k_wpass)
+//   W      [G][NP][KW]   W_m = Y_m (omega o Lambda_m)  (k_wpass; the fused K <= 32 chain keeps it in
+//                        registers: k_wcol draws Z from the W-pass accumulators)
 //   A      [G][KW][KW]   A_m = Lambda_m' diag(omega) Lambda_m             (k_prep)
 //   ZM     [G][4][KW][KW] Z-draw operators {M1, M2, U, NA} of shard m         (k_prep)
-//   Sp     [G][NP][KW]   per-shard X message W_m - sqrt(1-rho) A_m Z_m'   (k_zdraw)
-//   xin    [NP][KW]      local sum over shards of Sp;  xall [nranks][NP][KW] all-gathered (== xin if 1 rank)
+//   Sp     [G][NP][KW]   per-shard X message W_m - sqrt(1-rho) A_m Z_m'   (k_zdraw / k_wcol)
+//   xin    [NP][KW]      local sum over shards of Sp;  xall [nranks][NP][KW] all-gathered (== xin if 1 rank;
+//                        inside the packed message with the fused several-rank chain, Dims::xstride apart)
 //   xa, xa_all [nranks][KW][KW]  per-rank sum of A_m (gathered);  XM [2][KW][KW] X-draw operators {Tx, Ux} (k_xchol)
 //   C      [G][PP][KW]   C_m = Y_m' eta_m  (k_cpass);  E [G][KW][KW] = eta_m' eta_m
 //   cpart  [G][PP][KW]   psi o Lambda^2 per loading row (k_lambda), summed over rows by k_colsum
@@ -57,9 +59,10 @@ struct Dims {
     uint64_t seed;
     int inject;
     // gathered-message layout of the fused several-rank chain: the per-rank message is
-    // [sloc G x KP | sum_m A_m KP x KP] (one all-gather per iteration for both), so rank
-    // r's column sums sit at r * (G*KP + KP*KP) and its A sum at that + G*KP.  sgap = KP*KP
-    // and xstride = G*KP + KP*KP there; sgap = 0, xstride = KW*KW for separate gathers.
+    // [sloc G x KP | sum_m A_m KP x KP | X message NP x KP] (ONE all-gather per iteration), so
+    // rank r's column sums sit at r * xstride, its A sum at that + G*KP and its X message at
+    // that + G*KP + KP*KP.  sgap = KP*KP + NP*KP and xstride = G*KP + KP*KP + NP*KP there;
+    // sgap = 0, xstride = KW*KW for separate gathers.
     int sgap, xstride;
 };
 
@@ -98,7 +101,9 @@ struct Bufs {
     double *xa, *xa_all, *XM;          // per-rank sum of A, gathered sums, X-draw operators
     double *xpart;                     // k_wcol chunk sums of A (xsum_blocks(G) x KP x KP)
     unsigned *ticket;                  // k_wcol last-arrival ticket (0 between launches)
-    unsigned long long *sync;          // hand-off counters (monotonic): [2 + chunk] = k_wcol A_m of the chunk out
+    unsigned long long *sync;          // hand-off counters (monotonic): [0] = k_xdraw XM out (several ranks),
+                                       // [2 + chunk] = k_wcol A_m of the chunk out,
+                                       // [SYNC_ZM + m] = k_wcol Z operators of shard m out
     double *msg_all;                   // packed gather target (fused, nranks > 1), else null
     double *agree;                     // 3 doubles: the failure counts of a collective call (dcfm.hip agree)
     int2 *tiles;
@@ -108,6 +113,9 @@ struct Bufs {
 
 // k_wcol shard sum of A
 constexpr int XSUM_BLOCKS = 8;
+// Bufs::sync: [0] the X operators (k_xdraw, several ranks), [1] spare, [2, 2 + 256) chunk counters of the A sum, [SYNC_ZM, SYNC_ZM + G) the
+// per-shard Z-operator counters (the fused W pass draws Z once its shard's operators are out)
+constexpr int SYNC_ZM = 2 + 256;
 // blocks of the A sum: G / chunk, chunk = a power of two dividing G, grown while more than
 // XSUM_BLOCKS chunks remain — so each chunk is a subtree of the canonical tree (TreeSum) and
 // the tree over the chunk sums is T(0, G).  G <= XSUM_BLOCKS: one block sums every shard
@@ -144,21 +152,23 @@ void launch_prep(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_wpass(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s);
-// fused K <= 32 launches (kernels.hip: k_wcol, k_zxchol, k_xdraw roles)
+// fused K <= 32 launches (kernels.hip: k_wcol, k_xdraw roles)
 // K <= 32: the Z operators + shard sum of A (ops), the previous iteration's column sums
-// (colsum) and the Y pass W (wpass) in one launch (k_wcol); one rank also factors Xprec
-void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_epoch,
-                 hipStream_t s);
-// k_zxchol: X operators from the ranks' gathered A sums (block 0), optionally the delta chain of
-// delta_iter (delta_in != null; column sums from b.sall), and the Z draw tiles
-void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
-                   const double *delta_in = nullptr, const double *tau_in = nullptr, double *delta_out = nullptr,
-                   double *tau_out = nullptr, int64_t delta_iter = 0);
+// (colsum) and the Y pass W with the Z draw of its rows (wpass: Z, Sp; needs ops) in one launch
+// (k_wcol); one rank also factors Xprec
+void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool ops, bool colsum, bool wpass,
+                 unsigned long long ops_epoch, hipStream_t s);
 // one rank, K <= 32: k_xdraw plus, when delta_in != null, the delta chain of delta_iter, and
 // (lamgen) the iteration's loading-row variates into b.ldraw
 void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
                      const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s,
                      bool lamgen);
+// several ranks, K <= 32: k_xdraw with the X operators (block 0, from the ranks' A sums of the
+// packed gather, published through the counter b.sync[0] at xm_epoch), the delta chain of
+// delta_iter (delta_in != null) and the row blocks summing the ranks' X messages
+void launch_xdraw_mr(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
+                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter,
+                     unsigned long long xm_epoch, hipStream_t s, bool lamgen);
 void launch_asum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,

@@ -3,21 +3,21 @@
 // covariance assembly.  fp64 throughout (the reference is double precision).
 //
 // Kernel map (per iteration, in order)                         reference lines
-//   side stream (overlaps k_wpass):
-//   k_prep     A_m = Lambda' diag(w) Lambda (MFMA), R_m = cholcov(I+(1-rho)A_m)  dc:98-100,114-115
-//   k_xchol    Xprec = g I + rho sum_m A_m, Rx = cholcov   [+ RCCL all-gather]  dc:112-118
-//   main stream:
-//   k_wpass    W_m = Y_m (w o Lambda_m)           fp64 MFMA, Y pass 1      dc:102-103,122-123
-//   k_zdraw    Z rows: R\ , R'\ , noise; per-shard (W - s1r A Z')          dc:101-107,121-124
-//   k_xred     sum over local shards                                       dc:120-124
-//   [RCCL all-gather across ranks]
-//   k_xdraw    X rows                                                      dc:119-128
+//   fused chain (K <= 32), one stream:
+//   k_wcol     [Z operators A_m -> M1, M2, U, NA (dc:98-107) | column sums of t-1 (dc:156) |
+//              shard sum of A, one rank: Xprec = g I + rho sum A, Rx (dc:112-118)] beside
+//              the W pass W_m = Y_m (w o Lambda_m) whose tiles draw Z from their registers
+//              and write Z and the shard X message (dc:101-107,121-123)
+//   several ranks: k_xred (local sum of the X messages) + ONE RCCL all-gather of
+//              [column sums | A sum | X message]
+//   k_xdraw    X rows (dc:119-128) [+ several ranks: Xprec, Rx from the ranks' A sums] +
+//              the delta / tau chain of t-1 (dc:155-165) + the loading-row variates of t
 //   k_cpass    C_m = Y_m' eta_m, E_m = eta_m' eta_m  fp64 MFMA, Y pass 2   dc:133,138,141
 //   k_lambda   per loading row: Q, chol, 3 solves, Lambda_j; psi_j;        dc:140-145,150,
-//              SS_j via identity, ps_j, omega_j; column sums of psi o L^2  dc:156,169-171
-//   k_colsum   per-shard column sums                                       dc:156
-//   [RCCL all-gather across ranks]
-//   k_delta    MGP chain (quirks Q4/Q5) for all shards                     dc:155-165
+//              SS_j via identity, ps_j, omega_j; psi o L^2 per row         dc:156,169-171
+//   side-stream layouts (K > 32, DCFM_FLAG_UNFUSED):
+//   k_prep / k_xchol (side stream), k_wpass, k_zdraw, k_xred [+ all-gather], k_xdraw,
+//   k_cpass, k_lambda, k_colsum [+ all-gather], k_delta
 //   (Plam = psi o tau' of dc:175-177 is formed where it is read: in the next
 //    k_lambda, from the psi and tau arrays — the same single product)
 //   saved iterations: k_save; per batch on the assembly stream (overlapping
@@ -50,7 +50,8 @@ namespace dcfm {
 constexpr int PREP_SMEM = 4 * KP * (KP + 1) + 3 * TS16;
 // prep_gram: A_m (to HBM and LDS part[0]), NA, and Zprec's upper triangle into the
 // lower triangle of part[2]; prep_ops: the Z-draw operators from the LDS image.
-// PUB: A_m is published with agent-scope stores (read by other blocks of the same launch, k_wcol)
+// PUB: A_m, NA and (prep_ops) the Z operators are published with agent-scope stores (read by other
+// blocks of the same launch, k_wcol)
 template <bool PUB = false>
 __device__ __forceinline__ void prep_gram(const Dims &d, const double *__restrict__ Lam,
                                           const double *__restrict__ omega, double *__restrict__ A,
@@ -111,7 +112,8 @@ __device__ __forceinline__ void prep_gram(const Dims &d, const double *__restric
         av[u] = (part[0][a][b] + part[1][a][b]) + (part[2][a][b] + part[3][a][b]);
         if (PUB) st_agent(Am + e, av[u]);
         else Am[e] = av[u];
-        Zm[3 * KP * KP + e] = -d.s1r * av[u];                       // NA
+        if (PUB) st_agent(Zm + 3 * KP * KP + e, -d.s1r * av[u]);   // NA
+        else Zm[3 * KP * KP + e] = -d.s1r * av[u];
     }
     __syncthreads();
 #pragma unroll
@@ -140,6 +142,7 @@ __device__ __forceinline__ void prep_load(const Dims &d, const double *__restric
     __syncthreads();
 }
 
+template <bool PUB = false>
 __device__ __forceinline__ void prep_ops(const Dims &d, double *__restrict__ ZM, int m, double *smem) {
     double (*part)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);
     double *lds_l = smem + 4 * KP * (KP + 1), *lds_u = lds_l + 2 * TS16;
@@ -156,8 +159,13 @@ __device__ __forceinline__ void prep_ops(const Dims &d, double *__restrict__ ZM,
         for (int g = 0; g < 4; ++g) {
             const int a = 16 * ti + q + 4 * g, c = 16 * tj + j;
             part[2][a][c] = T[g];
-            Zm[a * KP + c] = d.s1r * T[g];                          // M1
-            Zm[2 * KP * KP + a * KP + c] = part[1][a][c];           // U
+            if (PUB) {
+                st_agent(Zm + a * KP + c, d.s1r * T[g]);
+                st_agent(Zm + 2 * KP * KP + a * KP + c, part[1][a][c]);
+            } else {
+                Zm[a * KP + c] = d.s1r * T[g];                      // M1
+                Zm[2 * KP * KP + a * KP + c] = part[1][a][c];       // U
+            }
         }
     }
     __syncthreads();
@@ -166,7 +174,11 @@ __device__ __forceinline__ void prep_ops(const Dims &d, double *__restrict__ ZM,
         const d4 M = mfma_tile32<false>(part[2], part[0], ti, tj, lane);
         const double s2 = -d.s1r * d.sr;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) Zm[KP * KP + (16 * ti + q + 4 * g) * KP + 16 * tj + j] = s2 * M[g];
+        for (int g = 0; g < 4; ++g) {
+            double *o = Zm + KP * KP + (16 * ti + q + 4 * g) * KP + 16 * tj + j;
+            if (PUB) st_agent(o, s2 * M[g]);
+            else *o = s2 * M[g];
+        }
     }
 }
 
@@ -186,29 +198,30 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 
 // ============================================================================
 // k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA, Y pass 1
-// one wave = (shard m, 16 MT rows i = MT M-tiles) x 32 k (even / odd k N-tiles) of
+// one wave = (shard m, 16 MT rows i = MT M-tiles) x 32 k (even / odd k tiles) of
 // column tile kt (KW/32 tiles, adjacent in the 1-D grid so the wide layouts re-read Y from L2),
 // reduction over j in chunks of 8: lane (r, q) holds Y[i0+r][8t+2q .. +1] (16 B);
-// k-step 2t uses element 0, 2t+1 element 1; the B operand (w_j L[j][2r], w_j L[j][2r+1])
-// uses the same j <-> (q, e) map.  Register prefetch 3 chunks ahead (ring of 4).
+// k-step 2t uses element 0, 2t+1 element 1; the (w_j L[j][2r], w_j L[j][2r+1]) values use the
+// same j <-> (q, e) map.  The product is formed transposed, W' = (w o L)' Y' (the Lambda values
+// the A operand, Y the B operand: the same products in the same order per element), so lane
+// (r, q) ends with W[i0 + 16a + r][8g + 2q + tb] in acc[a][tb][g] — row = lane & 15, the layout
+// the Z draw takes its W operand in (zdraw_rows; k_wcol draws Z from these registers).
+// Register prefetch 3 chunks ahead (ring of 4).
 // MT = 1 (64-row blocks, twice the blocks) where the launch would not fill the chip (a few
 // shards per rank): each element's reduction order is the same for both, so the choice
 // changes no bit of W.
 // ============================================================================
-template <int KW, int MT = 2>
-__device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restrict__ Y,
-                                           const double *__restrict__ Lam, const double *__restrict__ omega,
-                                           double *__restrict__ W, int w, int kt) {
-    const int nrb = d.NP / (64 * MT);                // row blocks per shard
-    const int m = w / nrb, rb = w % nrb;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int i0 = rb * 64 * MT + wave * 16 * MT;
+// pre() runs once the first three chunks' loads are issued (VALU work hidden behind their latency)
+template <int KW, int MT, class Pre>
+__device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restrict__ Y, const double *__restrict__ Lam,
+                                          const double *__restrict__ omega, int m, int i0, int kt, d4 (&acc)[MT][2],
+                                          Pre &&pre) {
+    const int lane = threadIdx.x & 63;
     const int r = lane & 15, q = lane >> 4;
     const double *Y0 = Y + ((size_t)m * d.NP + i0 + r) * d.PP + 2 * q;
     const double *Y1 = Y0 + (size_t)16 * (MT - 1) * d.PP;
     const double *L = Lam + (size_t)m * d.PP * KW + 32 * kt + 2 * r;
     const double *wp = omega + (size_t)m * d.PP + 2 * q;
-    d4 acc[MT][2];
 #pragma unroll
     for (int a = 0; a < MT; ++a)
 #pragma unroll
@@ -228,17 +241,17 @@ __device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restri
     {                                                                               \
         const double b00 = ww.x * l0.x, b01 = ww.x * l0.y;                          \
         const double b10 = ww.y * l1.x, b11 = ww.y * l1.y;                          \
-        acc[0][0] = mfma16x16x4(y0.x, b00, acc[0][0]);                              \
-        acc[0][1] = mfma16x16x4(y0.x, b01, acc[0][1]);                              \
+        acc[0][0] = mfma16x16x4(b00, y0.x, acc[0][0]);                              \
+        acc[0][1] = mfma16x16x4(b01, y0.x, acc[0][1]);                              \
         if (MT == 2) {                                                              \
-            acc[MT - 1][0] = mfma16x16x4(y1.x, b00, acc[MT - 1][0]);                \
-            acc[MT - 1][1] = mfma16x16x4(y1.x, b01, acc[MT - 1][1]);                \
+            acc[MT - 1][0] = mfma16x16x4(b00, y1.x, acc[MT - 1][0]);                \
+            acc[MT - 1][1] = mfma16x16x4(b01, y1.x, acc[MT - 1][1]);                \
         }                                                                           \
-        acc[0][0] = mfma16x16x4(y0.y, b10, acc[0][0]);                              \
-        acc[0][1] = mfma16x16x4(y0.y, b11, acc[0][1]);                              \
+        acc[0][0] = mfma16x16x4(b10, y0.y, acc[0][0]);                              \
+        acc[0][1] = mfma16x16x4(b11, y0.y, acc[0][1]);                              \
         if (MT == 2) {                                                              \
-            acc[MT - 1][0] = mfma16x16x4(y1.y, b10, acc[MT - 1][0]);                \
-            acc[MT - 1][1] = mfma16x16x4(y1.y, b11, acc[MT - 1][1]);                \
+            acc[MT - 1][0] = mfma16x16x4(b10, y1.y, acc[MT - 1][0]);                \
+            acc[MT - 1][1] = mfma16x16x4(b11, y1.y, acc[MT - 1][1]);                \
         }                                                                           \
     }
     // ring of 4 register buffers: chunk t + 3 is requested while chunk t multiplies, so three
@@ -247,6 +260,7 @@ __device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restri
     WP_LOAD(0, yA0, yA1, wA, lA0, lA1);
     if (1 < nch) WP_LOAD(1, yB0, yB1, wB, lB0, lB1);
     if (2 < nch) WP_LOAD(2, yC0, yC1, wC, lC0, lC1);
+    pre();
     for (int t = 0; t < nch; t += 4) {
         if (t + 3 < nch) WP_LOAD(t + 3, yD0, yD1, wD, lD0, lD1);
         WP_MMA(yA0, yA1, wA, lA0, lA1);
@@ -259,16 +273,29 @@ __device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restri
     }
 #undef WP_LOAD
 #undef WP_MMA
-    // D row = q + 4g (row i), col = r (k = 2r + tb)
+}
+
+template <int KW, int MT = 2>
+__device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restrict__ Y,
+                                           const double *__restrict__ Lam, const double *__restrict__ omega,
+                                           double *__restrict__ W, int w, int kt) {
+    const int nrb = d.NP / (64 * MT);                // row blocks per shard
+    const int m = w / nrb, rb = w % nrb;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int i0 = rb * 64 * MT + wave * 16 * MT;
+    const int r = lane & 15, q = lane >> 4;
+    d4 acc[MT][2];
+    wpass_acc<KW, MT>(d, Y, Lam, omega, m, i0, kt, acc, [] {});
+    // acc[a][tb][g] = W[i0 + 16a + r][32 kt + 8g + 2q + tb]: one 16-byte pair per (a, g)
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
-        double *Wt = W + ((size_t)m * d.NP + i0 + 16 * a) * KW + 32 * kt + 2 * r;
+        double *Wt = W + ((size_t)m * d.NP + i0 + 16 * a + r) * KW + 32 * kt + 2 * q;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             d2 v;
             v.x = acc[a][0][g];
             v.y = acc[a][1][g];
-            *reinterpret_cast<d2 *>(Wt + (size_t)(q + 4 * g) * KW) = v;
+            *reinterpret_cast<d2 *>(Wt + 8 * g) = v;
         }
     }
 }
@@ -296,6 +323,99 @@ __global__ __launch_bounds__(256) void k_wpass(Dims d, const double *__restrict_
 // ============================================================================
 constexpr int ZDRAW_SMEM = 4 * KP * (KP + 1);
 constexpr int ZROWS = 128, ZTHREADS = 512;     // rows and threads per k_zdraw block
+
+// The draw of 16 rows from the operand registers — lane (c, q) holds row i = (its tile's row c):
+// wv[t] = W[i][8t+2q .. +1], xv[t] = X[i][..], ev[t] = eps[i][..] (k-steps 2t + e) — and the
+// shard's operators Ms = {M1, M2, U, NA} in LDS.  The S' = W' + NA Z' product takes its A rows
+// in the order pi(16 mt + c) = 8 (c >> 2) + 2 (c & 3) + mt, so its C/D registers hold exactly the
+// features of wv (the accumulators start from W without a reload, and a lane stores S_i[8g+2q ..
+// +1] as one 16-byte pair); every element keeps its products and their order, so the values
+// are those of the unpermuted product.  Shared by k_zdraw (W from HBM) and k_wcol's
+// fused W pass (W' still in the W-pass accumulators), which therefore give the same bits.
+__device__ __forceinline__ void zdraw_rows(const Dims &d, const double (*Ms)[KP][KP + 1], const d2 (&wv)[4],
+                                           const d2 (&xv)[4], const d2 (&ev)[4], double *__restrict__ Zr,
+                                           double *__restrict__ Sr, bool live, int c, int q) {
+    d4 zw[2], zx[2], ze[2], as[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) zw[mt] = zx[mt] = ze[mt] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        double mo[2][3][2];   // this chunk's operator values, read before its 12 MFMAs
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int mat = 0; mat < 3; ++mat)
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) mo[e][mat][mt] = Ms[mat][16 * mt + c][8 * t + 2 * q + e];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const double we = e ? wv[t].y : wv[t].x, xe = e ? xv[t].y : xv[t].x;
+            const double ee = e ? ev[t].y : ev[t].x;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                zw[mt] = mfma16x16x4(mo[e][0][mt], we, zw[mt]);
+                zx[mt] = mfma16x16x4(mo[e][1][mt], xe, zx[mt]);
+                ze[mt] = mfma16x16x4(mo[e][2][mt], ee, ze[mt]);
+            }
+        }
+    }
+    d4 az[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+        az[mt] = (zw[mt] + zx[mt]) + ze[mt];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) as[mt][g] = mt ? wv[g].y : wv[g].x;     // W[i][8g + 2q + mt]
+    }
+    // S' = W' + NA Z' (rows of NA in the order pi)
+    const int prow = 8 * (c >> 2) + 2 * (c & 3);
+#pragma unroll
+    for (int mt2 = 0; mt2 < 2; ++mt2)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int kk = 16 * mt2 + 4 * g + q;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) as[mt] = mfma16x16x4(Ms[3][prow + mt][kk], az[mt2][g], as[mt]);
+        }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int k = 16 * mt + q + 4 * g;
+            if (live) Zr[k] = (k < d.K) ? az[mt][g] : 0.0;
+        }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        d2 v;
+        v.x = live ? as[0][g] : 0.0;
+        v.y = live ? as[1][g] : 0.0;
+        *reinterpret_cast<d2 *>(Sr + 8 * g + 2 * q) = v;
+    }
+}
+// eps[i][kk], kk = 8t + 2q + e of the Z draw (dc:104 normrnd): the injected draw buffer, or
+// generated here — Philox pair 4t + q of (SITE_Z, shard, row i) = normals kk, kk + 1
+__device__ __forceinline__ void z_eps(const Dims &d, const DrawsDev &dr, int64_t iter, int mg, int i, bool live, int q,
+                                      d2 (&ev)[4]) {
+    if (d.inject) {
+        const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int kk = 8 * t + 2 * q;
+            ev[t].x = (live && kk < d.K) ? nz[kk] : 0.0;
+            ev[t].y = (live && kk + 1 < d.K) ? nz[kk + 1] : 0.0;
+        }
+    } else {
+        const Rng rng(d.seed);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int kk = 8 * t + 2 * q;
+            double n0 = 0.0, n1 = 0.0;
+            if (live && kk < d.K) rng.normal2(SITE_Z, (uint32_t)mg, (uint32_t)i, (uint32_t)(4 * t + q), (uint32_t)iter, n0, n1);
+            ev[t].x = n0;
+            ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
+        }
+    }
+}
+
 // ZT threads = ZT / 4 rows per block: 256 (64-row blocks) where 128-row ones would leave CUs
 // idle (a few shards per rank); rows are independent, so the choice changes no bit
 template <int ZT = ZTHREADS>
@@ -330,33 +450,7 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
 #pragma unroll
         for (int u = 0; u < NU; ++u) zv[u] = Zm[threadIdx.x + ZT * u];
     }
-    if (d.inject) {   // eps[i][kk], kk = 8t + 2q + e   (dc:104 normrnd; injected draw buffer)
-        const double *nz = dr.NZ + (((size_t)(iter - dr.first_iter) * d.g + mg) * d.n + (live ? i : 0)) * d.K;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int kk = 8 * t + 2 * q;
-            ev[t].x = (live && kk < d.K) ? nz[kk] : 0.0;
-            ev[t].y = (live && kk + 1 < d.K) ? nz[kk + 1] : 0.0;
-        }
-    } else {          // generated here: Philox pair 4t + q of (SITE_Z, shard, row i) = normals kk, kk + 1
-        const Rng rng(d.seed);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int kk = 8 * t + 2 * q;
-            double n0 = 0.0, n1 = 0.0;
-            if (live && kk < d.K) rng.normal2(SITE_Z, (uint32_t)mg, (uint32_t)i, (uint32_t)(4 * t + q), (uint32_t)iter, n0, n1);
-            ev[t].x = n0;
-            ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
-        }
-    }
-    double wr[2][4];   // W in the C/D layout (row = q + 4g of tile mt): the S' accumulator's start
-    {
-        const double *Wr = W + ((size_t)m * d.NP + i) * KP;
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) wr[mt][g] = Wr[16 * mt + q + 4 * g];
-    }
+    z_eps(d, dr, iter, mg, i, live, q, ev);
     {
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
@@ -366,56 +460,7 @@ __device__ __forceinline__ void zdraw_tile(const Dims &d, const double *__restri
         }
     }
     __syncthreads();
-    d4 zw[2], zx[2], ze[2], as[2];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) zw[mt] = zx[mt] = ze[mt] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        double mo[2][3][2];   // this chunk's operator values, read before its 12 MFMAs
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-#pragma unroll
-            for (int mat = 0; mat < 3; ++mat)
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) mo[e][mat][mt] = Ms[mat][16 * mt + c][8 * t + 2 * q + e];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const double we = e ? wv[t].y : wv[t].x, xe = e ? xv[t].y : xv[t].x;
-            const double ee = e ? ev[t].y : ev[t].x;
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                zw[mt] = mfma16x16x4(mo[e][0][mt], we, zw[mt]);
-                zx[mt] = mfma16x16x4(mo[e][1][mt], xe, zx[mt]);
-                ze[mt] = mfma16x16x4(mo[e][2][mt], ee, ze[mt]);
-            }
-        }
-    }
-    d4 az[2];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-        az[mt] = (zw[mt] + zx[mt]) + ze[mt];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) as[mt][g] = wr[mt][g];
-    }
-    // S' = W' + NA Z'
-#pragma unroll
-    for (int mt2 = 0; mt2 < 2; ++mt2)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int kk = 16 * mt2 + 4 * g + q;
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) as[mt] = mfma16x16x4(Ms[3][16 * mt + c][kk], az[mt2][g], as[mt]);
-        }
-    double *Zr = Z + ((size_t)m * d.NP + i) * KP;
-    double *Sr = Sp + ((size_t)m * d.NP + i) * KP;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int k = 16 * mt + q + 4 * g;
-            if (live) Zr[k] = (k < d.K) ? az[mt][g] : 0.0;
-            Sr[k] = live ? as[mt][g] : 0.0;
-        }
+    zdraw_rows(d, Ms, wv, xv, ev, Z + ((size_t)m * d.NP + i) * KP, Sp + ((size_t)m * d.NP + i) * KP, live, c, q);
 }
 
 // ZT = 256 holds twice the operator staging registers per thread: 2 waves per SIMD (it runs
@@ -673,7 +718,7 @@ struct DeltaArgs {
 // idle; the row blocks sum their messages first and wait for XM only before the MFMAs.
 constexpr int XD_SMEM = (2 * KP * (KP + 1) + 4 * 4 * 64 * 2) > XCHOL_SMEM ? (2 * KP * (KP + 1) + 4 * 4 * 64 * 2)
                                                                           : XCHOL_SMEM;
-__global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict__ src, int nsrc,
+__global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict__ src, int nsrc, size_t sstride,
                                                 double *__restrict__ XM,
                                                 double *__restrict__ X, DrawsDev dr, int64_t iter, int xroles,
                                                 const double *__restrict__ xa, unsigned long long *xm_ctr,
@@ -690,7 +735,8 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
     }
     if (xroles & 1) {   // producer of XM
         if (blk == 0) {
-            for (int e = threadIdx.x; e < KP * KP; e += 1024) xprec_store(d, smem, e, xa[e]);
+            for (int e = threadIdx.x; e < KP * KP; e += 1024)   // several ranks: their sums, canonical tree
+                xprec_store(d, smem, e, d.nranks > 1 ? tree_sum(xa + e, d.nranks, (size_t)d.xstride) : xa[e]);
             __syncthreads();
             xchol_factor<true>(d, XM, smem);
             signal_count(xm_ctr);
@@ -714,7 +760,7 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
     const int tw = w & 3, sw = w >> 2;                 // column group, source chunk
     const int i0 = blk * 16, i = i0 + c;
     const bool live = i < d.n;
-    const size_t stride = (size_t)d.NP * KP;
+    const size_t stride = sstride;
     int nch, chunk;
     xdraw_chunks(nsrc, nch, chunk);     // chunk < 1024 (TreeSum levels below); dcfm_create caps g
     d2 sv[4], ev[4];
@@ -1087,7 +1133,7 @@ __global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__
 // Fused single-stream launches (K <= 32).  Cross-stream event hand-offs cost ~6 us each
 // on the critical path, and latency-bound work slows ~2x when it shares CUs with the
 // MFMA-bound Y passes, so the small per-shard K x K work rides in the launches of the
-// Y passes (k_wcol, k_zxchol, k_xdraw) as extra roles (dcfm_run names the plan).
+// Y passes (k_wcol, k_xdraw) as extra roles (dcfm_run names the plan).
 // ============================================================================
 // The chunk sums are handed to the last arrival with agent-scope relaxed atomics (sc1:
 // coherent across the XCDs' L2s without write-back / invalidate), ordered by the stores'
@@ -1109,36 +1155,6 @@ __device__ __forceinline__ bool last_arrival(unsigned *ticket, unsigned count, d
     return last;
 }
 
-constexpr int ZX_SMEM = ZDRAW_SMEM > XCHOL_SMEM ? ZDRAW_SMEM : XCHOL_SMEM;
-// block 0: the X operators from the ranks' shard sums of A (several ranks, fused chain);
-// blocks [1, 1 + ndel): the previous iteration's delta / tau chain from the gathered column
-// sums (ZT / 64 shards per block, one wave each), beside the Z pass; the rest: k_zdraw tiles
-// (ZT as k_zdraw: 256 where 128-row tiles would leave CUs idle)
-template <int ZT>
-__global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(ZT == ZTHREADS ? 4 : 2))) void k_zxchol(
-        Dims d, const double *__restrict__ W, const double *__restrict__ ZM, const double *__restrict__ X,
-        double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr, int64_t iter,
-        const double *__restrict__ xa_all, double *__restrict__ XM, int ndel, const double *__restrict__ sall,
-        DeltaArgs da) {
-    __shared__ double smem[ZX_SMEM];
-    const int blk = blockIdx.x;
-    if (blk > ndel) {
-        zdraw_tile<ZT>(d, W, ZM, X, Z, Sp, dr, iter, xcd_remap(blk - 1 - ndel, gridDim.x - 1 - ndel), smem);
-        return;
-    }
-    if (blk > 0) {
-        const int m = (blk - 1) * (ZT / 64) + (threadIdx.x >> 6);
-        if (m < d.g)
-            delta_shard(d, sall, da.delta_in, da.tau_in, da.delta_out, da.tau_out, dr, da.iter, m, threadIdx.x & 63);
-        return;
-    }
-    for (int e = threadIdx.x; e < KP * KP; e += ZT) {   // the ranks' shard sums, canonical tree
-        xprec_store(d, smem, e, tree_sum(xa_all + e, d.nranks, (size_t)d.xstride));
-    }
-    __syncthreads();
-    xchol_factor(d, XM, smem);
-}
-
 // ============================================================================
 // k_wcol (one rank, K <= 32): the small per-iteration work that feeds the Z / X draws rides
 // in the Y pass's launch.  As separate launches these latency-bound pieces (K x K
@@ -1149,10 +1165,10 @@ __global__ __launch_bounds__(ZT) __attribute__((amdgpu_waves_per_eu(ZT == ZTHREA
 //   OPS    [0, G)      prep_shard(m): A_m (published agent-coherent) and the Z operators ZM_m
 //                      of THIS iteration (from the incoming Lambda, omega)           dc:98-107
 //   COLSUM [.., +G)    column sums of the PREVIOUS iteration's psi o Lambda^2 (dc:156) for
-//                      the delta chain, which runs in the next launch (k_zxchol)
+//                      the delta chain, which runs in the next launch (k_xdraw)
 //   OPS    [.., +nxs)  wait for every A_m; chunk j's tree sum (a canonical subtree) -> xpart;
 //                      the last arrival sums the chunks (canonical tree) into xa (dc:117);
-//                      k_zxchol's block 0 factors Xprec                              dc:112-118
+//                      (several ranks: k_xdraw's block 0 factors Xprec from the ranks' sums) dc:112-118
 //   WPASS  [.., +nw)   W_m = Y_m (w o Lambda_m) tiles                          dc:102-103,122-123
 // Hand-off: payload by agent-scope stores, s_waitcnt vmcnt(0), then a relaxed fetch-add on a
 // monotonic 64-bit counter; consumers poll it (s_sleep) up to the launch's target and read
@@ -1164,8 +1180,68 @@ __device__ __forceinline__ double tree8(const double (&v)[8]) {
     return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
 }
 
-__global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsum, int wpass,
-                                              unsigned long long ops_epoch, int xchol) {
+// k_wcol's W pass with the Z draw of its rows (fused chain, K <= 32; dc:101-107,121-123): the
+// wave's W' tile stays in the accumulators (wpass_acc) and feeds zdraw_rows directly — no W
+// round trip through HBM and no k_zdraw launch.  The rows' normals are drawn while the first Y
+// chunks are in flight; the shard's operators come from its OPS block of the same launch
+// (agent-scope stores, counter SYNC_ZM + m, epoch = the launch's ops epoch), staged once per
+// block in LDS after the pass.
+template <int MT>
+__device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, int w,
+                                             unsigned long long zm_epoch, double *smem) {
+    double (*Ms)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);   // M1, M2, U, NA
+    const int nrb = d.NP / (64 * MT);
+    const int m = w / nrb, rb = w % nrb;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = lane & 15, q = lane >> 4;
+    const int mg = d.shard0 + m;
+    const int i0 = rb * 64 * MT + wave * 16 * MT;
+    d4 acc[MT][2];
+    wpass_acc<KP, MT>(d, b.Y, b.Lam, b.omega, m, i0, 0, acc, [] {});
+    // the operators are normally out long before the pass ends; their loads and the rows' X are
+    // issued first, the first tile's normals drawn while they are in flight
+    wait_count(b.sync + SYNC_ZM + m, zm_epoch);
+    constexpr int NU = 4 * KP * KP / 256;
+    double zv[NU];
+    {
+        const double *Zm = b.ZM + (size_t)m * 4 * KP * KP;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) zv[u] = ld_agent(Zm + threadIdx.x + 256 * u);
+    }
+    d2 xv[MT][4], ev[MT][4];
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+        const double *Xi = b.X + (size_t)(i0 + 16 * a + c) * KP + 2 * q;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) xv[a][t] = *reinterpret_cast<const d2 *>(Xi + 8 * t);
+    }
+    z_eps(d, dr, iter, mg, i0 + c, i0 + c < d.n, q, ev[0]);   // tile 1's after tile 0's draw (registers)
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int e = threadIdx.x + 256 * u;
+        const int mat = e / (KP * KP), rem = e % (KP * KP);
+        Ms[mat][rem / KP][rem % KP] = zv[u];
+    }
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+        const int i = i0 + 16 * a + c;
+        if (a > 0) z_eps(d, dr, iter, mg, i, i < d.n, q, ev[a]);
+        d2 wv[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            wv[g].x = acc[a][0][g];
+            wv[g].y = acc[a][1][g];
+        }
+        zdraw_rows(d, Ms, wv, xv[a], ev[a], b.Z + ((size_t)m * d.NP + i) * KP, b.Sp + ((size_t)m * d.NP + i) * KP,
+                   i < d.n, c, q);
+        __builtin_amdgcn_sched_barrier(0);   // one tile's draw at a time (registers)
+    }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_wcol(Dims d, Bufs b, DrawsDev dr, int64_t iter, int ops, int colsum,
+                                              int wpass, unsigned long long ops_epoch, int xchol) {
     __shared__ double smem[PREP_SMEM];
     const int G = d.G, nxs = xsum_blocks(G), chunk = G / nxs;
     unsigned long long *chunk_ctr = b.sync + 2;   // per chunk of shards: A_m published
@@ -1174,7 +1250,8 @@ __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsu
         if (blk < G) {
             prep_gram<true>(d, b.Lam, b.omega, b.A, b.ZM, blk, smem);
             signal_count(chunk_ctr + blk / chunk);   // A_m is out; the operators follow
-            prep_ops(d, b.ZM, blk, smem);
+            prep_ops<true>(d, b.ZM, blk, smem);
+            signal_count(b.sync + SYNC_ZM + blk);    // the Z operators are out (the W tiles draw Z)
             return;
         }
         blk -= G;
@@ -1262,10 +1339,10 @@ __global__ __launch_bounds__(256) void k_wcol(Dims d, Bufs b, int ops, int colsu
         }
         blk -= nxs;
     }
-    if (wpass) {   // 1: 128-row blocks, 2: 64-row blocks (wcol_wpass_mode)
+    if (wpass) {   // 1: 128-row blocks, 2: 64-row blocks (wcol_wpass_mode); W' -> the Z draw
         const int nw = gridDim.x - (int)(blockIdx.x - blk);
-        if (wpass == 2) wpass_tile<KP, 1>(d, b.Y, b.Lam, b.omega, b.W, xcd_remap(blk, nw), 0);
-        else wpass_tile<KP, 2>(d, b.Y, b.Lam, b.omega, b.W, xcd_remap(blk, nw), 0);
+        if (wpass == 2) wpass_z_tile<1>(d, b, dr, iter, xcd_remap(blk, nw), ops_epoch, smem);
+        else wpass_z_tile<2>(d, b, dr, iter, xcd_remap(blk, nw), ops_epoch, smem);
     }
 }
 
@@ -1548,33 +1625,14 @@ void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
                            b.Sp, dr, iter);
 }
 // k_wcol launch (K <= 32)
-void launch_wcol(const Dims &d, const Bufs &b, bool ops, bool colsum, bool wpass, unsigned long long ops_epoch,
-                 hipStream_t s) {
+void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool ops, bool colsum, bool wpass,
+                 unsigned long long ops_epoch, hipStream_t s) {
     // W pass tiles: 64-row blocks while 128-row blocks would leave CUs idle
     const int wmode = (d.NP / 128) * d.G < 256 ? 2 : 1;
     const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / (64 * (3 - wmode))) * d.G : 0);
     if (nb == 0) return;
-    hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, ops ? 1 : 0, colsum ? 1 : 0, wpass ? wmode : 0,
-                       ops_epoch, d.nranks == 1 ? 1 : 0);
-}
-void launch_zxchol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
-                   const double *delta_in, const double *tau_in, double *delta_out, double *tau_out,
-                   int64_t delta_iter) {
-    if (d.kp != KP) return;
-    // delta blocks (zw shards each) padded so that the zdraw tiles' first block sits on XCD 0 (xcd_remap)
-    const bool small = (d.NP / ZROWS) * d.G < 256;   // 64-row tiles (k_zdraw)
-    const int zw = small ? 4 : ZTHREADS / 64;
-    const int ndel = delta_in ? ((d.g + zw - 1) / zw + 1 + 7) / 8 * 8 - 1 : 0;
-    DeltaArgs da;
-    da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
-    da.iter = delta_iter;
-    const double *xs = d.nranks > 1 ? b.xa_all : b.xa;
-    if (small)
-        hipLaunchKernelGGL(k_zxchol<256>, dim3(1 + ndel + (d.NP / 64) * d.G), dim3(256), 0, s, d, b.W, b.ZM, b.X, b.Z,
-                           b.Sp, dr, iter, xs, b.XM, ndel, b.sall, da);
-    else
-        hipLaunchKernelGGL(k_zxchol<ZTHREADS>, dim3(1 + ndel + (d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM,
-                           b.X, b.Z, b.Sp, dr, iter, xs, b.XM, ndel, b.sall, da);
+    hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, dr, iter, ops ? 1 : 0, colsum ? 1 : 0,
+                       wpass ? wmode : 0, ops_epoch, d.nranks == 1 ? 1 : 0);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
     const int total = d.NP * d.kp;
@@ -1598,11 +1656,12 @@ void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
     DeltaArgs da = {};
     const LamGen lg = lam_gen_of(d, b, lamgen);
     const dim3 grid(cdiv(d.n, 16) + lg.b_total);
+    const size_t st = (size_t)d.NP * KP;
     if (from_shards)   // one rank: sum the G shard messages here (no k_xred)
-        hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X, dr, iter, 0,
+        hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.Sp, d.G, st, b.XM, b.X, dr, iter, 0,
                            nullptr, nullptr, 0ull, 0, nullptr, da, lg);
     else
-        hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.xall, d.nranks, b.XM, b.X, dr,
+        hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.xall, d.nranks, st, b.XM, b.X, dr,
                            iter, 0, nullptr, nullptr, 0ull, 0, nullptr, da, lg);
 }
 void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
@@ -1613,8 +1672,21 @@ void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t i
     da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
     da.iter = delta_iter;
     const LamGen lg = lam_gen_of(d, b, lamgen);
-    hipLaunchKernelGGL(k_xdraw, dim3(ndel + cdiv(d.n, 16) + lg.b_total), dim3(1024), 0, s, d, b.Sp, d.G, b.XM, b.X,
-                       dr, iter, delta_in ? 2 : 0, nullptr, nullptr, 0ull, ndel, b.sall, da, lg);
+    hipLaunchKernelGGL(k_xdraw, dim3(ndel + cdiv(d.n, 16) + lg.b_total), dim3(1024), 0, s, d, b.Sp, d.G,
+                       (size_t)d.NP * KP, b.XM, b.X, dr, iter, delta_in ? 2 : 0, nullptr, nullptr, 0ull, ndel, b.sall,
+                       da, lg);
+}
+void launch_xdraw_mr(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
+                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter,
+                     unsigned long long xm_epoch, hipStream_t s, bool lamgen) {
+    const int ndel = delta_in ? (d.g + 15) / 16 : 0;
+    DeltaArgs da;
+    da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
+    da.iter = delta_iter;
+    const LamGen lg = lam_gen_of(d, b, lamgen);
+    hipLaunchKernelGGL(k_xdraw, dim3(1 + ndel + cdiv(d.n, 16) + lg.b_total), dim3(1024), 0, s, d, b.xall, d.nranks,
+                       (size_t)d.xstride, b.XM, b.X, dr, iter, 1 | (delta_in ? 2 : 0), b.xa_all, b.sync, xm_epoch,
+                       ndel, b.sall, da, lg);
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(((d.PP + d.kp) / 32) * d.G * (d.kp / 32));

@@ -43,9 +43,14 @@ def synth_data(n, p, k0=10, sparsity=0.7, seed=20161209, factors=False):
     return (Y, L0, sig2) if factors else Y
 
 
-def algorithmic_work(kname, d, n_launch_samples):
-    """(flops, bytes, bound) per launch — the minimum the reference maths needs."""
+def algorithmic_work(kname, d, n_launch_samples, fused_z=False):
+    """(flops, bytes, bound) per launch — the minimum the reference maths needs.  fused_z: the
+    K <= 32 fused chain's W pass also draws Z (k_wcol: W stays in registers; read X, write Z
+    and the X message instead of writing W)."""
     n, P, K, G, p, nr = d["n"], d["P"], d["K"], d["G"], d["p"], d["nranks"]
+    if kname == "k_wpass" and fused_z:
+        return (2.0 * G * n * P * K + G * n * (4.0 * K * K + 2.0 * K * K),
+                8.0 * (G * n * P + G * P * (K + 1) + n * K + 2 * G * n * K), "hbm")
     if kname == "k_wpass":     # W_m = Y_m (w o L_m): one fp64 read of Y, L, w; write W
         return 2.0 * G * n * P * K, 8.0 * (G * n * P + G * P * (K + 1) + G * n * K), "hbm"
     if kname == "k_cpass":     # [C|E] = [Y|eta]' eta: read Y, X, Z; write C, E
@@ -391,13 +396,14 @@ def main():
     d = {"n": n, "P": P, "K": K, "G": gl, "p": p, "nranks": shard_ranks}
     kern = {}
     roof = None
+    fused_z = K <= 32 and "k_wpass" in stats and "k_zdraw" not in stats
     def work_of(name, cnt, saved, iters):
         """Algorithmic (flops, bytes, bound) per launch: per-iteration work spread over the
         launches of one iteration (the Y-pass / row kernels run as two shard groups)."""
         if name == "k_assemble":
             fl, by, _ = algorithmic_work(name, d, saved / max(cnt, 1))
             return fl, by, binding_roof(fl, by)
-        fl, by, _ = algorithmic_work(name, d, 0)
+        fl, by, _ = algorithmic_work(name, d, 0, fused_z)
         per_iter = max(cnt, 1) / max(iters, 1)
         return fl / per_iter, by / per_iter, binding_roof(fl, by)
 
