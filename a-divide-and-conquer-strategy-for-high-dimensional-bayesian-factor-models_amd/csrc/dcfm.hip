@@ -274,8 +274,10 @@ static hipEvent_t get_event(dcfm_handle *h) {
         h->evpool.pop_back();
         return e;
     }
+    // timing only (read after sync_all): no system-scope fence, whose L2 write-back and
+    // invalidate per record cost microseconds and slowed the kernel that followed
     hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
     return e;
 }
 

@@ -396,7 +396,7 @@ def main():
     d = {"n": n, "P": P, "K": K, "G": gl, "p": p, "nranks": shard_ranks}
     kern = {}
     roof = None
-    fused_z = K <= 32 and "k_wpass" in stats and "k_zdraw" not in stats
+    fused_z = K <= 32 and stats.get("k_wpass", (0, 0))[1] > 0 and stats.get("k_zdraw", (0, 0))[1] == 0
     def work_of(name, cnt, saved, iters):
         """Algorithmic (flops, bytes, bound) per launch: per-iteration work spread over the
         launches of one iteration (the Y-pass / row kernels run as two shard groups)."""
