@@ -1070,12 +1070,13 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     // (k_wcol, k_xdraw); K > 32 (or DCFM_FLAG_UNFUSED): prep and the X operators run on the
     // side stream
     const bool fused = h->fused;
-    const bool lamgen = fused && !d.inject;   // k_xdraw draws k_lambda's variates (b.ldraw)
+    const bool lamgen = fused && !d.inject;   // k_wcol draws k_lambda's variates (b.ldraw)
     // fused (K <= 32): per iteration t, k_wcol = [Z operators and shard sum of A of t, column
     // sums of t-1] beside the W pass of t, whose tiles draw Z; one rank: the last chunk also
     // factors Xprec.  Several ranks: k_xred and ONE all-gather of [column sums | A sum | X
-    // message].  Then k_xdraw = [X operators (several ranks), delta chain of t-1, loading-row
-    // variates of t] beside the X draw.  The last iteration's chain runs after the loop (k_delta).
+    // message].  Then k_xdraw = [X operators (several ranks), delta chain of t-1] beside the X
+    // draw.  k_wcol also draws the loading-row variates of t (generated chain).  The last
+    // iteration's chain runs after the loop (k_delta).
     const bool wc = fused && d.nranks == 1;
     bool delta_pending = false;           // k_lambda of it - 1 ran, its delta chain not yet queued
     auto after_delta = [&]() {            // iteration it - 1 is complete
@@ -1143,7 +1144,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         if (wc) {   // k_wcol: + the Z draw of the W tiles' rows
             KTimer t(h, DCFM_K_WPASS, s);
             h->wc_ops += 1;
-            launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s);
+            launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s, lamgen);
         } else if (fused) {   // several ranks: k_wcol (W pass + Z draw, no X factorisation), k_xred
                               // (the local X message), then ONE all-gather of [column sums of it - 1
                               // | local A sum | X message]; k_xdraw factors Xprec from the ranks' A
@@ -1151,7 +1152,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             {
                 KTimer t(h, DCFM_K_WPASS, s);
                 h->wc_ops += 1;
-                launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s);
+                launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s, lamgen);
             }
             { KTimer t(h, DCFM_K_XRED, s); launch_xred(d, b, s); }
             KTimer t(h, DCFM_K_COMM, s);
@@ -1183,9 +1184,9 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             KTimer t(h, DCFM_K_XDRAW, s);
             if (delta_pending)
                 launch_xdraw_wc(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
-                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, s, lamgen);
+                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, s);
             else
-                launch_xdraw_wc(d, b, dr, it, nullptr, nullptr, nullptr, nullptr, 0, s, lamgen);
+                launch_xdraw_wc(d, b, dr, it, nullptr, nullptr, nullptr, nullptr, 0, s);
             HIPC(h, hipGetLastError());
             if (delta_pending) after_delta();
             delta_pending = false;
@@ -1194,16 +1195,15 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             h->xm_ops += 1;
             if (delta_pending)
                 launch_xdraw_mr(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
-                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, h->xm_ops, s,
-                                lamgen);
+                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, h->xm_ops, s);
             else
-                launch_xdraw_mr(d, b, dr, it, nullptr, nullptr, nullptr, nullptr, 0, h->xm_ops, s, lamgen);
+                launch_xdraw_mr(d, b, dr, it, nullptr, nullptr, nullptr, nullptr, 0, h->xm_ops, s);
             HIPC(h, hipGetLastError());
             if (delta_pending) after_delta();
             delta_pending = false;
         } else {
             KTimer t(h, DCFM_K_XDRAW, s);
-            launch_xdraw(d, b, dr, it, s, fused && d.nranks == 1, lamgen);
+            launch_xdraw(d, b, dr, it, s, fused && d.nranks == 1);
         }
         { KTimer t(h, DCFM_K_CPASS, s);  launch_cpass(d, b, s); }
         {

@@ -75,11 +75,12 @@ struct DrawsDev {
 // loading-row variates of one iteration in k_lambda's layout (local shard m, loading row j):
 // NL [G][P][K] (dc:142 zlam), Gpsi [G][P][K] (dc:150), Gps [G][P] (dc:170)
 struct LamDraws { const double *NL, *Gpsi, *Gps; };
-// k_xdraw's extra blocks that generate them for the generated fused chain (K <= 32): block
-// segments [0, b_ps) ps gammas, [b_ps, b_psi) psi gammas, [b_psi, b_total) normal pairs,
-// one variate (pair) per thread of LAM_GEN_THREADS
-constexpr int LAM_GEN_THREADS = 1024;
-struct LamGen { double *NL, *Gpsi, *Gps; int b_ps, b_psi, b_total; };
+// k_wcol's extra blocks generate them for the generated fused chain (K <= 32): one index
+// space — [0, n_ps) ps gammas, [n_ps, n_psi) psi gammas, [n_psi, n_all) normal pairs — walked
+// grid-stride by b_total blocks of LAM_GEN_THREADS behind the W tiles (VALU work in the slots
+// and issue cycles the streaming W pass leaves free)
+constexpr int LAM_GEN_THREADS = 256, LAM_GEN_BLOCKS = 160;
+struct LamGen { double *NL, *Gpsi, *Gps; int n_ps, n_psi, n_all, b_total; };
 inline int lam_gen_doubles(const Dims &d) { return 2 * d.G * d.P * d.K + d.G * d.P; }
 inline LamGen lam_gen_plan(const Dims &d, double *base) {
     const int T = LAM_GEN_THREADS, GP = d.G * d.P;
@@ -87,9 +88,11 @@ inline LamGen lam_gen_plan(const Dims &d, double *base) {
     g.NL = base;
     g.Gpsi = base + (size_t)GP * d.K;
     g.Gps = base + 2 * (size_t)GP * d.K;
-    g.b_ps = (GP + T - 1) / T;
-    g.b_psi = g.b_ps + (GP * d.K + T - 1) / T;
-    g.b_total = g.b_psi + (GP * ((d.K + 1) / 2) + T - 1) / T;
+    g.n_ps = GP;
+    g.n_psi = GP + GP * d.K;
+    g.n_all = g.n_psi + GP * ((d.K + 1) / 2);
+    const int full = (g.n_all + T - 1) / T;
+    g.b_total = full < LAM_GEN_BLOCKS ? full : LAM_GEN_BLOCKS;
     return g;
 }
 
@@ -157,24 +160,22 @@ void launch_xred(const Dims &d, const Bufs &b, hipStream_t s);
 // (colsum) and the Y pass W with the Z draw of its rows (wpass: Z, Sp; needs ops) in one launch
 // (k_wcol); one rank also factors Xprec
 void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool ops, bool colsum, bool wpass,
-                 unsigned long long ops_epoch, hipStream_t s);
-// one rank, K <= 32: k_xdraw plus, when delta_in != null, the delta chain of delta_iter, and
-// (lamgen) the iteration's loading-row variates into b.ldraw
+                 unsigned long long ops_epoch, hipStream_t s, bool lamgen = false);
+// one rank, K <= 32: k_xdraw plus, when delta_in != null, the delta chain of delta_iter
 void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
-                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s,
-                     bool lamgen);
+                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s);
 // several ranks, K <= 32: k_xdraw with the X operators (block 0, from the ranks' A sums of the
 // packed gather, published through the counter b.sync[0] at xm_epoch), the delta chain of
 // delta_iter (delta_in != null) and the row blocks summing the ranks' X messages
 void launch_xdraw_mr(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
                      const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter,
-                     unsigned long long xm_epoch, hipStream_t s, bool lamgen);
+                     unsigned long long xm_epoch, hipStream_t s);
 void launch_asum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
-                  bool from_shards = false, bool lamgen = false);
+                  bool from_shards = false);
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s);
-// gen: K <= 32 reads the variates k_xdraw generated into b.ldraw (the generated fused chain)
+// gen: K <= 32 reads the variates k_wcol generated into b.ldraw (the generated fused chain)
 // instead of the draw buffers dr (injected draws, k_draws batches)
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, const double *plam_src, hipStream_t s, bool gen = false);

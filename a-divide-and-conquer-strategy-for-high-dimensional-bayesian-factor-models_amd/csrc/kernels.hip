@@ -7,11 +7,12 @@
 //   k_wcol     [Z operators A_m -> M1, M2, U, NA (dc:98-107) | column sums of t-1 (dc:156) |
 //              shard sum of A, one rank: Xprec = g I + rho sum A, Rx (dc:112-118)] beside
 //              the W pass W_m = Y_m (w o Lambda_m) whose tiles draw Z from their registers
-//              and write Z and the shard X message (dc:101-107,121-123)
+//              and write Z and the shard X message (dc:101-107,121-123), and behind it the
+//              loading-row variates of t (dc:142,150,170) for k_lambda
 //   several ranks: k_xred (local sum of the X messages) + ONE RCCL all-gather of
 //              [column sums | A sum | X message]
 //   k_xdraw    X rows (dc:119-128) [+ several ranks: Xprec, Rx from the ranks' A sums] +
-//              the delta / tau chain of t-1 (dc:155-165) + the loading-row variates of t
+//              the delta / tau chain of t-1 (dc:155-165)
 //   k_cpass    C_m = Y_m' eta_m, E_m = eta_m' eta_m  fp64 MFMA, Y pass 2   dc:133,138,141
 //   k_lambda   per loading row: Q, chol, 3 solves, Lambda_j; psi_j;        dc:140-145,150,
 //              SS_j via identity, ps_j, omega_j; psi o L^2 per row         dc:156,169-171
@@ -196,6 +197,7 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
     prep_shard(d, Lam, omega, A, ZM, blockIdx.x, smem);
 }
 
+constexpr int WP_RING = 4;   // W pass register ring depth (chunks)
 // ============================================================================
 // k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA, Y pass 1
 // one wave = (shard m, 16 MT rows i = MT M-tiles) x 32 k (even / odd k tiles) of
@@ -211,8 +213,10 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 // shards per rank): each element's reduction order is the same for both, so the choice
 // changes no bit of W.
 // ============================================================================
-// pre() runs once the first three chunks' loads are issued (VALU work hidden behind their latency)
-template <int KW, int MT, class Pre>
+// Register ring of R chunks: chunk t + R - 1 is requested while chunk t multiplies, so R - 1
+// chunks are in flight behind the MFMAs.  pre() runs once the first R - 1 chunks' loads are
+// issued (VALU work hidden behind their latency).
+template <int KW, int MT, int R = WP_RING, class Pre>
 __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restrict__ Y, const double *__restrict__ Lam,
                                           const double *__restrict__ omega, int m, int i0, int kt, d4 (&acc)[MT][2],
                                           Pre &&pre) {
@@ -227,52 +231,42 @@ __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restric
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
     const int nch = d.PP >> 3;
-    d2 yA0, yA1, wA, lA0, lA1, yB0, yB1, wB, lB0, lB1;
-#define WP_LOAD(t, y0, y1, ww, l0, l1)                                              \
-    {                                                                               \
-        const int j = 8 * (t);                                                      \
-        y0 = *reinterpret_cast<const d2 *>(Y0 + j);                                 \
-        if (MT == 2) y1 = *reinterpret_cast<const d2 *>(Y1 + j);                    \
-        ww = *reinterpret_cast<const d2 *>(wp + j);                                 \
-        l0 = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q) * KW);           \
-        l1 = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q + 1) * KW);       \
-    }
-#define WP_MMA(y0, y1, ww, l0, l1)                                                  \
-    {                                                                               \
-        const double b00 = ww.x * l0.x, b01 = ww.x * l0.y;                          \
-        const double b10 = ww.y * l1.x, b11 = ww.y * l1.y;                          \
-        acc[0][0] = mfma16x16x4(b00, y0.x, acc[0][0]);                              \
-        acc[0][1] = mfma16x16x4(b01, y0.x, acc[0][1]);                              \
-        if (MT == 2) {                                                              \
-            acc[MT - 1][0] = mfma16x16x4(b00, y1.x, acc[MT - 1][0]);                \
-            acc[MT - 1][1] = mfma16x16x4(b01, y1.x, acc[MT - 1][1]);                \
-        }                                                                           \
-        acc[0][0] = mfma16x16x4(b10, y0.y, acc[0][0]);                              \
-        acc[0][1] = mfma16x16x4(b11, y0.y, acc[0][1]);                              \
-        if (MT == 2) {                                                              \
-            acc[MT - 1][0] = mfma16x16x4(b10, y1.y, acc[MT - 1][0]);                \
-            acc[MT - 1][1] = mfma16x16x4(b11, y1.y, acc[MT - 1][1]);                \
-        }                                                                           \
-    }
-    // ring of 4 register buffers: chunk t + 3 is requested while chunk t multiplies, so three
-    // chunks (6 KB per wave) are in flight behind the MFMAs (nch is a multiple of 4: PP % 32 == 0)
-    d2 yC0, yC1, wC, lC0, lC1, yD0, yD1, wD, lD0, lD1;
-    WP_LOAD(0, yA0, yA1, wA, lA0, lA1);
-    if (1 < nch) WP_LOAD(1, yB0, yB1, wB, lB0, lB1);
-    if (2 < nch) WP_LOAD(2, yC0, yC1, wC, lC0, lC1);
+    d2 y0[R], y1[R], ww[R], l0[R], l1[R];
+    auto load = [&](int t, int k) {
+        const int j = 8 * t;
+        y0[k] = *reinterpret_cast<const d2 *>(Y0 + j);
+        if (MT == 2) y1[k] = *reinterpret_cast<const d2 *>(Y1 + j);
+        ww[k] = *reinterpret_cast<const d2 *>(wp + j);
+        l0[k] = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q) * KW);
+        l1[k] = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q + 1) * KW);
+    };
+    auto mma = [&](int k) {
+        const double b00 = ww[k].x * l0[k].x, b01 = ww[k].x * l0[k].y;
+        const double b10 = ww[k].y * l1[k].x, b11 = ww[k].y * l1[k].y;
+        acc[0][0] = mfma16x16x4(b00, y0[k].x, acc[0][0]);
+        acc[0][1] = mfma16x16x4(b01, y0[k].x, acc[0][1]);
+        if (MT == 2) {
+            acc[MT - 1][0] = mfma16x16x4(b00, y1[k].x, acc[MT - 1][0]);
+            acc[MT - 1][1] = mfma16x16x4(b01, y1[k].x, acc[MT - 1][1]);
+        }
+        acc[0][0] = mfma16x16x4(b10, y0[k].y, acc[0][0]);
+        acc[0][1] = mfma16x16x4(b11, y0[k].y, acc[0][1]);
+        if (MT == 2) {
+            acc[MT - 1][0] = mfma16x16x4(b10, y1[k].y, acc[MT - 1][0]);
+            acc[MT - 1][1] = mfma16x16x4(b11, y1[k].y, acc[MT - 1][1]);
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < R - 1; ++k)
+        if (k < nch) load(k, k);
     pre();
-    for (int t = 0; t < nch; t += 4) {
-        if (t + 3 < nch) WP_LOAD(t + 3, yD0, yD1, wD, lD0, lD1);
-        WP_MMA(yA0, yA1, wA, lA0, lA1);
-        if (t + 4 < nch) WP_LOAD(t + 4, yA0, yA1, wA, lA0, lA1);
-        if (t + 1 < nch) WP_MMA(yB0, yB1, wB, lB0, lB1);
-        if (t + 5 < nch) WP_LOAD(t + 5, yB0, yB1, wB, lB0, lB1);
-        if (t + 2 < nch) WP_MMA(yC0, yC1, wC, lC0, lC1);
-        if (t + 6 < nch) WP_LOAD(t + 6, yC0, yC1, wC, lC0, lC1);
-        if (t + 3 < nch) WP_MMA(yD0, yD1, wD, lD0, lD1);
+    for (int t = 0; t < nch; t += R) {
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            if (t + k + R - 1 < nch) load(t + k + R - 1, (k + R - 1) % R);
+            if (t + k < nch) mma(k);
+        }
     }
-#undef WP_LOAD
-#undef WP_MMA
 }
 
 template <int KW, int MT = 2>
@@ -723,16 +717,9 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
                                                 double *__restrict__ X, DrawsDev dr, int64_t iter, int xroles,
                                                 const double *__restrict__ xa, unsigned long long *xm_ctr,
                                                 unsigned long long xm_target, int ndel,
-                                                const double *__restrict__ sall, DeltaArgs da, LamGen lg) {
+                                                const double *__restrict__ sall, DeltaArgs da) {
     __shared__ double smem[XD_SMEM];
     int blk = blockIdx.x;
-    {   // the loading-row variates of this iteration: blocks after the row blocks (lam_draws_block)
-        const int nlead = ((xroles & 1) ? 1 : 0) + ((xroles & 2) ? ndel : 0) + (d.n + 15) / 16;
-        if (blk >= nlead) {
-            lam_draws_block(d, lg, iter, blk - nlead);
-            return;
-        }
-    }
     if (xroles & 1) {   // producer of XM
         if (blk == 0) {
             for (int e = threadIdx.x; e < KP * KP; e += 1024)   // several ranks: their sums, canonical tree
@@ -1169,7 +1156,11 @@ __device__ __forceinline__ bool last_arrival(unsigned *ticket, unsigned count, d
 //   OPS    [.., +nxs)  wait for every A_m; chunk j's tree sum (a canonical subtree) -> xpart;
 //                      the last arrival sums the chunks (canonical tree) into xa (dc:117);
 //                      (several ranks: k_xdraw's block 0 factors Xprec from the ranks' sums) dc:112-118
-//   WPASS  [.., +nw)   W_m = Y_m (w o Lambda_m) tiles                          dc:102-103,122-123
+//   WPASS  [.., +nw)   W_m = Y_m (w o Lambda_m) tiles, each drawing Z for its rows and writing
+//                      the shard's X message (wpass_z_tile)       dc:101-107,121-123
+//   LAMGEN [.., +nlg)  the generated chain's loading-row variates of this iteration for the
+//                      k_lambda that follows (lam_draws; VALU work in the slots and issue
+//                      cycles the streaming W tiles leave free)      dc:142,150,170
 // Hand-off: payload by agent-scope stores, s_waitcnt vmcnt(0), then a relaxed fetch-add on a
 // monotonic 64-bit counter; consumers poll it (s_sleep) up to the launch's target and read
 // the payload with agent-scope loads.
@@ -1241,7 +1232,7 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_wcol(Dims d, Bufs b, DrawsDev dr, int64_t iter, int ops, int colsum,
-                                              int wpass, unsigned long long ops_epoch, int xchol) {
+                                              int wpass, unsigned long long ops_epoch, int xchol, LamGen lg) {
     __shared__ double smem[PREP_SMEM];
     const int G = d.G, nxs = xsum_blocks(G), chunk = G / nxs;
     unsigned long long *chunk_ctr = b.sync + 2;   // per chunk of shards: A_m published
@@ -1340,10 +1331,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         blk -= nxs;
     }
     if (wpass) {   // 1: 128-row blocks, 2: 64-row blocks (wcol_wpass_mode); W' -> the Z draw
-        const int nw = gridDim.x - (int)(blockIdx.x - blk);
-        if (wpass == 2) wpass_z_tile<1>(d, b, dr, iter, xcd_remap(blk, nw), ops_epoch, smem);
-        else wpass_z_tile<2>(d, b, dr, iter, xcd_remap(blk, nw), ops_epoch, smem);
+        const int nw = (d.NP / (64 * (3 - wpass))) * d.G;
+        if (blk < nw) {
+            if (wpass == 2) wpass_z_tile<1>(d, b, dr, iter, xcd_remap(blk, nw), ops_epoch, smem);
+            else wpass_z_tile<2>(d, b, dr, iter, xcd_remap(blk, nw), ops_epoch, smem);
+            return;
+        }
+        blk -= nw;
     }
+    // the loading-row variates of this iteration (generated chain), behind every other role
+    if (blk < lg.b_total) lam_draws(d, lg, iter, blk * LAM_GEN_THREADS + (int)threadIdx.x, lg.b_total * LAM_GEN_THREADS);
 }
 
 // ============================================================================
@@ -1626,13 +1623,16 @@ void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
 }
 // k_wcol launch (K <= 32)
 void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool ops, bool colsum, bool wpass,
-                 unsigned long long ops_epoch, hipStream_t s) {
+                 unsigned long long ops_epoch, hipStream_t s, bool lamgen) {
+    static_assert(LAM_GEN_THREADS == 256, "k_wcol blocks are 256 threads");
+    LamGen lg = {};
+    if (lamgen && b.ldraw) lg = lam_gen_plan(d, b.ldraw);
     // W pass tiles: 64-row blocks while 128-row blocks would leave CUs idle
     const int wmode = (d.NP / 128) * d.G < 256 ? 2 : 1;
     const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / (64 * (3 - wmode))) * d.G : 0);
-    if (nb == 0) return;
-    hipLaunchKernelGGL(k_wcol, dim3(nb), dim3(256), 0, s, d, b, dr, iter, ops ? 1 : 0, colsum ? 1 : 0,
-                       wpass ? wmode : 0, ops_epoch, d.nranks == 1 ? 1 : 0);
+    if (nb + lg.b_total == 0) return;
+    hipLaunchKernelGGL(k_wcol, dim3(nb + lg.b_total), dim3(256), 0, s, d, b, dr, iter, ops ? 1 : 0, colsum ? 1 : 0,
+                       wpass ? wmode : 0, ops_epoch, d.nranks == 1 ? 1 : 0, lg);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
     const int total = d.NP * d.kp;
@@ -1645,48 +1645,38 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
     if (d.kp != KP) return wide::launch_xchol(d, b, s);
     hipLaunchKernelGGL(k_xchol, dim3(1), dim3(256), 0, s, d, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
 }
-static LamGen lam_gen_of(const Dims &d, const Bufs &b, bool lamgen) {
-    if (lamgen && b.ldraw) return lam_gen_plan(d, b.ldraw);
-    LamGen g = {};
-    return g;
-}
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
-                  bool from_shards, bool lamgen) {
+                  bool from_shards) {
     if (d.kp != KP) return wide::launch_xdraw(d, b, dr, iter, s);
     DeltaArgs da = {};
-    const LamGen lg = lam_gen_of(d, b, lamgen);
-    const dim3 grid(cdiv(d.n, 16) + lg.b_total);
+    const dim3 grid(cdiv(d.n, 16));
     const size_t st = (size_t)d.NP * KP;
     if (from_shards)   // one rank: sum the G shard messages here (no k_xred)
         hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.Sp, d.G, st, b.XM, b.X, dr, iter, 0,
-                           nullptr, nullptr, 0ull, 0, nullptr, da, lg);
+                           nullptr, nullptr, 0ull, 0, nullptr, da);
     else
         hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.xall, d.nranks, st, b.XM, b.X, dr,
-                           iter, 0, nullptr, nullptr, 0ull, 0, nullptr, da, lg);
+                           iter, 0, nullptr, nullptr, 0ull, 0, nullptr, da);
 }
 void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
-                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s,
-                     bool lamgen) {
+                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s) {
     const int ndel = delta_in ? (d.g + 15) / 16 : 0;
     DeltaArgs da;
     da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
     da.iter = delta_iter;
-    const LamGen lg = lam_gen_of(d, b, lamgen);
-    hipLaunchKernelGGL(k_xdraw, dim3(ndel + cdiv(d.n, 16) + lg.b_total), dim3(1024), 0, s, d, b.Sp, d.G,
-                       (size_t)d.NP * KP, b.XM, b.X, dr, iter, delta_in ? 2 : 0, nullptr, nullptr, 0ull, ndel, b.sall,
-                       da, lg);
+    hipLaunchKernelGGL(k_xdraw, dim3(ndel + cdiv(d.n, 16)), dim3(1024), 0, s, d, b.Sp, d.G, (size_t)d.NP * KP, b.XM,
+                       b.X, dr, iter, delta_in ? 2 : 0, nullptr, nullptr, 0ull, ndel, b.sall, da);
 }
 void launch_xdraw_mr(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
                      const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter,
-                     unsigned long long xm_epoch, hipStream_t s, bool lamgen) {
+                     unsigned long long xm_epoch, hipStream_t s) {
     const int ndel = delta_in ? (d.g + 15) / 16 : 0;
     DeltaArgs da;
     da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
     da.iter = delta_iter;
-    const LamGen lg = lam_gen_of(d, b, lamgen);
-    hipLaunchKernelGGL(k_xdraw, dim3(1 + ndel + cdiv(d.n, 16) + lg.b_total), dim3(1024), 0, s, d, b.xall, d.nranks,
+    hipLaunchKernelGGL(k_xdraw, dim3(1 + ndel + cdiv(d.n, 16)), dim3(1024), 0, s, d, b.xall, d.nranks,
                        (size_t)d.xstride, b.XM, b.X, dr, iter, 1 | (delta_in ? 2 : 0), b.xa_all, b.sync, xm_epoch,
-                       ndel, b.sall, da, lg);
+                       ndel, b.sall, da);
 }
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(((d.PP + d.kp) / 32) * d.G * (d.kp / 32));

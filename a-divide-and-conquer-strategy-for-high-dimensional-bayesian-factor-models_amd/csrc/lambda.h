@@ -10,36 +10,31 @@ namespace dcfm {
 
 // The loading-row variates of one iteration (dc:142 zlam, dc:150 psi gammas, dc:170 ps
 // gamma) into k_lambda's buffer layout, at the counters every other path draws them from
-// (k_draws, dcfm_rng_fill): one thread per ps gamma, per psi gamma and per normal pair, the
-// rejection-sampled ps gammas first.  Runs as extra blocks of k_xdraw (latency-bound, most
-// CUs idle) so the loading-row kernel reads its variates instead of drawing them.
-__device__ __forceinline__ void lam_draws_block(const Dims &d, const LamGen &lg, int64_t iter, int blk) {
+// (k_draws, dcfm_rng_fill): thread gtid of gthreads takes variates gtid, gtid + gthreads, ...
+// of the index space (ps gammas, psi gammas, normal pairs).  Runs as extra blocks of k_wcol
+// (behind the W tiles) so the loading-row kernel reads its variates instead of drawing them.
+__device__ __forceinline__ void lam_draws(const Dims &d, const LamGen &lg, int64_t iter, int gtid, int gthreads) {
     const Rng rng(d.seed);
     const uint32_t it = (uint32_t)iter;
-    const int t = threadIdx.x;
-    if (blk < lg.b_ps) {
-        const int x = blk * LAM_GEN_THREADS + t;            // (m, j)
-        if (x >= d.G * d.P) return;
-        const int m = x / d.P, j = x - m * d.P;
-        lg.Gps[x] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, (uint32_t)(d.shard0 + m), (uint32_t)j, 0u, it);
-        return;
-    }
-    if (blk < lg.b_psi) {
-        const int x = (blk - lg.b_ps) * LAM_GEN_THREADS + t;   // (m, j, k)
-        if (x >= d.G * d.P * d.K) return;
-        const int mj = x / d.K, k = x - mj * d.K, m = mj / d.P, j = mj - m * d.P;
-        lg.Gpsi[x] = rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)k, it);
-        return;
-    }
     const int kp2 = (d.K + 1) / 2;
-    const int x = (blk - lg.b_psi) * LAM_GEN_THREADS + t;      // (m, j, pair)
-    if (x >= d.G * d.P * kp2) return;
-    const int mj = x / kp2, q = x - mj * kp2, m = mj / d.P, j = mj - m * d.P;
-    double n0, n1;
-    rng.normal2(SITE_LAMBDA, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)q, it, n0, n1);
-    double *o = lg.NL + (size_t)mj * d.K + 2 * q;
-    o[0] = n0;
-    if (2 * q + 1 < d.K) o[1] = n1;
+    for (int x = gtid; x < lg.n_all; x += gthreads) {
+        if (x < lg.n_ps) {                                 // (m, j)
+            const int m = x / d.P, j = x - m * d.P;
+            lg.Gps[x] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, (uint32_t)(d.shard0 + m), (uint32_t)j, 0u, it);
+        } else if (x < lg.n_psi) {                         // (m, j, k)
+            const int y = x - lg.n_ps;
+            const int mj = y / d.K, k = y - mj * d.K, m = mj / d.P, j = mj - m * d.P;
+            lg.Gpsi[y] = rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)k, it);
+        } else {                                           // (m, j, pair)
+            const int y = x - lg.n_psi;
+            const int mj = y / kp2, q = y - mj * kp2, m = mj / d.P, j = mj - m * d.P;
+            double n0, n1;
+            rng.normal2(SITE_LAMBDA, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)q, it, n0, n1);
+            double *o = lg.NL + (size_t)mj * d.K + 2 * q;
+            o[0] = n0;
+            if (2 * q + 1 < d.K) o[1] = n1;
+        }
+    }
 }
 
 // ============================================================================
@@ -66,7 +61,7 @@ __device__ __forceinline__ void lam_draws_block(const Dims &d, const LamGen &lg,
 //     second read of E or C), ps_j and omega_j (dc:169-171), psi o Lambda^2 -> cpart (dc:156).
 // Plam_j = psi_j o tau' (dc:176) is formed from the previous iteration's psi and tau unless
 // plam_src is given (first iteration after dcfm_set_state).  The row's variates (dc:142, 150,
-// 170) come from a draw buffer: the generated chain's k_xdraw draws them (lam_draws_block),
+// 170) come from a draw buffer: the generated chain's k_wcol draws them (lam_draws),
 // injected draws and the k_draws batches are read in place.
 // ============================================================================
 // DPP moves within the aligned 8-lane group (every source lane of these patterns is valid)
