@@ -1180,32 +1180,28 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             }
             HIPC(h, hipStreamWaitEvent(s, h->e_xchol, 0));
         }
-        if (wc) {   // + the delta chain of it - 1
-            KTimer t(h, DCFM_K_XDRAW, s);
-            if (delta_pending)
-                launch_xdraw_wc(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
-                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, s);
-            else
-                launch_xdraw_wc(d, b, dr, it, nullptr, nullptr, nullptr, nullptr, 0, s);
-            HIPC(h, hipGetLastError());
-            if (delta_pending) after_delta();
-            delta_pending = false;
-        } else if (fused) {   // several ranks: + the X factorisation and the delta chain of it - 1
+        if (fused && d.nranks > 1) {   // several ranks: + the X factorisation
             KTimer t(h, DCFM_K_XDRAW, s);
             h->xm_ops += 1;
+            launch_xdraw_mr(d, b, dr, it, h->xm_ops, s);
+        } else {
+            KTimer t(h, DCFM_K_XDRAW, s);
+            launch_xdraw(d, b, dr, it, s, wc);
+        }
+        if (fused) {   // k_cpass + the delta chain of it - 1 (column sums from k_wcol / the gather)
+            KTimer t(h, DCFM_K_CPASS, s);
             if (delta_pending)
-                launch_xdraw_mr(d, b, dr, it, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
-                                b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1, h->xm_ops, s);
+                launch_cpass(d, b, s, dr, b.delta + h->cur * nkg, b.tau + h->cur * nkg, b.delta + (1 - h->cur) * nkg,
+                             b.tau + (1 - h->cur) * nkg, it - 1);
             else
-                launch_xdraw_mr(d, b, dr, it, nullptr, nullptr, nullptr, nullptr, 0, h->xm_ops, s);
+                launch_cpass(d, b, s);
             HIPC(h, hipGetLastError());
             if (delta_pending) after_delta();
             delta_pending = false;
         } else {
-            KTimer t(h, DCFM_K_XDRAW, s);
-            launch_xdraw(d, b, dr, it, s, fused && d.nranks == 1);
+            KTimer t(h, DCFM_K_CPASS, s);
+            launch_cpass(d, b, s);
         }
-        { KTimer t(h, DCFM_K_CPASS, s);  launch_cpass(d, b, s); }
         {
             KTimer t(h, DCFM_K_LAMBDA, s);
             launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, lamgen);

@@ -161,20 +161,20 @@ void launch_xred(const Dims &d, const Bufs &b, hipStream_t s);
 // (k_wcol); one rank also factors Xprec
 void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool ops, bool colsum, bool wpass,
                  unsigned long long ops_epoch, hipStream_t s, bool lamgen = false);
-// one rank, K <= 32: k_xdraw plus, when delta_in != null, the delta chain of delta_iter
-void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
-                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s);
 // several ranks, K <= 32: k_xdraw with the X operators (block 0, from the ranks' A sums of the
-// packed gather, published through the counter b.sync[0] at xm_epoch), the delta chain of
-// delta_iter (delta_in != null) and the row blocks summing the ranks' X messages
-void launch_xdraw_mr(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
-                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter,
-                     unsigned long long xm_epoch, hipStream_t s);
+// packed gather, published through the counter b.sync[0] at xm_epoch) and the row blocks
+// summing the ranks' X messages
+void launch_xdraw_mr(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, unsigned long long xm_epoch,
+                     hipStream_t s);
 void launch_asum(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
                   bool from_shards = false);
-void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s);
+// k_cpass; with delta_in (fused K <= 32 chain) also the delta / tau chain of delta_iter in
+// extra blocks (column sums from b.sall)
+void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &dr = DrawsDev{},
+                  const double *delta_in = nullptr, const double *tau_in = nullptr, double *delta_out = nullptr,
+                  double *tau_out = nullptr, int64_t delta_iter = 0);
 // gen: K <= 32 reads the variates k_wcol generated into b.ldraw (the generated fused chain)
 // instead of the draw buffers dr (injected draws, k_draws batches)
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,

@@ -706,18 +706,19 @@ struct DeltaArgs {
     double *delta_out, *tau_out;
     int64_t iter;                          // iteration whose delta / tau the chain updates
 };
-// Roles of the one-rank launch (xroles != 0), in block order: block 0 factors Xprec from the
-// shard sum xa (dc:117-118) and publishes XM; blocks [1, 1 + ndel) run the previous
-// iteration's delta chain (16 shards per block; dc:155-165), on CUs the 63 row blocks leave
-// idle; the row blocks sum their messages first and wait for XM only before the MFMAs.
+// Roles (xroles & 1, several ranks): block 0 factors Xprec from the ranks' A sums and publishes
+// XM; the row blocks sum their messages first and wait for XM only before the MFMAs.  Row
+// blocks of XD_ROWS = 8 rows (the MFMA's other 8 columns padding): the shard-message sums are
+// bound by the memory parallelism of the CUs that issue them (phase stamps: 9 of 14 us with 63
+// blocks of 16 rows at c3), so twice the blocks halve them.
+constexpr int XD_ROWS = 8;
 constexpr int XD_SMEM = (2 * KP * (KP + 1) + 4 * 4 * 64 * 2) > XCHOL_SMEM ? (2 * KP * (KP + 1) + 4 * 4 * 64 * 2)
                                                                           : XCHOL_SMEM;
 __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict__ src, int nsrc, size_t sstride,
                                                 double *__restrict__ XM,
                                                 double *__restrict__ X, DrawsDev dr, int64_t iter, int xroles,
                                                 const double *__restrict__ xa, unsigned long long *xm_ctr,
-                                                unsigned long long xm_target, int ndel,
-                                                const double *__restrict__ sall, DeltaArgs da) {
+                                                unsigned long long xm_target) {
     __shared__ double smem[XD_SMEM];
     int blk = blockIdx.x;
     if (xroles & 1) {   // producer of XM
@@ -731,22 +732,12 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
         }
         blk -= 1;
     }
-    if (xroles & 2) {   // the previous iteration's delta chain
-        if (blk < ndel) {
-            const int m = blk * 16 + (threadIdx.x >> 6);
-            if (m < d.g)
-                delta_shard(d, sall, da.delta_in, da.tau_in, da.delta_out, da.tau_out, dr, da.iter, m,
-                            threadIdx.x & 63);
-            return;
-        }
-        blk -= ndel;
-    }
     double (*Ms)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);
     d2 (*part)[4][64] = reinterpret_cast<d2 (*)[4][64]>(smem + 2 * KP * (KP + 1));
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, q = lane >> 4;
     const int tw = w & 3, sw = w >> 2;                 // column group, source chunk
-    const int i0 = blk * 16, i = i0 + c;
-    const bool live = i < d.n;
+    const int i0 = blk * XD_ROWS, i = i0 + c;
+    const bool live = c < XD_ROWS && i < d.n;          // lanes c >= XD_ROWS pad the MFMA's 16 columns
     const size_t stride = sstride;
     int nch, chunk;
     xdraw_chunks(nsrc, nch, chunk);     // chunk < 1024 (TreeSum levels below); dcfm_create caps g
@@ -770,15 +761,28 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
             ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
         }
     }
-    if (sw < nch) {
-        const double *p = src + (size_t)sw * chunk * stride + (size_t)i * KP + 8 * tw + 2 * q;
-        part[sw][tw][lane] =
-            tree_sum_f<d2, 8, 10>(chunk, [&](int rk) { return *reinterpret_cast<const d2 *>(p + (size_t)rk * stride); });
+    // one rank: the operators are already out (k_wcol's last arrival): their loads go out before
+    // the sums' (two per thread), the LDS stores after
+    double xmv[2] = {0.0, 0.0};
+    if (!(xroles & 1)) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) xmv[u] = XM[threadIdx.x + 1024 * u];
     }
-    if (xroles & 1) wait_count(xm_ctr, xm_target);       // XM of this launch's block 0
-    for (int e = threadIdx.x; e < 2 * KP * KP; e += 1024) {
+    if (sw < nch) {
+        const double *p = src + (size_t)sw * chunk * stride + (size_t)(live ? i : i0) * KP + 8 * tw + 2 * q;
+        part[sw][tw][lane] = live ? tree_sum_f<d2, 8, 10>(chunk, [&](int rk) { return *reinterpret_cast<const d2 *>(p + (size_t)rk * stride); })
+                                  : d2{0.0, 0.0};
+    }
+    if (xroles & 1) {
+        wait_count(xm_ctr, xm_target);       // XM of this launch's block 0
+#pragma unroll
+        for (int u = 0; u < 2; ++u) xmv[u] = ld_agent(XM + threadIdx.x + 1024 * u);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = threadIdx.x + 1024 * u;
         const int mat = e / (KP * KP), rem = e % (KP * KP);
-        Ms[mat][rem / KP][rem % KP] = (xroles & 1) ? ld_agent(XM + e) : XM[e];
+        Ms[mat][rem / KP][rem % KP] = xmv[u];
     }
     __syncthreads();
     if (w > 0) return;
@@ -884,17 +888,30 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
 template <int KW> constexpr int cp_waves() { return 4; }
 // PS (K <= 32, where the launch would leave CUs idle): each block computes one parity of its
 // 32 k columns (twice the blocks, the pair adjacent: Y from L2); per-element order unchanged
+// ndel > 0 (fused K <= 32 chain): the last ndel blocks run the previous iteration's delta / tau
+// chain (one wave per shard, dc:155-165) beside the pass — it needs only the column sums k_wcol
+// (and, several ranks, the packed gather) left, and its ~12 us chain of dependent steps would
+// otherwise be the long pole of k_xdraw
 template <int KW, bool PS = false>
 __global__ __launch_bounds__(64 * cp_waves<KW>()) void k_cpass(Dims d, const double *__restrict__ Y,
                                                               const double *__restrict__ X,
                                                               const double *__restrict__ Z,
-                                                              double *__restrict__ C, double *__restrict__ E) {
+                                                              double *__restrict__ C, double *__restrict__ E,
+                                                              DrawsDev dr, const double *__restrict__ sall,
+                                                              DeltaArgs da, int ndel) {
     constexpr int NWV = cp_waves<KW>();
     __shared__ double red[NWV][32][33];
+    const int nbc = gridDim.x - ndel;
+    if ((int)blockIdx.x >= nbc) {
+        const int m = (blockIdx.x - nbc) * NWV + (threadIdx.x >> 6);
+        if (m < d.g)
+            delta_shard(d, sall, da.delta_in, da.tau_in, da.delta_out, da.tau_out, dr, da.iter, m, threadIdx.x & 63);
+        return;
+    }
     // 1-D grid, the KW/32 eta column tiles of one [Y | eta] tile adjacent (same XCD,
     // so the Y tile is fetched once and re-read from L2)
     const int nt = (d.PP + KW) >> 5, nkt = KW / 32;
-    int w = xcd_remap(blockIdx.x, gridDim.x);
+    int w = xcd_remap(blockIdx.x, nbc);
     const int par = PS ? (w & 1) : 0;
     if (PS) w >>= 1;
     const int kt = w % nkt, m = (w / nkt) / nt, tile = (w / nkt) % nt;
@@ -1648,48 +1665,42 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
                   bool from_shards) {
     if (d.kp != KP) return wide::launch_xdraw(d, b, dr, iter, s);
-    DeltaArgs da = {};
-    const dim3 grid(cdiv(d.n, 16));
+    const dim3 grid(cdiv(d.n, XD_ROWS));
     const size_t st = (size_t)d.NP * KP;
     if (from_shards)   // one rank: sum the G shard messages here (no k_xred)
-        hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.Sp, d.G, st, b.XM, b.X, dr, iter, 0,
-                           nullptr, nullptr, 0ull, 0, nullptr, da);
+        hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.Sp, d.G, st, b.XM, b.X, dr, iter, 0, nullptr, nullptr,
+                           0ull);
     else
-        hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.xall, d.nranks, st, b.XM, b.X, dr,
-                           iter, 0, nullptr, nullptr, 0ull, 0, nullptr, da);
+        hipLaunchKernelGGL(k_xdraw, grid, dim3(1024), 0, s, d, b.xall, d.nranks, st, b.XM, b.X, dr, iter, 0, nullptr,
+                           nullptr, 0ull);
 }
-void launch_xdraw_wc(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
-                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter, hipStream_t s) {
-    const int ndel = delta_in ? (d.g + 15) / 16 : 0;
-    DeltaArgs da;
-    da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
-    da.iter = delta_iter;
-    hipLaunchKernelGGL(k_xdraw, dim3(ndel + cdiv(d.n, 16)), dim3(1024), 0, s, d, b.Sp, d.G, (size_t)d.NP * KP, b.XM,
-                       b.X, dr, iter, delta_in ? 2 : 0, nullptr, nullptr, 0ull, ndel, b.sall, da);
+void launch_xdraw_mr(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, unsigned long long xm_epoch,
+                     hipStream_t s) {
+    hipLaunchKernelGGL(k_xdraw, dim3(1 + cdiv(d.n, XD_ROWS)), dim3(1024), 0, s, d, b.xall, d.nranks, (size_t)d.xstride,
+                       b.XM, b.X, dr, iter, 1, b.xa_all, b.sync, xm_epoch);
 }
-void launch_xdraw_mr(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
-                     const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter,
-                     unsigned long long xm_epoch, hipStream_t s) {
-    const int ndel = delta_in ? (d.g + 15) / 16 : 0;
-    DeltaArgs da;
-    da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
-    da.iter = delta_iter;
-    hipLaunchKernelGGL(k_xdraw, dim3(1 + ndel + cdiv(d.n, 16)), dim3(1024), 0, s, d, b.xall, d.nranks,
-                       (size_t)d.xstride, b.XM, b.X, dr, iter, 1 | (delta_in ? 2 : 0), b.xa_all, b.sync, xm_epoch,
-                       ndel, b.sall, da);
-}
-void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s) {
+void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &dr, const double *delta_in,
+                  const double *tau_in, double *delta_out, double *tau_out, int64_t delta_iter) {
     const dim3 grid(((d.PP + d.kp) / 32) * d.G * (d.kp / 32));
+    DeltaArgs da;
+    da.delta_in = delta_in; da.tau_in = tau_in; da.delta_out = delta_out; da.tau_out = tau_out;
+    da.iter = delta_iter;
+    const int ndel = (delta_in && d.kp == KP) ? cdiv(d.g, cp_waves<32>()) : 0;
     switch (d.kp) {
     case 32:
         if (grid.x < 512)   // a few shards per rank: split the k columns by parity (k_cpass PS)
-            hipLaunchKernelGGL((k_cpass<32, true>), dim3(2 * grid.x), dim3(64 * cp_waves<32>()), 0, s, d, b.Y, b.X, b.Z,
-                               b.C, b.E);
+            hipLaunchKernelGGL((k_cpass<32, true>), dim3(2 * grid.x + ndel), dim3(64 * cp_waves<32>()), 0, s, d, b.Y,
+                               b.X, b.Z, b.C, b.E, dr, b.sall, da, ndel);
         else
-            hipLaunchKernelGGL((k_cpass<32, false>), grid, dim3(64 * cp_waves<32>()), 0, s, d, b.Y, b.X, b.Z, b.C, b.E);
+            hipLaunchKernelGGL((k_cpass<32, false>), dim3(grid.x + ndel), dim3(64 * cp_waves<32>()), 0, s, d, b.Y, b.X,
+                               b.Z, b.C, b.E, dr, b.sall, da, ndel);
         break;
-    case 64: hipLaunchKernelGGL(k_cpass<64>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
-    default: hipLaunchKernelGGL(k_cpass<128>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E); break;
+    case 64:
+        hipLaunchKernelGGL(k_cpass<64>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E, dr, b.sall, da, 0);
+        break;
+    default:
+        hipLaunchKernelGGL(k_cpass<128>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E, dr, b.sall, da, 0);
+        break;
     }
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
