@@ -769,9 +769,20 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
         for (int u = 0; u < 2; ++u) xmv[u] = XM[threadIdx.x + 1024 * u];
     }
     if (sw < nch) {
-        const double *p = src + (size_t)sw * chunk * stride + (size_t)(live ? i : i0) * KP + 8 * tw + 2 * q;
-        part[sw][tw][lane] = live ? tree_sum_f<d2, 8, 10>(chunk, [&](int rk) { return *reinterpret_cast<const d2 *>(p + (size_t)rk * stride); })
-                                  : d2{0.0, 0.0};
+        if (chunk >= 2) {   // lanes c and c + 8 sum the two halves of the chunk (canonical subtrees) for row c & 7
+            const int r8 = c & 7, h = c >> 3, half = chunk >> 1;
+            const bool rl = i0 + r8 < d.n;
+            const double *p = src + (size_t)(sw * chunk + h * half) * stride + (size_t)(rl ? i0 + r8 : i0) * KP + 8 * tw + 2 * q;
+            d2 v = rl ? tree_sum_f<d2, 8, 10>(half, [&](int rk) { return *reinterpret_cast<const d2 *>(p + (size_t)rk * stride); })
+                      : d2{0.0, 0.0};
+            d2 u;
+            u.x = __shfl_down(v.x, 8, 16);
+            u.y = __shfl_down(v.y, 8, 16);
+            part[sw][tw][lane] = h == 0 ? d2{v.x + u.x, v.y + u.y} : d2{0.0, 0.0};
+        } else {
+            const double *p = src + (size_t)sw * chunk * stride + (size_t)(live ? i : i0) * KP + 8 * tw + 2 * q;
+            part[sw][tw][lane] = live ? *reinterpret_cast<const d2 *>(p) : d2{0.0, 0.0};
+        }
     }
     if (xroles & 1) {
         wait_count(xm_ctr, xm_target);       // XM of this launch's block 0
