@@ -708,10 +708,10 @@ struct DeltaArgs {
 };
 // Roles (xroles & 1, several ranks): block 0 factors Xprec from the ranks' A sums and publishes
 // XM; the row blocks sum their messages first and wait for XM only before the MFMAs.  Row
-// blocks of XD_ROWS = 8 rows (the MFMA's other 8 columns padding): the shard-message sums are
-// bound by the memory parallelism of the CUs that issue them (phase stamps: 9 of 14 us with 63
-// blocks of 16 rows at c3), so twice the blocks halve them.
-constexpr int XD_ROWS = 8;
+// blocks of XD_ROWS rows (the MFMA's other columns padding), every lane summing one part of a
+// source chunk: the shard-message sums are bound by the memory parallelism of the CUs that
+// issue them (phase stamps: 9 of 14 us with 63 blocks of 16 rows at c3).
+constexpr int XD_ROWS = 4;
 constexpr int XD_SMEM = (2 * KP * (KP + 1) + 4 * 4 * 64 * 2) > XCHOL_SMEM ? (2 * KP * (KP + 1) + 4 * 4 * 64 * 2)
                                                                           : XCHOL_SMEM;
 __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict__ src, int nsrc, size_t sstride,
@@ -769,16 +769,23 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
         for (int u = 0; u < 2; ++u) xmv[u] = XM[threadIdx.x + 1024 * u];
     }
     if (sw < nch) {
-        if (chunk >= 2) {   // lanes c and c + 8 sum the two halves of the chunk (canonical subtrees) for row c & 7
-            const int r8 = c & 7, h = c >> 3, half = chunk >> 1;
-            const bool rl = i0 + r8 < d.n;
-            const double *p = src + (size_t)(sw * chunk + h * half) * stride + (size_t)(rl ? i0 + r8 : i0) * KP + 8 * tw + 2 * q;
-            d2 v = rl ? tree_sum_f<d2, 8, 10>(half, [&](int rk) { return *reinterpret_cast<const d2 *>(p + (size_t)rk * stride); })
+        if (chunk >= 2) {   // lane c sums part c / XD_ROWS (a canonical subtree) of the chunk for row c % XD_ROWS
+            constexpr int NPART = 16 / XD_ROWS;
+            const int np = chunk < NPART ? chunk : NPART, per = chunk / np;
+            const int rr = c % XD_ROWS, h = c / XD_ROWS;
+            const bool rl = i0 + rr < d.n && h < np;
+            const double *p = src + (size_t)(sw * chunk + (h < np ? h : 0) * per) * stride +
+                              (size_t)(i0 + rr < d.n ? i0 + rr : i0) * KP + 8 * tw + 2 * q;
+            d2 v = rl ? tree_sum_f<d2, 8, 10>(per, [&](int rk) { return *reinterpret_cast<const d2 *>(p + (size_t)rk * stride); })
                       : d2{0.0, 0.0};
-            d2 u;
-            u.x = __shfl_down(v.x, 8, 16);
-            u.y = __shfl_down(v.y, 8, 16);
-            part[sw][tw][lane] = h == 0 ? d2{v.x + u.x, v.y + u.y} : d2{0.0, 0.0};
+            for (int o = 1; o < np; o <<= 1) {   // adjacent parts pairwise: the canonical tree over the parts
+                d2 u;
+                u.x = __shfl_down(v.x, o * XD_ROWS, 16);
+                u.y = __shfl_down(v.y, o * XD_ROWS, 16);
+                v.x = v.x + u.x;
+                v.y = v.y + u.y;
+            }
+            part[sw][tw][lane] = h == 0 ? v : d2{0.0, 0.0};
         } else {
             const double *p = src + (size_t)sw * chunk * stride + (size_t)(live ? i : i0) * KP + 8 * tw + 2 * q;
             part[sw][tw][lane] = live ? *reinterpret_cast<const d2 *>(p) : d2{0.0, 0.0};
