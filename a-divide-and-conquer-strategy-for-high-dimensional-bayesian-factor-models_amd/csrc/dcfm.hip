@@ -1189,14 +1189,16 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             launch_xdraw(d, b, dr, it, s, wc);
         }
         if (fused) {   // k_cpass + the delta chain of it - 1 (column sums from k_wcol / the gather)
-            KTimer t(h, DCFM_K_CPASS, s);
-            if (delta_pending)
-                launch_cpass(d, b, s, dr, b.delta + h->cur * nkg, b.tau + h->cur * nkg, b.delta + (1 - h->cur) * nkg,
-                             b.tau + (1 - h->cur) * nkg, it - 1);
-            else
-                launch_cpass(d, b, s);
+            {
+                KTimer t(h, DCFM_K_CPASS, s);
+                if (delta_pending)
+                    launch_cpass(d, b, s, dr, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
+                                 b.delta + (1 - h->cur) * nkg, b.tau + (1 - h->cur) * nkg, it - 1);
+                else
+                    launch_cpass(d, b, s);
+            }
             HIPC(h, hipGetLastError());
-            if (delta_pending) after_delta();
+            if (delta_pending) after_delta();   // outside the timer: it may launch k_trace_part
             delta_pending = false;
         } else {
             KTimer t(h, DCFM_K_CPASS, s);
