@@ -93,6 +93,11 @@ def config_key(args, world):
             f"steps{args.steps}_warmup{args.warmup}_gpus{world}{'_chains' if args.chains else ''}")
 
 
+# HIP-event role name -> the kernel rocprofv3 records it under (the fused K <= 32 chain's W pass
+# and Z draw run as roles of k_wcol)
+PMC_KERNEL = {"k_wpass": "k_wcol"}
+
+
 def pmc_traffic(kernel, build, key, launches):
     """HBM bytes per launch of `kernel` in the timed region, from a committed rocprofv3 PMC
     summary (profiles/*_pmc.json, tools/pmc_summary.py over separate FETCH_SIZE /
@@ -108,12 +113,19 @@ def pmc_traffic(kernel, build, key, launches):
         if doc.get("build") != build or doc.get("config") != key:
             continue
         ks = doc.get("kernels", {})
-        k = ks.get(kernel) or next((v for name, v in ks.items() if name.startswith(kernel + "_")), None)
+        k = (ks.get(kernel) or ks.get(PMC_KERNEL.get(kernel, ""))
+             or next((v for name, v in ks.items() if name.startswith(kernel + "_")), None))
         if not k:
             continue
         fe, wr = k.get("fetch_bytes_each"), k.get("write_bytes_each")
-        if fe and wr and len(fe) >= launches and len(wr) >= launches:
-            return sum(fe[-launches:]) / launches + sum(wr[-launches:]) / launches, str(f.relative_to(ROOT))
+        if fe and wr:
+            tot = [a + b for a, b in zip(fe, wr)]
+            if kernel in PMC_KERNEL:   # a run's last k_wcol is its column-sum-only launch, not a W pass
+                big = max(tot)
+                while tot and tot[-1] < 0.1 * big:
+                    tot.pop()
+            if len(tot) >= launches:
+                return sum(tot[-launches:]) / launches, str(f.relative_to(ROOT))
         if k.get("hbm_bytes_per_dispatch") is not None:
             return k["hbm_bytes_per_dispatch"], str(f.relative_to(ROOT))
     return None, None
