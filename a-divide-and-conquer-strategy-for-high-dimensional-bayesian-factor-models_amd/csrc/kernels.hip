@@ -910,8 +910,11 @@ template <int KW> constexpr int cp_waves() { return 4; }
 // chain (one wave per shard, dc:155-165) beside the pass — it needs only the column sums k_wcol
 // (and, several ranks, the packed gather) left, and its ~12 us chain of dependent steps would
 // otherwise be the long pole of k_xdraw
+// waves_per_eu(3): 164 VGPRs and no AGPRs (without it hipcc took 168 + 32 AGPRs, 2 waves per
+// SIMD); measured neutral at c3 and c4 (the pass is bound by its fp64 MFMA work, §4), kept
+// for the occupancy headroom
 template <int KW, bool PS = false>
-__global__ __launch_bounds__(64 * cp_waves<KW>()) void k_cpass(Dims d, const double *__restrict__ Y,
+__global__ __launch_bounds__(64 * cp_waves<KW>()) __attribute__((amdgpu_waves_per_eu(3))) void k_cpass(Dims d, const double *__restrict__ Y,
                                                               const double *__restrict__ X,
                                                               const double *__restrict__ Z,
                                                               double *__restrict__ C, double *__restrict__ E,

@@ -90,3 +90,50 @@ def test_full_get_equals_stripes(dcfm):
             assert np.array_equal(S[:, c0:c0 + nc], smp.get_sigma_cols(c0, nc))
     finally:
         smp.close()
+
+
+@pytest.mark.parametrize("name,n,P,g,K", [
+    ("c3", 1000, 312, 64, 30),           # BASELINE configs[2] shape on one GPU
+])
+def test_batched_flush_full_size(dcfm, name, n, P, g, K):
+    """The driver bench's assembly flush at full size (dc:180-196, Q8): burnin 0, MCMC 20,
+    thin 5 in ONE dcfm_run, so the 4 saved samples are accumulated by one k_assemble launch with
+    k extent 4K.  A second sampler with the same seed steps one iteration per dcfm_run (its
+    sweep is the same chain, bitwise) and records Lambda / omega after every saved iteration;
+    the batched chain's Sigmaout stripes must equal the closed form summed over those samples.
+    Pins the batched-flush path (asm_batch > 1) at a BASELINE shape, not only at p <= 2,560."""
+    rho = 0.5
+    Yd, st = _synthetic_state(dcfm, n, P, g, K, rho, seed=7)
+    p = P * g
+    burnin, mcmc, thin = 0, 20, 5
+    init = {f: st[f] for f in dcfm.STATE_FIELDS if f != "eta"}
+    batched = dcfm.Sampler(n, P, g, K, rho, burnin, mcmc, thin, seed=21)
+    stepped = dcfm.Sampler(n, P, g, K, rho, burnin, mcmc, thin, seed=21)
+    try:
+        for s in (batched, stepped):
+            s.set_data(Yd)
+            s.set_state(init)
+        del Yd
+        batched.run(1, burnin + mcmc)
+        samples = []
+        for it in range(1, burnin + mcmc + 1):
+            stepped.run(it, 1)
+            if it > burnin and it % thin == 0:
+                samples.append(stepped.get_state(("Lambda", "omega")))
+        assert batched.saved_samples() == len(samples) == mcmc // thin
+        fin_b = batched.get_state(("Lambda", "ps", "tau"))
+        fin_s = stepped.get_state(("Lambda", "ps", "tau"))
+        for f in fin_b:
+            assert np.array_equal(fin_b[f], fin_s[f]), f"{name}: the stepped chain left the batched one at {f}"
+        for c0, nc in [(0, 64), (p // 2 - 37, 101), (p - 70, 70)]:
+            S = batched.get_sigma_cols(c0, nc)
+            cols = np.arange(c0, c0 + nc)
+            E = sum(_sigma_cols_expected(sm["Lambda"], sm["omega"], P, rho, cols, mcmc / thin) for sm in samples)
+            err = np.max(np.abs(S - E)) / np.max(np.abs(E))
+            assert err < 1e-12, f"{name}: batched stripe {c0}+{nc} rel err {err:.3e}"
+            # the stepped chain flushed one sample per run: same Sigmaout up to summation order
+            S1 = stepped.get_sigma_cols(c0, nc)
+            assert np.max(np.abs(S1 - S)) / np.max(np.abs(E)) < 1e-13
+    finally:
+        batched.close()
+        stepped.close()
