@@ -79,7 +79,10 @@ struct LamDraws { const double *NL, *Gpsi, *Gps; };
 // space — [0, n_ps) ps gammas, [n_ps, n_psi) psi gammas, [n_psi, n_all) normal pairs — walked
 // grid-stride by b_total blocks of LAM_GEN_THREADS behind the W tiles (VALU work in the slots
 // and issue cycles the streaming W pass leaves free)
-constexpr int LAM_GEN_THREADS = 256, LAM_GEN_BLOCKS = 160;
+#ifndef DCFM_LAM_GEN_BLOCKS
+#define DCFM_LAM_GEN_BLOCKS 160
+#endif
+constexpr int LAM_GEN_THREADS = 256, LAM_GEN_BLOCKS = DCFM_LAM_GEN_BLOCKS;
 struct LamGen { double *NL, *Gpsi, *Gps; int n_ps, n_psi, n_all, b_total; };
 inline int lam_gen_doubles(const Dims &d) { return 2 * d.G * d.P * d.K + d.G * d.P; }
 inline LamGen lam_gen_plan(const Dims &d, double *base) {

@@ -234,15 +234,30 @@ __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restric
     d2 y0[R], y1[R], ww[R], l0[R], l1[R];
     auto load = [&](int t, int k) {
         const int j = 8 * t;
+#ifdef DCFM_WP_NOY   // timing-only dev build: no Y stream
+        y0[k].x = (double)j; y0[k].y = (double)(j + 1); y1[k] = y0[k];
+#else
         y0[k] = *reinterpret_cast<const d2 *>(Y0 + j);
         if (MT == 2) y1[k] = *reinterpret_cast<const d2 *>(Y1 + j);
+#endif
+#ifdef DCFM_WP_NOL   // timing-only dev build: no Lambda / omega loads
+        ww[k].x = 1.0 + j; ww[k].y = 2.0; l0[k].x = 0.5 * j; l0[k].y = 0.25; l1[k] = l0[k];
+#else
         ww[k] = *reinterpret_cast<const d2 *>(wp + j);
         l0[k] = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q) * KW);
         l1[k] = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q + 1) * KW);
+#endif
     };
     auto mma = [&](int k) {
         const double b00 = ww[k].x * l0[k].x, b01 = ww[k].x * l0[k].y;
         const double b10 = ww[k].y * l1[k].x, b11 = ww[k].y * l1[k].y;
+#ifdef DCFM_WP_NOMMA   // timing-only dev build: the products as VALU FMAs
+        acc[0][0][0] = fma(b00, y0[k].x, acc[0][0][0]); acc[0][1][0] = fma(b01, y0[k].x, acc[0][1][0]);
+        acc[MT - 1][0][1] = fma(b00, y1[k].x, acc[MT - 1][0][1]); acc[MT - 1][1][1] = fma(b01, y1[k].x, acc[MT - 1][1][1]);
+        acc[0][0][2] = fma(b10, y0[k].y, acc[0][0][2]); acc[0][1][2] = fma(b11, y0[k].y, acc[0][1][2]);
+        acc[MT - 1][0][3] = fma(b10, y1[k].y, acc[MT - 1][0][3]); acc[MT - 1][1][3] = fma(b11, y1[k].y, acc[MT - 1][1][3]);
+        return;
+#endif
         acc[0][0] = mfma16x16x4(b00, y0[k].x, acc[0][0]);
         acc[0][1] = mfma16x16x4(b01, y0[k].x, acc[0][1]);
         if (MT == 2) {
@@ -866,7 +881,11 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
             x[u] = *reinterpret_cast<const d2 *>(Xp + (size_t)i * KW);
             z[u] = *reinterpret_cast<const d2 *>(Zp + (size_t)i * KW);
             if (!IS_E) {
+#ifdef DCFM_CP_NOY   // timing-only dev build: no Y stream
+                y[u].x = (double)i; y[u].y = (double)(i + 1);
+#else
                 y[u] = *reinterpret_cast<const d2 *>(Yp + (size_t)i * d.PP);
+#endif
             } else if (EXTRA) {   // eta of tile te, formed into y
                 const d2 xa = *reinterpret_cast<const d2 *>(Xa + (size_t)i * KW);
                 const d2 za = *reinterpret_cast<const d2 *>(Za + (size_t)i * KW);
@@ -886,10 +905,17 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
                 acc[0][0] = mfma16x16x4(a0, ep, acc[0][0]);
                 acc[1][0] = mfma16x16x4(a1, ep, acc[1][0]);
             } else {
+#ifdef DCFM_CP_NOMMA   // timing-only dev build: the products as one VALU FMA each
+                acc[0][0][u] = fma(a0, e0, acc[0][0][u]);
+                acc[0][1][u] = fma(a0, e1, acc[0][1][u]);
+                acc[1][0][u] = fma(a1, e0, acc[1][0][u]);
+                acc[1][1][u] = fma(a1, e1, acc[1][1][u]);
+#else
                 acc[0][0] = mfma16x16x4(a0, e0, acc[0][0]);
                 acc[0][1] = mfma16x16x4(a0, e1, acc[0][1]);
                 acc[1][0] = mfma16x16x4(a1, e0, acc[1][0]);
                 acc[1][1] = mfma16x16x4(a1, e1, acc[1][1]);
+#endif
             }
         }
     };
@@ -1227,6 +1253,10 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
     const int i0 = rb * 64 * MT + wave * 16 * MT;
     d4 acc[MT][2];
     wpass_acc<KP, MT>(d, b.Y, b.Lam, b.omega, m, i0, 0, acc, [] {});
+#ifdef DCFM_WP_NOZ   // timing-only dev build: the W pass without the Z draw (Z, S stale)
+    if (acc[0][0][0] == 1.2345e300) b.Z[i0] = acc[0][1][0] + acc[MT - 1][0][1] + acc[MT - 1][1][2];
+    return;
+#endif
     // the operators are normally out long before the pass ends; their loads and the rows' X are
     // issued first, the first tile's normals drawn while they are in flight
     wait_count(b.sync + SYNC_ZM + m, zm_epoch);
@@ -1269,9 +1299,32 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
     }
 }
 
+#ifdef DCFM_WSTAMPS   // dev build: per-block [start, end] (s_memrealtime, 100 MHz) of the last full k_wcol
+__device__ unsigned long long g_wstamps[8192][2];
+extern "C" int dcfm_debug_wstamps(unsigned long long *out, int nblocks) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), (size_t)nblocks * 16, 0, hipMemcpyDeviceToHost);
+}
+#endif
+__device__ __forceinline__ void wcol_body(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, int ops, int colsum,
+                                          int wpass, unsigned long long ops_epoch, int xchol, const LamGen &lg,
+                                          double *smem);
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_wcol(Dims d, Bufs b, DrawsDev dr, int64_t iter, int ops, int colsum,
                                               int wpass, unsigned long long ops_epoch, int xchol, LamGen lg) {
     __shared__ double smem[PREP_SMEM];
+#ifdef DCFM_WSTAMPS
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    wcol_body(d, b, dr, iter, ops, colsum, wpass, ops_epoch, xchol, lg, smem);
+#ifdef DCFM_WSTAMPS
+    if (wpass && threadIdx.x == 0 && blockIdx.x < 8192) {
+        g_wstamps[blockIdx.x][0] = t0;
+        g_wstamps[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+}
+__device__ __forceinline__ void wcol_body(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, int ops, int colsum,
+                                          int wpass, unsigned long long ops_epoch, int xchol, const LamGen &lg,
+                                          double *smem) {
     const int G = d.G, nxs = xsum_blocks(G), chunk = G / nxs;
     unsigned long long *chunk_ctr = b.sync + 2;   // per chunk of shards: A_m published
     int blk = blockIdx.x;
@@ -1378,6 +1431,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         blk -= nw;
     }
     // the loading-row variates of this iteration (generated chain), behind every other role
+#ifdef DCFM_WP_NOLG   // timing-only dev build: no loading-row variates (stale)
+    return;
+#endif
     if (blk < lg.b_total) lam_draws(d, lg, iter, blk * LAM_GEN_THREADS + (int)threadIdx.x, lg.b_total * LAM_GEN_THREADS);
 }
 

@@ -10,29 +10,71 @@ namespace dcfm {
 
 // The loading-row variates of one iteration (dc:142 zlam, dc:150 psi gammas, dc:170 ps
 // gamma) into k_lambda's buffer layout, at the counters every other path draws them from
-// (k_draws, dcfm_rng_fill): thread gtid of gthreads takes variates gtid, gtid + gthreads, ...
-// of the index space (ps gammas, psi gammas, normal pairs).  Runs as extra blocks of k_wcol
-// (behind the W tiles) so the loading-row kernel reads its variates instead of drawing them.
+// (k_draws, dcfm_rng_fill).  Runs as extra blocks of k_wcol (behind the W tiles) so the
+// loading-row kernel reads its variates instead of drawing them.  Thread gtid of gthreads walks
+// each index range — ps gammas (m, j), psi gammas (m, j, k), normal pairs (m, j, pair) — grid-
+// stride, LAM_ILP independent variates per step: one variate is a chain of dependent Philox
+// rounds and transcendental steps, so a thread drawing them one after another is latency-bound
+// (block stamps at c3: 160 such blocks took 35 us alone, the long pole of k_wcol); the
+// branch-free shapes (psi gammas of integer shape, Box-Muller pairs) run LAM_ILP chains side by
+// side.  Every variate keeps its counter and formula: the same values as rng.gamma / normal2.
+#ifndef DCFM_LAM_ILP
+#define DCFM_LAM_ILP 4
+#endif
+constexpr int LAM_ILP = DCFM_LAM_ILP;
 __device__ __forceinline__ void lam_draws(const Dims &d, const LamGen &lg, int64_t iter, int gtid, int gthreads) {
     const Rng rng(d.seed);
     const uint32_t it = (uint32_t)iter;
     const int kp2 = (d.K + 1) / 2;
-    for (int x = gtid; x < lg.n_all; x += gthreads) {
-        if (x < lg.n_ps) {                                 // (m, j)
-            const int m = x / d.P, j = x - m * d.P;
-            lg.Gps[x] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, (uint32_t)(d.shard0 + m), (uint32_t)j, 0u, it);
-        } else if (x < lg.n_psi) {                         // (m, j, k)
-            const int y = x - lg.n_ps;
+    for (int x = gtid; x < lg.n_ps; x += gthreads) {   // (m, j): Marsaglia-Tsang, rejection loop
+        const int m = x / d.P, j = x - m * d.P;
+        lg.Gps[x] = rng.gamma(d.as_ + 0.5 * d.n, SITE_PS, (uint32_t)(d.shard0 + m), (uint32_t)j, 0u, it);
+    }
+    const double sh = d.df * 0.5 + 0.5;
+    const int npsi = lg.n_psi - lg.n_ps;
+    if (sh == 1.0 || sh == 2.0) {   // rng.gamma's integer-shape branch: -log(u1 [* u2]), no rejection
+        for (int y0 = gtid; y0 < npsi; y0 += LAM_ILP * gthreads) {
+            double u[LAM_ILP];
+#pragma unroll
+            for (int t = 0; t < LAM_ILP; ++t) {
+                const int y = y0 + t * gthreads, yc = y < npsi ? y : 0;
+                const int mj = yc / d.K, k = yc - mj * d.K, m = mj / d.P, j = mj - m * d.P;
+                const u32x4 a = rng.raw(SITE_PSI, (uint32_t)(d.shard0 + m), (uint32_t)j,
+                                        0x80000000u | (((uint32_t)k & 0x7FFFFFu) << 8), it);
+                const double u1 = u01_53(a.x, a.y);
+                u[t] = sh == 1.0 ? u1 : u1 * u01_53(a.z, a.w);
+            }
+#pragma unroll
+            for (int t = 0; t < LAM_ILP; ++t) {
+                const int y = y0 + t * gthreads;
+                const double gv = -log_u01(u[t]);
+                if (y < npsi) lg.Gpsi[y] = gv;
+            }
+        }
+    } else {
+        for (int y = gtid; y < npsi; y += gthreads) {   // (m, j, k)
             const int mj = y / d.K, k = y - mj * d.K, m = mj / d.P, j = mj - m * d.P;
-            lg.Gpsi[y] = rng.gamma(d.df * 0.5 + 0.5, SITE_PSI, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)k, it);
-        } else {                                           // (m, j, pair)
-            const int y = x - lg.n_psi;
-            const int mj = y / kp2, q = y - mj * kp2, m = mj / d.P, j = mj - m * d.P;
-            double n0, n1;
-            rng.normal2(SITE_LAMBDA, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)q, it, n0, n1);
-            double *o = lg.NL + (size_t)mj * d.K + 2 * q;
-            o[0] = n0;
-            if (2 * q + 1 < d.K) o[1] = n1;
+            lg.Gpsi[y] = rng.gamma(sh, SITE_PSI, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)k, it);
+        }
+    }
+    const int nnp = lg.n_all - lg.n_psi;
+    for (int y0 = gtid; y0 < nnp; y0 += LAM_ILP * gthreads) {   // (m, j, pair)
+        double n0[LAM_ILP], n1[LAM_ILP];
+#pragma unroll
+        for (int t = 0; t < LAM_ILP; ++t) {
+            const int y = y0 + t * gthreads, yc = y < nnp ? y : 0;
+            const int mj = yc / kp2, q = yc - mj * kp2, m = mj / d.P, j = mj - m * d.P;
+            rng.normal2(SITE_LAMBDA, (uint32_t)(d.shard0 + m), (uint32_t)j, (uint32_t)q, it, n0[t], n1[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < LAM_ILP; ++t) {
+            const int y = y0 + t * gthreads;
+            if (y < nnp) {
+                const int mj = y / kp2, q = y - mj * kp2;
+                double *o = lg.NL + (size_t)mj * d.K + 2 * q;
+                o[0] = n0[t];
+                if (2 * q + 1 < d.K) o[1] = n1[t];
+            }
         }
     }
 }
