@@ -234,30 +234,15 @@ __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restric
     d2 y0[R], y1[R], ww[R], l0[R], l1[R];
     auto load = [&](int t, int k) {
         const int j = 8 * t;
-#ifdef DCFM_WP_NOY   // timing-only dev build: no Y stream
-        y0[k].x = (double)j; y0[k].y = (double)(j + 1); y1[k] = y0[k];
-#else
         y0[k] = *reinterpret_cast<const d2 *>(Y0 + j);
         if (MT == 2) y1[k] = *reinterpret_cast<const d2 *>(Y1 + j);
-#endif
-#ifdef DCFM_WP_NOL   // timing-only dev build: no Lambda / omega loads
-        ww[k].x = 1.0 + j; ww[k].y = 2.0; l0[k].x = 0.5 * j; l0[k].y = 0.25; l1[k] = l0[k];
-#else
         ww[k] = *reinterpret_cast<const d2 *>(wp + j);
         l0[k] = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q) * KW);
         l1[k] = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q + 1) * KW);
-#endif
     };
     auto mma = [&](int k) {
         const double b00 = ww[k].x * l0[k].x, b01 = ww[k].x * l0[k].y;
         const double b10 = ww[k].y * l1[k].x, b11 = ww[k].y * l1[k].y;
-#ifdef DCFM_WP_NOMMA   // timing-only dev build: the products as VALU FMAs
-        acc[0][0][0] = fma(b00, y0[k].x, acc[0][0][0]); acc[0][1][0] = fma(b01, y0[k].x, acc[0][1][0]);
-        acc[MT - 1][0][1] = fma(b00, y1[k].x, acc[MT - 1][0][1]); acc[MT - 1][1][1] = fma(b01, y1[k].x, acc[MT - 1][1][1]);
-        acc[0][0][2] = fma(b10, y0[k].y, acc[0][0][2]); acc[0][1][2] = fma(b11, y0[k].y, acc[0][1][2]);
-        acc[MT - 1][0][3] = fma(b10, y1[k].y, acc[MT - 1][0][3]); acc[MT - 1][1][3] = fma(b11, y1[k].y, acc[MT - 1][1][3]);
-        return;
-#endif
         acc[0][0] = mfma16x16x4(b00, y0[k].x, acc[0][0]);
         acc[0][1] = mfma16x16x4(b01, y0[k].x, acc[0][1]);
         if (MT == 2) {
@@ -881,11 +866,7 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
             x[u] = *reinterpret_cast<const d2 *>(Xp + (size_t)i * KW);
             z[u] = *reinterpret_cast<const d2 *>(Zp + (size_t)i * KW);
             if (!IS_E) {
-#ifdef DCFM_CP_NOY   // timing-only dev build: no Y stream
-                y[u].x = (double)i; y[u].y = (double)(i + 1);
-#else
                 y[u] = *reinterpret_cast<const d2 *>(Yp + (size_t)i * d.PP);
-#endif
             } else if (EXTRA) {   // eta of tile te, formed into y
                 const d2 xa = *reinterpret_cast<const d2 *>(Xa + (size_t)i * KW);
                 const d2 za = *reinterpret_cast<const d2 *>(Za + (size_t)i * KW);
@@ -905,17 +886,10 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
                 acc[0][0] = mfma16x16x4(a0, ep, acc[0][0]);
                 acc[1][0] = mfma16x16x4(a1, ep, acc[1][0]);
             } else {
-#ifdef DCFM_CP_NOMMA   // timing-only dev build: the products as one VALU FMA each
-                acc[0][0][u] = fma(a0, e0, acc[0][0][u]);
-                acc[0][1][u] = fma(a0, e1, acc[0][1][u]);
-                acc[1][0][u] = fma(a1, e0, acc[1][0][u]);
-                acc[1][1][u] = fma(a1, e1, acc[1][1][u]);
-#else
                 acc[0][0] = mfma16x16x4(a0, e0, acc[0][0]);
                 acc[0][1] = mfma16x16x4(a0, e1, acc[0][1]);
                 acc[1][0] = mfma16x16x4(a1, e0, acc[1][0]);
                 acc[1][1] = mfma16x16x4(a1, e1, acc[1][1]);
-#endif
             }
         }
     };
@@ -937,8 +911,8 @@ template <int KW> constexpr int cp_waves() { return 4; }
 // (and, several ranks, the packed gather) left, and its ~12 us chain of dependent steps would
 // otherwise be the long pole of k_xdraw
 // waves_per_eu(3): 164 VGPRs and no AGPRs (without it hipcc took 168 + 32 AGPRs, 2 waves per
-// SIMD); measured neutral at c3 and c4 (the pass is bound by its fp64 MFMA work, §4), kept
-// for the occupancy headroom
+// SIMD); measured neutral at c3 and c4 (42.4 vs 42.9 us, 132 vs 135 us), kept for the
+// occupancy headroom
 template <int KW, bool PS = false>
 __global__ __launch_bounds__(64 * cp_waves<KW>()) __attribute__((amdgpu_waves_per_eu(3))) void k_cpass(Dims d, const double *__restrict__ Y,
                                                               const double *__restrict__ X,
@@ -1253,10 +1227,6 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
     const int i0 = rb * 64 * MT + wave * 16 * MT;
     d4 acc[MT][2];
     wpass_acc<KP, MT>(d, b.Y, b.Lam, b.omega, m, i0, 0, acc, [] {});
-#ifdef DCFM_WP_NOZ   // timing-only dev build: the W pass without the Z draw (Z, S stale)
-    if (acc[0][0][0] == 1.2345e300) b.Z[i0] = acc[0][1][0] + acc[MT - 1][0][1] + acc[MT - 1][1][2];
-    return;
-#endif
     // the operators are normally out long before the pass ends; their loads and the rows' X are
     // issued first, the first tile's normals drawn while they are in flight
     wait_count(b.sync + SYNC_ZM + m, zm_epoch);
@@ -1431,9 +1401,6 @@ __device__ __forceinline__ void wcol_body(const Dims &d, const Bufs &b, const Dr
         blk -= nw;
     }
     // the loading-row variates of this iteration (generated chain), behind every other role
-#ifdef DCFM_WP_NOLG   // timing-only dev build: no loading-row variates (stale)
-    return;
-#endif
     if (blk < lg.b_total) lam_draws(d, lg, iter, blk * LAM_GEN_THREADS + (int)threadIdx.x, lg.b_total * LAM_GEN_THREADS);
 }
 

@@ -121,8 +121,8 @@ def test_batched_flush_full_size(dcfm, name, n, P, g, K):
             if it > burnin and it % thin == 0:
                 samples.append(stepped.get_state(("Lambda", "omega")))
         assert batched.saved_samples() == len(samples) == mcmc // thin
-        fin_b = batched.get_state(("Lambda", "ps", "tau"))
-        fin_s = stepped.get_state(("Lambda", "ps", "tau"))
+        fin_b = batched.get_state(("Lambda", "ps", "tauh"))
+        fin_s = stepped.get_state(("Lambda", "ps", "tauh"))
         for f in fin_b:
             assert np.array_equal(fin_b[f], fin_s[f]), f"{name}: the stepped chain left the batched one at {f}"
         for c0, nc in [(0, 64), (p // 2 - 37, 101), (p - 70, 70)]:
