@@ -94,6 +94,7 @@ def test_full_get_equals_stripes(dcfm):
 
 @pytest.mark.parametrize("name,n,P,g,K", [
     ("c3", 1000, 312, 64, 30),           # BASELINE configs[2] shape on one GPU
+    ("c5", 2000, 391, 256, 30),          # BASELINE configs[4]: two 40 GB lower-triangle Sigmas
 ])
 def test_batched_flush_full_size(dcfm, name, n, P, g, K):
     """The driver bench's assembly flush at full size (dc:180-196, Q8): burnin 0, MCMC 20,
