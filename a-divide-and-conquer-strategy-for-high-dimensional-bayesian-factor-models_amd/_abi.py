@@ -24,13 +24,15 @@ DCFM_FLAG_INJECT_DRAWS = 0x1
 DCFM_FLAG_UNFUSED = 0x2        # K <= 32 through the side-stream layout (same results)
 DCFM_FLAG_ONE_STREAM = 0x4     # every launch on one stream
 DCFM_FLAG_FLAT_PRIORITY = 0x8  # default priority for every stream
+DCFM_FLAG_COMM_SELF = 0x20   # one rank on the collective path with a real 1-rank RCCL communicator
+DCFM_FLAG_EXACT_RESIDUAL = 0x10  # ps / omega from the direct residual (dc:169), one more Y pass
 
 KERNEL_IDS = {
     "k_prep": 0, "k_wpass": 1, "k_zdraw": 2, "k_xred": 3, "k_xdraw": 4, "k_cpass": 5,
     "k_lambda": 6, "k_colsum": 7, "k_delta": 8, "k_save": 9, "k_assemble": 10, "rccl": 11,
-    "k_xchol": 12, "k_draws": 13,
+    "k_xchol": 12, "k_draws": 13, "k_resid": 14,
 }
-K_COUNT = 14
+K_COUNT = 15
 
 # every symbol include/dcfm.h declares
 EXPORTS = (

@@ -324,7 +324,7 @@ static int numeric_status(dcfm_handle *h) {
 // [invalid, numeric, other] failure counts to an all-reduce first; any failure anywhere
 // fails the call on all ranks (a rank that saw none reports which failure another rank had).
 static int agree(dcfm_handle *h, int code) {
-    if (h->d.nranks == 1) return code;
+    if (!h->d.coll) return code;
     const double f[3] = {code == DCFM_ERR_INVALID ? 1.0 : 0.0, code == DCFM_ERR_NUMERIC ? 1.0 : 0.0,
                          (code != DCFM_OK && code != DCFM_ERR_INVALID && code != DCFM_ERR_NUMERIC) ? 1.0 : 0.0};
     double g[3] = {0.0, 0.0, 0.0};
@@ -392,7 +392,7 @@ const char *dcfm_kernel_name(int id) {
     static const char *names[DCFM_K_COUNT] = {"k_prep",  "k_wpass", "k_zdraw",  "k_xred",
                                               "k_xdraw", "k_cpass", "k_lambda", "k_colsum",
                                               "k_delta", "k_save",  "k_assemble", "rccl", "k_xchol",
-                                              "k_draws"};
+                                              "k_draws", "k_resid"};
     return (id >= 0 && id < DCFM_K_COUNT) ? names[id] : "?";
 }
 
@@ -478,6 +478,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     Dims &d = h->d;
     d.n = c.n; d.P = c.P; d.g = c.g; d.K = c.K;
     d.nranks = nranks; d.rank = c.rank;
+    d.coll = (nranks > 1 || (c.flags & DCFM_FLAG_COMM_SELF)) ? 1 : 0;
     d.G = c.g / nranks;
     d.shard0 = c.rank * d.G;
     d.NP = round_up(c.n, 128);
@@ -492,7 +493,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     h->fused = d.kp == KP && !(c.flags & DCFM_FLAG_UNFUSED);
     // fused narrow chain on several ranks: column sums, the A sum and the X message travel in
     // ONE message per iteration (Dims::sgap / xstride)
-    const bool packed = nranks > 1 && h->fused;
+    const bool packed = d.coll && h->fused;
     d.sgap = packed ? KP * KP + d.NP * KP : 0;
     d.xstride = packed ? d.G * KP + KP * KP + d.NP * KP : d.kp * d.kp;
     h->B = c.asm_batch > 0 ? c.asm_batch : 32;
@@ -528,7 +529,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         b.xall = b.xa_all + KP * KP;
     } else {
         ALLOC(b.xin, NP * KP);
-        if (nranks > 1) { ALLOC(b.xall, (size_t)nranks * NP * KP); } else b.xall = b.xin;
+        if (d.coll) { ALLOC(b.xall, (size_t)nranks * NP * KP); } else b.xall = b.xin;
         ALLOC(b.xa, KP * KP);
         ALLOC(b.xa_all, (size_t)nranks * KP * KP);
     }
@@ -548,7 +549,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     ALLOC(b.cpart, G * PP * KP);
     if (!d.sgap) {
         ALLOC(b.sloc, G * KP);
-        if (nranks > 1) { ALLOC(b.sall, g * KP); } else b.sall = b.sloc;
+        if (d.coll) { ALLOC(b.sall, g * KP); } else b.sall = b.sloc;
     }
     ALLOC(b.Lb[0], p * (size_t)b.LDB);
     ALLOC(b.Lb[1], p * (size_t)b.LDB);
@@ -562,7 +563,8 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         b.T1 = h->Tb[c.rank + 1];
     }
     ALLOC(b.Sigma, (size_t)(tri(b.T1) - tri(b.T0)) * ASM_TILE * ASM_TILE);
-    // the generated fused chain: k_xdraw draws the loading-row variates into b.ldraw each iteration
+    // the generated fused chain: k_wcol's LAMGEN blocks draw the loading-row variates into b.ldraw
+    // each iteration (lam_draws)
     if (h->fused && !d.inject) ALLOC(b.ldraw, (size_t)lam_gen_doubles(d));
     if (!d.inject && !h->fused) {   // k_draws batches of the side-stream layouts
         const size_t K = c.K, n = c.n, P = c.P;
@@ -655,7 +657,7 @@ int dcfm_comm_unique_id(uint8_t out[128]) {
 
 int dcfm_comm_init(dcfm_handle *h, const uint8_t id[128]) {
     if (!h || !id) return fail(h, DCFM_ERR_INVALID, "null argument");
-    if (h->d.nranks == 1) return DCFM_OK;
+    if (!h->d.coll) return DCFM_OK;
     HIPC(h, hipSetDevice(h->cfg.device));
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
@@ -1015,7 +1017,7 @@ static int flush_batch(dcfm_handle *h) {
     const int lb = h->lb;
     HIPC(h, hipEventRecord(h->e_batch, h->stream));
     HIPC(h, hipStreamWaitEvent(h->sasm, h->e_batch, 0));
-    if (d.nranks > 1) {
+    if (d.coll) {
         KTimer t(h, DCFM_K_COMM, h->sasm);
         const size_t rows = (size_t)d.G * d.P;
         if (!h->loop) NCCLC(h, ncclGroupStart());
@@ -1054,7 +1056,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     if (first_iter < 1 || n_iter < 0) return fail(h, DCFM_ERR_INVALID, "iterations are 1-based");
     Dims &d = h->d;
     Bufs &b = h->b;
-    if (d.nranks > 1 && !h->comm_ok) return fail(h, DCFM_ERR_INVALID, "dcfm_comm_init first (nranks > 1)");
+    if (d.coll && !h->comm_ok) return fail(h, DCFM_ERR_INVALID, "dcfm_comm_init first (nranks > 1 or COMM_SELF)");
     if (d.inject) {
         if (!h->dr.NZ) return fail(h, DCFM_ERR_INVALID, "INJECT_DRAWS set but no draws");
         if (first_iter < h->dr.first_iter || first_iter + n_iter > h->dr.first_iter + h->dr.n_iter)
@@ -1077,7 +1079,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     // message].  Then k_xdraw = [X operators (several ranks), delta chain of t-1] beside the X
     // draw.  k_wcol also draws the loading-row variates of t (generated chain).  The last
     // iteration's chain runs after the loop (k_delta).
-    const bool wc = fused && d.nranks == 1;
+    const bool wc = fused && !d.coll;
     bool delta_pending = false;           // k_lambda of it - 1 ran, its delta chain not yet queued
     auto after_delta = [&]() {            // iteration it - 1 is complete
         h->cur ^= 1;
@@ -1125,8 +1127,8 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     };
     // Generated draws (Philox, counter-addressed): the fused K <= 32 chain (any rank count) draws
     // its variates where they are consumed (Z / X normals, the delta gammas) or in the launch
-    // before (k_lambda's normals and gammas: extra blocks of k_xdraw, whose row blocks leave most
-    // CUs idle); the other paths read k_draws buffers generated a batch ahead on the draw stream
+    // before (k_lambda's normals and gammas: the LAMGEN blocks of k_wcol, behind its W tiles); the
+    // other paths read k_draws buffers generated a batch ahead on the draw stream
     const bool gen_draws = !d.inject && !fused;
     int slot = -1;
     int64_t batch0 = first_iter, batch_n = 0;
@@ -1163,7 +1165,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             { KTimer t(h, DCFM_K_PREP, ss); launch_prep(d, b, ss); }
             HIPC(h, hipEventRecord(h->e_prep, ss));
             { KTimer t(h, DCFM_K_XCHOL, ss); launch_asum(d, b, ss); }
-            if (d.nranks > 1) {
+            if (d.coll) {
                 KTimer t(h, DCFM_K_COMM, ss);
                 if (int rc = coll_allgather(h, CH_SIDE, b.xa, b.xa_all, KW * KW, ss)) return rc;
             }
@@ -1174,13 +1176,13 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             HIPC(h, hipStreamWaitEvent(s, h->e_prep, 0));
             { KTimer t(h, DCFM_K_ZDRAW, s);  launch_zdraw(d, b, dr, it, s); }
             { KTimer t(h, DCFM_K_XRED, s);   launch_xred(d, b, s); }
-            if (d.nranks > 1) {
+            if (d.coll) {
                 KTimer t(h, DCFM_K_COMM, s);
                 if (int rc = coll_allgather(h, CH_MAIN, b.xin, b.xall, (size_t)d.NP * KW, s)) return rc;
             }
             HIPC(h, hipStreamWaitEvent(s, h->e_xchol, 0));
         }
-        if (fused && d.nranks > 1) {   // several ranks: + the X factorisation
+        if (fused && d.coll) {   // several ranks: + the X factorisation
             KTimer t(h, DCFM_K_XDRAW, s);
             h->xm_ops += 1;
             launch_xdraw_mr(d, b, dr, it, h->xm_ops, s);
@@ -1208,13 +1210,17 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             KTimer t(h, DCFM_K_LAMBDA, s);
             launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, lamgen);
         }
+        if (h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL) {   // ps, omega by dc:169's direct residual
+            KTimer t(h, DCFM_K_RESID, s);
+            launch_resid(d, b, dr, it, s, lamgen);
+        }
         h->plam_valid = false;
         if (fused) {
             delta_pending = true;     // column sums + delta chain ride in the next iteration's launches
         } else {
             HIPC(h, hipEventRecord(h->e_lam, s));
             { KTimer t(h, DCFM_K_COLSUM, s); launch_colsum(d, b, s); }
-            if (d.nranks > 1) {
+            if (d.coll) {
                 KTimer t(h, DCFM_K_COMM, s);
                 if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.sall, (size_t)d.G * KW, s)) return rc;
             }
@@ -1254,7 +1260,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     if (delta_pending) {   // the last iteration's column sums (+ their gather) and delta chain
         KTimer t(h, DCFM_K_DELTA, s);
         launch_wcol(d, b, h->dr, end_iter - 1, false, true, false, 0, s);
-        if (d.nranks > 1)
+        if (d.coll)
             if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)) return rc;
         const DrawsDev &dr = d.inject ? h->dr : h->gen[0];   // gammas drawn in place unless injected
         launch_delta(d, b, dr, end_iter - 1, b.delta + h->cur * nkg, b.tau + h->cur * nkg,
@@ -1325,29 +1331,45 @@ int dcfm_get_sigma_cols(dcfm_handle *h, int64_t col0, int64_t ncols, double *out
     else if (col0 < 0 || ncols < 0 || col0 + ncols > d.p)
         code = fail(h, DCFM_ERR_INVALID, "columns [%lld, %lld) outside 0..p = %d", (long long)col0,
                     (long long)(col0 + ncols), d.p);
-    HIPC(h, hipSetDevice(h->cfg.device));
+    // every failure before the gather -- arguments, device, state, scratch allocation -- is folded
+    // into `code` and agreed on: every rank enters the gather, or none (no rank left blocked in it)
+    if (code == DCFM_OK) {
+        const hipError_t e = hipSetDevice(h->cfg.device);
+        if (e != hipSuccess) code = fail(h, DCFM_ERR_HIP, "get_sigma_cols: %s", hipGetErrorString(e));
+    }
     sync_all(h);
     if (code == DCFM_OK) code = numeric_status(h);
-    if (int rc = agree(h, code)) return rc;     // every rank enters the gather, or none
-    if (ncols == 0) return DCFM_OK;
     const int nr = d.nranks;
     const long long p = d.p, c0 = col0, c1 = col0 + ncols;
     // every rank's packed-window count for this stripe (known to all ranks: no size exchange)
     std::vector<long long> cnt(nr), base(nr);
     long long tot = 0;
-    for (int k = 0; k < nr; ++k) {
-        const long long R0 = std::min<long long>(p, (long long)h->Tb[k] * ASM_TILE);
-        const long long R1 = std::min<long long>(p, (long long)h->Tb[k + 1] * ASM_TILE);
-        cnt[k] = win_off(c1, c0, R0, R1);
-        base[k] = tot;
-        tot += cnt[k];
-    }
-    if (tot != p * ncols) return fail(h, DCFM_ERR_INVALID, "sigma_cols: windows cover %lld of %lld", tot, p * ncols);
     const bool is_root = d.rank == root;
-    // root: [recv (all ranks' windows, own part packed in place) | dense stripe]; others: own windows
-    const size_t ndev = is_root ? (nr > 1 ? 2 * (size_t)tot : (size_t)tot) : (size_t)std::max<long long>(cnt[d.rank], 1);
     void *q = nullptr;
-    HIPC(h, hipMalloc(&q, ndev * sizeof(double)));
+    if (code == DCFM_OK && ncols > 0) {
+        for (int k = 0; k < nr; ++k) {
+            const long long R0 = std::min<long long>(p, (long long)h->Tb[k] * ASM_TILE);
+            const long long R1 = std::min<long long>(p, (long long)h->Tb[k + 1] * ASM_TILE);
+            cnt[k] = win_off(c1, c0, R0, R1);
+            base[k] = tot;
+            tot += cnt[k];
+        }
+        if (tot != p * ncols) code = fail(h, DCFM_ERR_INVALID, "sigma_cols: windows cover %lld of %lld", tot, p * ncols);
+    }
+    if (code == DCFM_OK && ncols > 0) {
+        // root: [recv (all ranks' windows, own part packed in place) | dense stripe]; others: own windows
+        const size_t ndev = is_root ? (nr > 1 ? 2 * (size_t)tot : (size_t)tot) : (size_t)std::max<long long>(cnt[d.rank], 1);
+        const hipError_t e = hipMalloc(&q, ndev * sizeof(double));
+        if (e != hipSuccess) {
+            q = nullptr;
+            code = fail(h, DCFM_ERR_ALLOC, "get_sigma_cols: %zu doubles of scratch: %s", ndev, hipGetErrorString(e));
+        }
+    }
+    if (int rc = agree(h, code)) {
+        if (q) (void)hipFree(q);
+        return rc;
+    }
+    if (ncols == 0) return DCFM_OK;
     double *buf = static_cast<double *>(q);
     double *mine = is_root ? buf + base[d.rank] : buf;
     int rc = DCFM_OK;
@@ -1458,20 +1480,28 @@ int dcfm_sigma_error(dcfm_handle *h, const double *U, int32_t r, const double *s
     if (!sdiag || !out || (r > 0 && !U)) code = fail(h, DCFM_ERR_INVALID, "null argument");
     else if (r < 0 || r > 32) code = fail(h, DCFM_ERR_INVALID, "truth rank r = %d outside 0..32", r);
     else if (iters < 0) code = fail(h, DCFM_ERR_INVALID, "iters = %d < 0", iters);
-    HIPC(h, hipSetDevice(h->cfg.device));
+    if (code == DCFM_OK) {
+        const hipError_t e = hipSetDevice(h->cfg.device);
+        if (e != hipSuccess) code = fail(h, DCFM_ERR_HIP, "sigma_error: %s", hipGetErrorString(e));
+    }
     sync_all(h);
     if (code == DCFM_OK) code = numeric_status(h);
-    if (int rc = agree(h, code)) return rc;     // the all-reduces below run on every rank, or on none
     const Dims &d = h->d;
     const int p = d.p;
     const size_t P = (size_t)p;
     const int m = std::min<int>(iters, p);
     double *dev = nullptr;
     const size_t ns = (size_t)sigma_err_splits(p);
-    {
+    if (code == DCFM_OK) {   // scratch before agree(): an allocation failure fails the call on every rank
         void *q = nullptr;
-        HIPC(h, hipMalloc(&q, (P * (size_t)std::max(r, 1) + 5 * P + 3 * ns * P) * sizeof(double)));
-        dev = static_cast<double *>(q);
+        const size_t nd = P * (size_t)std::max(r, 1) + 5 * P + 3 * ns * P;
+        const hipError_t e = hipMalloc(&q, nd * sizeof(double));
+        if (e != hipSuccess) code = fail(h, DCFM_ERR_ALLOC, "sigma_error: %zu doubles of scratch: %s", nd, hipGetErrorString(e));
+        else dev = static_cast<double *>(q);
+    }
+    if (int rc = agree(h, code)) {   // the all-reduces below run on every rank, or on none
+        if (dev) (void)hipFree(dev);
+        return rc;
     }
     // U, s, v, then the summed outputs y | fro | tru (contiguous), then the split partials
     double *dU = dev, *ds = dU + P * std::max(r, 1), *dv = ds + P, *dy = dv + P, *dfro = dy + P, *dtru = dfro + P;
@@ -1492,7 +1522,7 @@ int dcfm_sigma_error(dcfm_handle *h, const double *U, int32_t r, const double *s
         launch_sigma_err(h->b.Sigma, p, dU, r, ds, vh ? dv : nullptr, h->b.T0, h->b.T1, first, vh ? py : nullptr,
                          pfro, ptru, dy, h->stream);
         if (!hip_ok(hipGetLastError(), "launch")) return false;
-        if (d.nranks > 1) {
+        if (d.coll) {
             if (vh && (rc = coll_allreduce_sum(h, CH_ASM, dy, P, h->stream))) return false;
             if (first && (rc = coll_allreduce_sum(h, CH_ASM, dfro, P, h->stream))) return false;
             if (first && (rc = coll_allreduce_sum(h, CH_ASM, dtru, P, h->stream))) return false;

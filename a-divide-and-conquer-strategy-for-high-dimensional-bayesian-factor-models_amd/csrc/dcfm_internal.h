@@ -52,6 +52,8 @@ struct Dims {
     int NP, PP;                 // padded rows / cols
     int shard0;                 // first global shard of this rank
     int nranks, rank;
+    int coll;                   // the collective (multi-rank) data path: nranks > 1, or one rank with
+                                // a real RCCL communicator (DCFM_FLAG_COMM_SELF)
     int p;                      // P * g
     int kp;                     // padded factor width KW of every [..][KW] array: 32, 64 or 128
     double rho, sr, s1r;        // rho, sqrt(rho), sqrt(1-rho)
@@ -183,6 +185,9 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &d
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, const double *plam_src, hipStream_t s, bool gen = false);
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s);
+// resid.hip (DCFM_FLAG_EXACT_RESIDUAL): ps, omega from the direct residual Yd - eta Lambda'
+// (dc:169-171), after the loading-row kernel, with its ps variates (gen: b.ldraw, else dr)
+void launch_resid(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s, bool gen);
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                   const double *delta_in, const double *tau_in, double *delta_out,
                   double *tau_out, hipStream_t s);

@@ -770,8 +770,11 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
     }
     if (sw < nch) {
         if (chunk >= 2) {   // lane c sums part c / XD_ROWS (a canonical subtree) of the chunk for row c % XD_ROWS
+            // the parts split only a power-of-two chunk (np | chunk, each part a canonical
+            // subtree); a chunk of any other size (xdraw_chunks: nch = 1, chunk = nsrc, e.g.
+            // g = 5 or 10 shards) is summed whole by the h == 0 lanes
             constexpr int NPART = 16 / XD_ROWS;
-            const int np = chunk < NPART ? chunk : NPART, per = chunk / np;
+            const int np = (chunk & (chunk - 1)) ? 1 : (chunk < NPART ? chunk : NPART), per = chunk / np;
             const int rr = c % XD_ROWS, h = c / XD_ROWS;
             const bool rl = i0 + rr < d.n && h < np;
             const double *p = src + (size_t)(sw * chunk + (h < np ? h : 0) * per) * stride +
@@ -1693,7 +1696,7 @@ void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
     const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / (64 * (3 - wmode))) * d.G : 0);
     if (nb + lg.b_total == 0) return;
     hipLaunchKernelGGL(k_wcol, dim3(nb + lg.b_total), dim3(256), 0, s, d, b, dr, iter, ops ? 1 : 0, colsum ? 1 : 0,
-                       wpass ? wmode : 0, ops_epoch, d.nranks == 1 ? 1 : 0, lg);
+                       wpass ? wmode : 0, ops_epoch, d.coll ? 0 : 1, lg);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
     const int total = d.NP * d.kp;
@@ -1704,7 +1707,7 @@ void launch_asum(const Dims &d, const Bufs &b, hipStream_t s) {
 }
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
     if (d.kp != KP) return wide::launch_xchol(d, b, s);
-    hipLaunchKernelGGL(k_xchol, dim3(1), dim3(256), 0, s, d, d.nranks > 1 ? b.xa_all : b.xa, b.XM);
+    hipLaunchKernelGGL(k_xchol, dim3(1), dim3(256), 0, s, d, d.coll ? b.xa_all : b.xa, b.XM);
 }
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s,
                   bool from_shards) {
@@ -1751,7 +1754,7 @@ void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t ite
                    const double *tau_cur, const double *plam_src, hipStream_t s, bool gen) {
     if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, plam_src, s);
     LamDraws ld;
-    if (gen) {   // this iteration's variates, drawn by k_xdraw
+    if (gen) {   // this iteration's variates, drawn by k_wcol's LAMGEN blocks (lam_draws)
         const LamGen g = lam_gen_plan(d, b.ldraw);
         ld.NL = g.NL; ld.Gpsi = g.Gpsi; ld.Gps = g.Gps;
     } else {     // [T][g][P][K] / [T][g][P] draw buffers: this iteration, this rank's first shard

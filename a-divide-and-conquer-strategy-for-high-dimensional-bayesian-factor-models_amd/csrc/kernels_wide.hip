@@ -694,7 +694,7 @@ void launch_prep(const Dims &d, const Bufs &b, hipStream_t s) {
 }
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
     WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_xchol<KW>, dim3(1), dim3(256), 0, s, d,
-                                           d.nranks > 1 ? b.xa_all : b.xa, b.XM));
+                                           d.coll ? b.xa_all : b.xa, b.XM));
 }
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_zdraw<KW>, dim3((d.NP / (16 * ZD_RT)) * d.G), dim3(256), 0, s, d, b.W, b.A,

@@ -1,6 +1,5 @@
 // Loading-row kernel of the narrow (K <= 32) chain and the generator of its variates
-// (divideconquer.m:140-145, 150, 156, 169-171), shared by kernels.hip and the dev harness
-// tools/lambench.
+// (divideconquer.m:140-145, 150, 156, 169-171), included by kernels.hip.
 #pragma once
 #include "dcfm_internal.h"
 #include "philox.h"

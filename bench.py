@@ -59,6 +59,8 @@ def algorithmic_work(kname, d, n_launch_samples, fused_z=False):
         return float(p) * (p + 1) * n_launch_samples * K / nr, 16.0 * p * (p + 1) / 2 / nr, "mfma"
     if kname == "k_lambda":   # per row: read C, psi, NL, Gpsi (K each), ps, yy, Gps; write Lam, psi, cpart, ps, omega
         return G * P * (K ** 3 / 3.0 + 6.0 * K * K), 8.0 * G * P * (7 * K + 5), "mfma"
+    if kname == "k_resid":    # dc:169 Ytil = Y - eta L': read Y, X, Z, L, Gps; write ps, omega
+        return 2.0 * G * n * P * K, 8.0 * (G * n * P + n * K + G * n * K + G * P * K + 3 * G * P), "hbm"
     if kname == "k_zdraw":
         return G * n * (4.0 * K * K + 2.0 * K * K), 8.0 * G * n * 4 * K, "hbm"
     return 0.0, 0.0, "hbm"
@@ -90,7 +92,8 @@ def build_id():
 def config_key(args, world):
     """The bench invocation a PMC summary must match (workload, flush sizes, step counts)."""
     return (f"g{args.g}_P{args.P}_n{args.n}_K{args.K}_thin{args.thin}_asm{args.asm_batch}_"
-            f"steps{args.steps}_warmup{args.warmup}_gpus{world}{'_chains' if args.chains else ''}")
+            f"steps{args.steps}_warmup{args.warmup}_gpus{world}{'_chains' if args.chains else ''}"
+            f"{'_exact' if args.exact_residual else ''}")
 
 
 # HIP-event role name -> the kernel rocprofv3 records it under (the fused K <= 32 chain's W pass
@@ -197,6 +200,9 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--no-faithful", action="store_true", help="skip the faithful-loop CPU leg (~30 s)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--exact-residual", action="store_true",
+                    help="DCFM_FLAG_EXACT_RESIDUAL: ps / omega from dc:169's direct residual (k_resid, one "
+                         "more Y pass) instead of the SS identity; the parity mode, timed for its cost")
     ap.add_argument("--chains", action="store_true",
                     help="one independent chain per rank (config c4: parallel chains, seed 1 + rank, no "
                          "collectives; weak scaling) instead of splitting the shards of one chain")
@@ -260,7 +266,7 @@ def main():
 
     smp = dcfm.Sampler(n, P, g, K, rho, burnin, mcmc, thin, seed=1 + (rank if chains else 0),
                        nranks=shard_ranks, rank=0 if chains else rank, device=device,
-                       asm_batch=args.asm_batch)
+                       asm_batch=args.asm_batch, flags=0x10 if args.exact_residual else 0)
     if shard_ranks > 1:
         obj = [dcfm.Sampler.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
@@ -455,7 +461,8 @@ def main():
         "higher_is_better": True, "scaling": "weak" if chains else "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (sparse factor model, seed 20161209; initial state dc:68-87 drawn on the device)",
         "config": {"workload": f"{wtag}: p={p} (P={P} x g={g}), n={n}, K={K} (k={K * g}), rho={rho}, "
-                               f"thin={thin}, burnin=0 (assembly in timed region), asm_batch={args.asm_batch}",
+                               f"thin={thin}, burnin=0 (assembly in timed region), asm_batch={args.asm_batch}"
+                               f"{', exact residual (k_resid)' if args.exact_residual else ''}",
                    "global_batch": n,
                    "parallelism": f"chains{world} (1 per GPU)" if chains else f"shards{g}/gpus{world}"},
         "roofline": roof,

@@ -53,6 +53,14 @@ extern "C" {
                                         same results (tests, diagnostics)           */
 #define DCFM_FLAG_ONE_STREAM   0x4u  /* every launch on one stream (isolated timings) */
 #define DCFM_FLAG_FLAT_PRIORITY 0x8u /* default priority for every stream          */
+#define DCFM_FLAG_COMM_SELF    0x20u  /* one rank through the collective data path with a
+                                        real one-rank RCCL communicator (dcfm_comm_init):
+                                        exercises the RCCL calls on a one-GPU box; same
+                                        results as the plain one-rank chain (tests)        */
+#define DCFM_FLAG_EXACT_RESIDUAL 0x10u /* ps / omega (dc:169-171) from the direct residual
+                                        sum((Yd - eta*Lambda').^2), one extra pass over Y
+                                        (k_resid), instead of the SS identity inside the
+                                        loading-row kernel (parity runs)   */
 
 typedef struct dcfm_handle dcfm_handle;
 
@@ -216,7 +224,8 @@ int  dcfm_get_trace(dcfm_handle *h, double *out, int64_t *count);
 #define DCFM_K_COMM     11
 #define DCFM_K_XCHOL    12
 #define DCFM_K_DRAWS    13   /* on-device Philox variates of the next iteration (side stream) */
-#define DCFM_K_COUNT    14
+#define DCFM_K_RESID    14   /* direct-residual ps / omega (DCFM_FLAG_EXACT_RESIDUAL) */
+#define DCFM_K_COUNT    15
 int  dcfm_set_profiling(dcfm_handle *h, int enable);
 /* Time only the kernels whose bit (1u << DCFM_K_*) is set: two events per timed
  * launch cost host time, so a throughput run times just the kernel it reports. */

@@ -82,7 +82,7 @@ def update_eta(st: SamplerState, rho):
 
 
 def loading_systems(st: SamplerState, D: Data, d: IterDraws):
-    """The loading rows' systems of dc:137-144 from the state after the eta update:
+    r"""The loading rows' systems of dc:137-144 from the state after the eta update:
     E (g x K x K, dc:138), C = eta'Y (g x P x K), Q_j = ps_j E + diag(Plam_j) (dc:141),
     b_j = ps_j C_j, L_j = chol(Q_j, 'lower') (dc:142) and the draws z_j (all g x P x ...).
     Lambda_j = L_j' \ (L_j \ b_j + z_j) solves Q_j Lambda_j = b_j + L_j z_j exactly."""
@@ -101,8 +101,17 @@ def loading_systems(st: SamplerState, D: Data, d: IterDraws):
     return E, C, Q, b, L, z
 
 
-def update_Lambda_psi_delta_ps(st: SamplerState, D: Data, hyper: Hyper, d: IterDraws, lam_given=None):
-    """dc:136-172 batched; SS_j by the identity (no residual pass over Y).  ``lam_given``
+def residual_ss(D: Data, st: SamplerState, lam):
+    """dc:169 as the reference writes it: sum_i (Yd - eta Lambda')_ij^2 per shard (g x P)."""
+    eta = np.moveaxis(st.eta, 2, 0)                                  # g x n x K
+    R = D.Ys - eta @ np.swapaxes(lam, 1, 2)                          # g x n x P
+    return np.einsum("mij,mij->mj", R, R)
+
+
+def update_Lambda_psi_delta_ps(st: SamplerState, D: Data, hyper: Hyper, d: IterDraws, lam_given=None,
+                               direct=False):
+    """dc:136-172 batched; SS_j by the identity (no residual pass over Y), or with ``direct``
+    by dc:169's residual (residual_ss: the library's DCFM_FLAG_EXACT_RESIDUAL).  ``lam_given``
     (P x K x g, MATLAB layout) replaces the loading draw: the rest of the update is then
     applied to that Lambda (stage-wise parity checks of an implementation's later stages)."""
     g, n, P = D.Ys.shape
@@ -118,8 +127,11 @@ def update_Lambda_psi_delta_ps(st: SamplerState, D: Data, hyper: Hyper, d: IterD
     st.psi[...] = (1.0 / (hyper.df / 2 + 0.5 * (st.Lambda ** 2 * tau))) * d.Gpsi
     # delta / tau (dc:155-165)
     update_delta_tau(st, hyper, d)
-    # ps (dc:169-171): SS = yy - 2 lam.C + lam E lam'
-    SS = D.yy - 2.0 * np.einsum("mjk,mjk->mj", lam, C) + np.einsum("mjk,mkl,mjl->mj", lam, E, lam)
+    # ps (dc:169-171): SS = yy - 2 lam.C + lam E lam'  (or the residual itself)
+    if direct:
+        SS = residual_ss(D, st, lam)
+    else:
+        SS = D.yy - 2.0 * np.einsum("mjk,mjk->mj", lam, C) + np.einsum("mjk,mkl,mjl->mj", lam, E, lam)
     st.ps[:, 0, :] = ((1.0 / (hyper.bs + 0.5 * SS)) * d.Gps.T).T
     st.omega[...] = 1.0 / st.ps[:, 0, :]
 
@@ -144,11 +156,11 @@ def update_Plam(st: SamplerState):
     st.Plam[...] = st.psi * st.tauh[:, 0, :][None, :, :]
 
 
-def gibbs_iteration(st: SamplerState, Yd, rho, hyper: Hyper, d: IterDraws):
+def gibbs_iteration(st: SamplerState, Yd, rho, hyper: Hyper, d: IterDraws, direct=False):
     D = _as_data(Yd)
     update_ZX(st, D, rho, d)
     update_eta(st, rho)
-    update_Lambda_psi_delta_ps(st, D, hyper, d)
+    update_Lambda_psi_delta_ps(st, D, hyper, d, direct=direct)
     update_Plam(st)
     return st
 
@@ -175,15 +187,16 @@ def full(SigLower):
 
 
 def run_chain(Yd, st: SamplerState, rho, hyper: Hyper, draws, first_iter, n_iter,
-              burnin, mcmc, thin, SigLower=None):
-    """Returns the lower-triangle accumulator (Fortran order); ``full()`` mirrors it."""
+              burnin, mcmc, thin, SigLower=None, direct=False):
+    """Returns the lower-triangle accumulator (Fortran order); ``full()`` mirrors it.
+    ``direct``: SS_j of dc:169 by the residual itself (see update_Lambda_psi_delta_ps)."""
     D = _as_data(Yd)
     g, n, P = D.Ys.shape
     effsamp = mcmc / thin
     if SigLower is None:
         SigLower = np.zeros((P * g, P * g), order="F")
     for it in range(first_iter, first_iter + n_iter):
-        gibbs_iteration(st, D, rho, hyper, draws(it))
+        gibbs_iteration(st, D, rho, hyper, draws(it), direct=direct)
         if it % thin == 0 and it > burnin:
             assemble_lower(SigLower, st, rho, effsamp)
     return SigLower

@@ -74,9 +74,13 @@ def stagewise_errors(start, got, Yd, rho, hyper, draws, check_lambda=None):
         oracle's systems (Q_j, b_j, L_j, z_j) built from got's eta -- cond(Q_j) reaches ~1e7 at
         c1/c2, where two restatements' forward errors differ by cond x eps (see
         tests/test_gpu_parity_configs.py);
-      * every later stage (psi, delta/tau, ps, omega, Plam; dc:149-177) vs the oracle update
-        applied to got's own Lambda, relative (ps, omega per row and relative to the
-        conditioning kappa_j of the residual identity they are computed by).
+      * every later stage (psi, delta/tau, Plam; dc:149-165, 174-177) vs the oracle update applied
+        to got's own Lambda, relative;
+      * ps, omega (dc:168-172) per row, unscaled relative, vs the faithful loop's update
+        (oracle/dc_oracle.py update_ps: the reference's direct residual Yd - eta Lambda') applied
+        to got's own eta and Lambda.  The library meets this with DCFM_FLAG_EXACT_RESIDUAL at
+        every shape; its default SS identity cancels where SS_j is small against its terms
+        (resid.hip header), e.g. 1.3e-10 at config c2's second iteration.
     `got` maps state fields to MATLAB-layout arrays (Sampler.get_state, or an oracle state's
     as_dict()).  Returns ({field: rel err}, lambda backward error, the oracle state after the
     iteration with got's Lambda)."""
@@ -90,22 +94,18 @@ def stagewise_errors(start, got, Yd, rho, hyper, draws, check_lambda=None):
         getattr(st, f)[...] = np.asarray(got[f], dtype=np.float64).reshape(getattr(st, f).shape)
     E, C, Q, b, L, z = V.loading_systems(st, D, draws)
     bw = loading_backward_error(got["Lambda"], Q, b, L, z)
-    # ps_j (dc:169-171) from SS_j = yy_j - 2 lam_j.C_j + lam_j E lam_j': evaluating that sum (the
-    # oracle's and the kernels' identity, or the reference's direct residual) carries the condition
-    # number kappa_j = (yy_j + 2 sum_k |lam_jk C_jk| + sum_kl |lam_jk E_kl lam_jl|) / SS_j (up to
-    # ~1e6 at c2's second iteration, where the |X| excursions make E large), so its rows are
-    # compared relative to kappa_j: a forward-error bound, no second implementation involved
-    lam = np.moveaxis(np.asarray(got["Lambda"], dtype=np.float64), 2, 0)   # g x P x K
-    ss = D.yy - 2.0 * np.einsum("mjk,mjk->mj", lam, C) + np.einsum("mjk,mkl,mjl->mj", lam, E, lam)
-    alc = np.einsum("mjk,mjk->mj", np.abs(lam), np.abs(C))
-    alel = np.einsum("mjk,mkl,mjl->mj", np.abs(lam), np.abs(E), np.abs(lam))
-    kappa = np.maximum(1.0, (D.yy + 2.0 * alc + alel) / np.abs(ss)).T         # P x g
     V.update_Lambda_psi_delta_ps(st, D, hyper, draws, lam_given=got["Lambda"])
     V.update_Plam(st)
     for f in ("psi", "delta", "tauh", "Plam"):
         errs[f] = rel_err(got[f], getattr(st, f))
+    F.update_ps(st, D.Yd, hyper, draws)      # dc:169-171 as written, on got's eta and Lambda
     for f in ("ps", "omega"):
-        a = np.asarray(got[f], dtype=np.float64).reshape(kappa.shape)
-        r = np.asarray(getattr(st, f), dtype=np.float64).reshape(kappa.shape)
-        errs[f] = float(np.max(np.abs(a - r) / np.abs(r) / kappa))
+        errs[f] = elem_rel_err(got[f], getattr(st, f))
     return errs, bw, st
+
+
+def elem_rel_err(a, b):
+    """max_i |a_i - b_i| / |b_i| (per element, unscaled)."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64).reshape(a.shape)
+    return float(np.max(np.abs(a - b) / np.abs(b))) if b.size else 0.0

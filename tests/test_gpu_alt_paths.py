@@ -45,7 +45,8 @@ UNFUSED, ONE_STREAM = 0x2, 0x4
 
 
 @pytest.mark.parametrize("flags,case", [(UNFUSED, "basic"), (UNFUSED, "K30"), (ONE_STREAM, "K30"),
-                                        (UNFUSED | ONE_STREAM, "basic")])
+                                        (UNFUSED | ONE_STREAM, "basic"),
+                                        (UNFUSED, "g5_odd_chunk"), (UNFUSED, "g10_odd_chunk")])
 def test_alternate_path_parity(flags, case):
     import test_gpu_parity as T
     if case not in T.CASES:

@@ -86,7 +86,9 @@ def _check_blocks(out, p, n):
         assert out[r]["Sig"] is None
 
 
-@pytest.mark.parametrize("n,g,K,nobs,p", [(2, 4, 5, 40, 60), (4, 8, 6, 50, 96), (2, 4, 40, 60, 120)])
+# (5, 10, ...): five ranks, so k_xdraw sums a non-power-of-two run of rank messages
+@pytest.mark.parametrize("n,g,K,nobs,p", [(2, 4, 5, 40, 60), (4, 8, 6, 50, 96), (2, 4, 40, 60, 120),
+                                         (5, 10, 5, 40, 100)])
 def test_loopback_ranks_match_oracle(dcfm, n, g, K, nobs, p):
     burnin, mcmc, thin = 1, 4, 2
     c = make_case(nobs, p, g, K, seed=13)

@@ -100,3 +100,45 @@ def test_ranks_match_oracle(tmp_path, gpu_available):
     for f in ("Lambda", "ps", "omega", "psi", "Plam", "Z", "eta"):
         both = np.concatenate([r[k][f] for k in range(world)], axis=-1)
         assert rel_err(both, getattr(ref, f)) < 1e-10, f
+
+
+COMM_SELF = 0x20   # DCFM_FLAG_COMM_SELF
+
+
+@pytest.mark.parametrize("K,flags", [(5, 0), (30, 0), (40, 0), (5, 0x2)])   # fused, fused c3 width, wide, unfused
+def test_one_rank_rccl_communicator(dcfm, K, flags):
+    """RCCL on a ONE-GPU box: a one-rank chain with DCFM_FLAG_COMM_SELF takes the collective data
+    path (packed all-gather per iteration, side / assembly all-gathers, agree()'s all-reduce in
+    get_sigma and the Lanczos all-reduces of sigma_error) through a real one-rank RCCL
+    communicator (ncclGetUniqueId, ncclCommInitRank, ncclCommSplit x 2, ncclAllGather,
+    ncclAllReduce).  Its results must be bitwise those of the plain one-rank chain, which skips
+    every collective; the 'rccl' kernel-stat counter proves the calls ran."""
+    from helpers import make_case, stacked_draws, state_dict
+    n, p, g, burnin, mcmc, thin = 40, 256, 4, 1, 4, 2
+    c = make_case(n, p, g, K, seed=21)
+    N = burnin + mcmc
+    draws = stacked_draws(c["src"], 1, N)
+    _, _, L0, s2 = __import__("oracle").synth.make_data(n, p, k0=4, factors=True)
+    U, s = dcfm.truth_factors(L0, s2, c["Y"], c["keep"], c["init"].varind)
+    out = []
+    for f in (flags, flags | COMM_SELF):
+        smp = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], burnin, mcmc, thin, inject_draws=True, flags=f)
+        try:
+            if f & COMM_SELF:
+                smp.comm_init(dcfm.Sampler.unique_id())
+            smp.set_data(c["Yd"])
+            smp.set_state({k: v for k, v in state_dict(c["st"]).items() if k != "eta"})
+            smp.set_draws(draws, 1, N)
+            smp.set_profiling_kernels(["rccl"])
+            smp.run(1, N)
+            comm = smp.kernel_stats()["rccl"][1]
+            got = smp.get_state()
+            got["Sig"] = smp.get_sigma()
+            got["err"] = np.array([v for v in smp.sigma_error(U, s, iters=20).values()])
+            out.append((got, comm))
+        finally:
+            smp.close()
+    (plain, c0), (rccl, c1) = out
+    assert c0 == 0 and c1 >= N, (c0, c1)
+    for f in plain:
+        assert np.array_equal(plain[f], rccl[f]), f"{f} differs with the one-rank RCCL communicator"

@@ -146,7 +146,8 @@ def test_faithful_vs_vectorised_at_baseline_shapes(name, n, p, g, K, iters):
     the faithful per-row loop (the reference's loop structure, dc:97-177) AT those shapes, with
     absolute bars: every iteration starts both restatements from the same state, and
     tests/helpers.stagewise_errors checks the stages before the loading solve and after it at
-    1e-12 relative and the loading draw by its per-row backward error (<= 1e-14) -- at c2's
+    1e-12 relative (ps / omega per row, unscaled, against the faithful residual update) and the
+    loading draw by its per-row backward error (<= 1e-14) -- at c2's
     second iteration cond(Q_j) ~ 1e7 makes the two restatements' Lambda differ by ~1e-9 in
     forward error while both solve their systems to machine precision."""
     from helpers import stagewise_errors
@@ -161,7 +162,13 @@ def test_faithful_vs_vectorised_at_baseline_shapes(name, n, p, g, K, iters):
         for f, e in errs.items():
             assert e < 1e-12, (name, it, f, e)
         assert bw < 1e-14, (name, it, bw)
-        V.gibbs_iteration(st, D, c["rho"], c["hyper"], d)
+        # the vectorised chain with dc:169's residual (the GPU's DCFM_FLAG_EXACT_RESIDUAL
+        # reference): its ps / omega against the faithful update on its own eta and Lambda
+        vec = st.copy()
+        V.gibbs_iteration(vec, D, c["rho"], c["hyper"], d, direct=True)
+        errs, bw, _ = stagewise_errors(st, vec.as_dict(), D, c["rho"], c["hyper"], d)
+        assert errs["ps"] < 1e-12 and errs["omega"] < 1e-12, (name, it, errs["ps"], errs["omega"])
+        st = vec
 
 
 def test_posterior_mean_recovers_truth():
