@@ -74,7 +74,12 @@ struct dcfm_handle {
                e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
     bool fused = false;           // K <= 32 fused launch chain (else the side-stream layout), fixed at create
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
-    unsigned long long wc_ops = 0;   // k_wcol launches with the operator roles (hand-off counter epoch)
+    int64_t lg_iter[2] = {-1, -1};   // iteration whose loading-row variates b.ldraw[slot] holds (generated
+                                     // fused chain; counter-based, so valid whatever the state)
+    unsigned long long wc_ops = 0;   // Z-operator computations scheduled (k_wcol's OPS blocks or k_lambda's OPS
+                                     // role): the epoch of their hand-off counters
+    unsigned long long lam_ops = 0;  // k_lambda launches with the OPS role (epoch of its row-block counters)
+    int64_t ops_iter = -1;           // iteration whose Z operators the last k_lambda computed (A, ZM out)
     unsigned long long xm_ops = 0;   // k_xdraw launches with the X-operator role (several ranks; its counter's epoch)
     bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
@@ -541,7 +546,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         ALLOC(tk, 1);
         b.ticket = reinterpret_cast<unsigned *>(tk);
         double *sy = nullptr;
-        ALLOC(sy, SYNC_ZM + G);           // zeroed: the hand-off counters start at 0 (<= 255 chunks, G shards)
+        ALLOC(sy, SYNC_ZM + 2 * G);       // zeroed: the hand-off counters start at 0 (<= 255 chunks, G shards x 2)
         b.sync = reinterpret_cast<unsigned long long *>(sy);
     }
     ALLOC(b.C, G * PP * KP);
@@ -563,9 +568,12 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         b.T1 = h->Tb[c.rank + 1];
     }
     ALLOC(b.Sigma, (size_t)(tri(b.T1) - tri(b.T0)) * ASM_TILE * ASM_TILE);
-    // the generated fused chain: k_wcol's LAMGEN blocks draw the loading-row variates into b.ldraw
-    // each iteration (lam_draws)
-    if (h->fused && !d.inject) ALLOC(b.ldraw, (size_t)lam_gen_doubles(d));
+    // the generated fused chain: k_lambda's LAMGEN blocks draw the next iteration's loading-row
+    // variates into b.ldraw[(it + 1) & 1] (lam_draws)
+    if (h->fused && !d.inject) {
+        ALLOC(b.ldraw[0], (size_t)lam_gen_doubles(d));
+        ALLOC(b.ldraw[1], (size_t)lam_gen_doubles(d));
+    }
     if (!d.inject && !h->fused) {   // k_draws batches of the side-stream layouts
         const size_t K = c.K, n = c.n, P = c.P;
         const size_t nz = K * n * g, nx = K * n, nl = K * P * g, gpsi = P * K * g, gdel = K * g, gps = P * g;
@@ -785,6 +793,7 @@ int dcfm_init_state(dcfm_handle *h) {
     HIPC(h, hipGetLastError());
     HIPC(h, hipStreamSynchronize(h->stream));
     h->cur = 0;
+    h->ops_iter = -1;          // the Z operators follow the new Lambda, omega
     h->plam_valid = true;      // Plam = psi o tau' was formed (dc:86), as set_state's caller Plam
     h->have_state = true;
     return reset_numeric(h);
@@ -921,6 +930,7 @@ int dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s) {
     h->cur = 0;
     k_to_dev(d, s->delta, v);   if ((rc = up(h, h->b.delta, v))) return rc;
     k_to_dev(d, s->tauh, v);    if ((rc = up(h, h->b.tau, v))) return rc;
+    h->ops_iter = -1;
     h->plam_valid = true;
     h->have_state = true;
     return reset_numeric(h);
@@ -1072,7 +1082,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     // (k_wcol, k_xdraw); K > 32 (or DCFM_FLAG_UNFUSED): prep and the X operators run on the
     // side stream
     const bool fused = h->fused;
-    const bool lamgen = fused && !d.inject;   // k_wcol draws k_lambda's variates (b.ldraw)
+    const bool lamgen = fused && !d.inject;   // k_lambda draws the next iteration's variates (b.ldraw)
     // fused (K <= 32): per iteration t, k_wcol = [Z operators and shard sum of A of t, column
     // sums of t-1] beside the W pass of t, whose tiles draw Z; one rank: the last chunk also
     // factors Xprec.  Several ranks: k_xred and ONE all-gather of [column sums | A sum | X
@@ -1143,18 +1153,24 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             if (it + batch_n < end_iter && gen_batch(it + batch_n, slot) < 0) return rc_gen;   // next batch
         }
         const DrawsDev &dr = d.inject ? h->dr : h->gen[gen_draws ? slot : 0];
+        if (lamgen && h->lg_iter[it & 1] != it) {   // not drawn ahead by the previous k_lambda
+            KTimer t(h, DCFM_K_DRAWS, s);
+            launch_lamgen(d, b, it, s);
+            h->lg_iter[it & 1] = it;
+        }
+        // the Z operators: from the previous k_lambda's OPS role, else k_wcol's own OPS blocks
+        const int ops_mode = (h->ops_iter == it) ? 2 : 1;
+        if (fused && ops_mode == 1) h->wc_ops += 1;
         if (wc) {   // k_wcol: + the Z draw of the W tiles' rows
             KTimer t(h, DCFM_K_WPASS, s);
-            h->wc_ops += 1;
-            launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s, lamgen);
+            launch_wcol(d, b, dr, it, ops_mode, delta_pending, true, h->wc_ops, s);
         } else if (fused) {   // several ranks: k_wcol (W pass + Z draw, no X factorisation), k_xred
                               // (the local X message), then ONE all-gather of [column sums of it - 1
                               // | local A sum | X message]; k_xdraw factors Xprec from the ranks' A
                               // sums, runs the delta chain of it - 1 and draws X
             {
                 KTimer t(h, DCFM_K_WPASS, s);
-                h->wc_ops += 1;
-                launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s, lamgen);
+                launch_wcol(d, b, dr, it, ops_mode, delta_pending, true, h->wc_ops, s);
             }
             { KTimer t(h, DCFM_K_XRED, s); launch_xred(d, b, s); }
             KTimer t(h, DCFM_K_COMM, s);
@@ -1208,7 +1224,17 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         }
         {
             KTimer t(h, DCFM_K_LAMBDA, s);
-            launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, lamgen);
+            // fused: the launch's tail also computes the next iteration's Z operators (not with the
+            // exact residual, whose omega comes after)
+            const bool lops = fused && !(h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL);
+            if (lops) {
+                h->wc_ops += 1;
+                h->lam_ops += 1;
+            }
+            launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, lamgen,
+                          lops ? h->lam_ops : 0);
+            if (lamgen) h->lg_iter[(it + 1) & 1] = it + 1;
+            h->ops_iter = lops ? it + 1 : -1;
         }
         if (h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL) {   // ps, omega by dc:169's direct residual
             KTimer t(h, DCFM_K_RESID, s);
