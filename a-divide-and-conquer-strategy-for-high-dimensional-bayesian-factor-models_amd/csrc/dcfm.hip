@@ -85,6 +85,7 @@ struct dcfm_handle {
     int cur = 0;                  // delta/tau buffer in use
     int lb = 0;                   // Lb buffer being filled
     int B = 16;                   // saved samples per flush
+    int tail = 1;                 // eager flush once this many saved samples of a call remain (< 0: off)
     int batch = 0;                // saved samples pending in Lb[lb]
     int64_t saved = 0;
     bool have_data = false, have_state = false;
@@ -502,6 +503,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     d.sgap = packed ? KP * KP + d.NP * KP : 0;
     d.xstride = packed ? d.G * KP + KP * KP + d.NP * KP : d.kp * d.kp;
     h->B = c.asm_batch > 0 ? c.asm_batch : 32;
+    h->tail = c.asm_tail == 0 ? 1 : (c.asm_tail < 0 ? -1 : c.asm_tail);
 
     Bufs &b = h->b;
     const size_t G = d.G, NP = d.NP, PP = d.PP, g = d.g, p = d.p, KP = d.kp;
@@ -1020,6 +1022,13 @@ int dcfm_set_draws(dcfm_handle *h, const dcfm_draws_view *dv, int64_t first_iter
 }
 
 // Hand the filled Lb[lb] batch to the assembly stream (overlaps the next iterations).
+// saved iterations t in (a, b] (dc:180: mod(t, thin) == 0 && t > BURNIN)
+static int64_t saves_in(const dcfm_handle *h, int64_t a, int64_t b) {
+    const int64_t th = h->cfg.thin, lo = std::max<int64_t>(a, h->cfg.burnin);
+    if (b <= lo) return 0;
+    return b / th - lo / th;
+}
+
 static int flush_batch(dcfm_handle *h) {
     if (h->batch == 0) return DCFM_OK;
     Dims &d = h->d;
@@ -1277,7 +1286,10 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             HIPC(h, hipGetLastError());
             h->batch += 1;
             h->saved += 1;
-            if (h->batch == h->B) {
+            // eager tail flush: the samples saved so far go out now, on the assembly stream beside
+            // the call's remaining iterations, so the call's closing flush holds only the last `tail`
+            const bool eager = h->tail >= 0 && h->batch > h->tail && saves_in(h, it, end_iter - 1) == h->tail;
+            if (h->batch == h->B || eager) {
                 int rc = flush_batch(h);
                 if (rc) return rc;
             }

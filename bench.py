@@ -93,7 +93,7 @@ def config_key(args, world):
     """The bench invocation a PMC summary must match (workload, flush sizes, step counts)."""
     return (f"g{args.g}_P{args.P}_n{args.n}_K{args.K}_thin{args.thin}_asm{args.asm_batch}_"
             f"steps{args.steps}_warmup{args.warmup}_gpus{world}{'_chains' if args.chains else ''}"
-            f"{'_exact' if args.exact_residual else ''}")
+            f"{'_exact' if args.exact_residual else ''}{f'_tail{args.asm_tail}' if args.asm_tail else ''}")
 
 
 # HIP-event role name -> the kernel rocprofv3 records it under (the fused K <= 32 chain's W pass
@@ -162,12 +162,12 @@ def cpu_baseline_run(n, p, g, K, rho, steps=5, thin=5):
     Yd, st, src, hyper = _cpu_case(n, p, g, K, rho)
     D = V.Data(Yd)
     t0 = time.perf_counter()
-    V.run_chain(D, st, rho, hyper, src.iteration, 1, steps, 0, steps, thin)
+    V.run_chain(D, st, rho, hyper, src.iteration, 1, steps, 0, steps, thin, direct=True)
     dt = time.perf_counter() - t0
     return {"value": steps / dt, "unit": "iter/s", "cores": int(_threads()), "kind": "port",
             "sample": f"{steps} Gibbs iterations of c3 (incl. {steps // thin} covariance assembly at thin={thin} "
                       f"and the draw generation), vectorised NumPy/OpenBLAS restatement of divideconquer.m:90-196 "
-                      f"(not MATLAB), {dt:.1f} s"}
+                      f"with dc:169's residual product as written (not MATLAB), {dt:.1f} s"}
 
 
 def cpu_faithful_run(n, p, g, K, rho):
@@ -192,6 +192,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--thin", type=int, default=5)
     ap.add_argument("--asm-batch", type=int, default=96)
+    ap.add_argument("--asm-tail", type=int, default=0,
+                    help="dcfm_config.asm_tail: 0 = library default (eager flush when one saved sample of the "
+                         "run remains), -1 = off")
     ap.add_argument("--g", type=int, default=64)
     ap.add_argument("--P", type=int, default=312)
     ap.add_argument("--n", "--nobs", dest="n", type=int, default=1000)   # --nobs under torchrun (--n is ambiguous there)
@@ -266,7 +269,7 @@ def main():
 
     smp = dcfm.Sampler(n, P, g, K, rho, burnin, mcmc, thin, seed=1 + (rank if chains else 0),
                        nranks=shard_ranks, rank=0 if chains else rank, device=device,
-                       asm_batch=args.asm_batch, flags=0x10 if args.exact_residual else 0)
+                       asm_batch=args.asm_batch, flags=0x10 if args.exact_residual else 0, asm_tail=args.asm_tail)
     if shard_ranks > 1:
         obj = [dcfm.Sampler.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
