@@ -1233,19 +1233,20 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         }
         {
             KTimer t(h, DCFM_K_LAMBDA, s);
-            // fused: the launch's tail also computes the next iteration's Z operators (not with the
-            // exact residual, whose omega comes after)
-            const bool lops = fused && !(h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL);
+            // fused: the launch's tail also computes the next iteration's Z operators; exact residual:
+            // every row block takes ps, omega from dc:169's residual (K <= 32 in k_lambda itself)
+            const bool exact = h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL;
+            const bool lops = fused;
             if (lops) {
                 h->wc_ops += 1;
                 h->lam_ops += 1;
             }
             launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, lamgen,
-                          lops ? h->lam_ops : 0);
+                          lops ? h->lam_ops : 0, exact ? 0.0 : KAPPA_IDENTITY_MAX);
             if (lamgen) h->lg_iter[(it + 1) & 1] = it + 1;
             h->ops_iter = lops ? it + 1 : -1;
         }
-        if (h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL) {   // ps, omega by dc:169's direct residual
+        if ((h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL) && d.kp != KP) {   // wide: dc:169's residual, own launch
             KTimer t(h, DCFM_K_RESID, s);
             launch_resid(d, b, dr, it, s, lamgen);
         }

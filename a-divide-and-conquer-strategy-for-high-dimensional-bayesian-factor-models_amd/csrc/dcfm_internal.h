@@ -190,10 +190,13 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &d
 // chain) instead of the draw buffers dr (injected draws, k_draws batches), and its LAMGEN blocks
 // (behind the loading rows, in the launch's tail) draw iteration iter + 1's into the other slot
 // ops_epoch > 0 (fused chain): the launch's OPS role computes the next iteration's Z operators (A_m,
-// ZM_m) and signals the hand-off counters as k_wcol's OPS blocks would, as the ops_epoch-th such launch
+// ZM_m) and signals the hand-off counters as k_wcol's OPS blocks would, as the ops_epoch-th such launch.
+// K <= 32: a row block whose SS identity may be off by more than ~kappa_max eps (lambda.h guard) takes
+// ps, omega from dc:169's direct residual instead (resid.h); kappa_max = 0: every block (exact mode)
+constexpr double KAPPA_IDENTITY_MAX = 1e3;
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, const double *plam_src, hipStream_t s, bool gen = false,
-                   unsigned long long ops_epoch = 0);
+                   unsigned long long ops_epoch = 0, double kappa_max = KAPPA_IDENTITY_MAX);
 // the generated fused chain's loading-row variates of iteration iter into b.ldraw[iter & 1] on
 // their own (a run's first iteration when the previous k_lambda did not draw them)
 void launch_lamgen(const Dims &d, const Bufs &b, int64_t iter, hipStream_t s);

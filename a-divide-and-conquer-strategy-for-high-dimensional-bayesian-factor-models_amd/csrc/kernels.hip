@@ -1775,7 +1775,8 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &d
     }
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
-                   const double *tau_cur, const double *plam_src, hipStream_t s, bool gen, unsigned long long ops_epoch) {
+                   const double *tau_cur, const double *plam_src, hipStream_t s, bool gen, unsigned long long ops_epoch,
+                   double kappa_max) {
     if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, plam_src, s);
     LamDraws ld;
     LamGen next = {};     // gen: the next iteration's variates, drawn in the launch's tail
@@ -1800,7 +1801,7 @@ void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t ite
     const dim3 grid(nrb * d.G + ops.nops + next.b_total);
 #define LAUNCH_LAM(KE)                                                                                       \
     hipLaunchKernelGGL(k_lambda<KE>, grid, dim3(64 * LAM_WAVES), 0, s, d, b.C, b.E, b.yy, tau_cur, b.Lam, b.psi, \
-                       plam_src, b.ps, b.omega, b.cpart, ld, nrb, next, iter + 1, ops)
+                       plam_src, b.ps, b.omega, b.cpart, ld, nrb, next, iter + 1, ops, b.Y, b.X, b.Z, kappa_max)
     // the factor width rounded up to an instantiated one (rows >= K are identity padding)
     if (d.K <= 8) LAUNCH_LAM(8);
     else if (d.K <= 16) LAUNCH_LAM(16);

@@ -4,6 +4,7 @@
 #include "dcfm_internal.h"
 #include "philox.h"
 #include "linalg.h"
+#include "resid.h"
 
 namespace dcfm {
 
@@ -165,7 +166,9 @@ __global__ __launch_bounds__(64 * LAM_WAVES) __attribute__((amdgpu_waves_per_eu(
                                                const double *__restrict__ plam_src, double *__restrict__ ps,
                                                double *__restrict__ omega, double *__restrict__ cpart,
                                                LamDraws ld, int nrb, LamGen next, int64_t next_iter,
-                                               LamOps ops) {
+                                               LamOps ops, const double *__restrict__ Y,
+                                               const double *__restrict__ X, const double *__restrict__ Z,
+                                               double kappa_max) {
     static_assert(KE % 2 == 0 && KE >= 2 && KE <= KP, "even factor width");
     constexpr int NB = (KE + 7) / 8;
     // LDS: double-buffered image [2][8 systems][KP + 1 (bank spread)][2] | rhs image [2][8][KP+2] |
@@ -173,8 +176,9 @@ __global__ __launch_bounds__(64 * LAM_WAVES) __attribute__((amdgpu_waves_per_eu(
     constexpr int LSN = 2 * LAM_ROWS * (KP + 1) * 2, BSN = 2 * LAM_ROWS * (KP + 2), VSN = LAM_ROWS * (KP + 2);
     constexpr int EP = KP + 2;
     static_assert(KP * EP <= LSN + BSN, "E staging fits the image area");
-    constexpr int WSN = LSN + BSN + 2 * VSN;   // one wave's LDS
+    constexpr int WSN = LSN + BSN + 2 * VSN + KP;   // one wave's LDS (+ sqrt(diag E_m) for the guard)
     __shared__ __attribute__((aligned(16))) double SMB[LAM_WAVES * WSN];
+    __shared__ int exact_blk;                       // some row of the block needs dc:169's residual
     static_assert(LAM_WAVES * WSN >= PREP_SMEM_DOUBLES, "the OPS role's LDS fits the block's");
     const int blk = (int)blockIdx.x, nrow = nrb * d.G;
     if (blk >= nrow) {
@@ -192,8 +196,11 @@ __global__ __launch_bounds__(64 * LAM_WAVES) __attribute__((amdgpu_waves_per_eu(
     double(*LS)[LAM_ROWS][KP + 1][2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 1][2]>(SM);
     double(*BS)[LAM_ROWS][KP + 2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 2]>(SM + LSN);
     double *Vs = SM + LSN + BSN, *Is = Vs + VSN;
+    double *Dg = SM + LSN + BSN + 2 * VSN;          // sqrt(E_m[k][k])
     double *Es = SM;
     const int m = blk / nrb, mg = d.shard0 + m;
+    if (threadIdx.x == 0) exact_blk = 0;
+    __syncthreads();
     const int lane = threadIdx.x & 63, grp = lane >> 3, l = lane & 7;
     Vs += grp * (KP + 2);
     Is += grp * (KP + 2);
@@ -251,7 +258,10 @@ __global__ __launch_bounds__(64 * LAM_WAVES) __attribute__((amdgpu_waves_per_eu(
         }
 #pragma unroll
         for (int c = 8 * b; c < nc; ++c)
-            if (c == l + 8 * b) q[c] += dg[b];
+            if (c == l + 8 * b) {
+                if (grp == 0) Dg[c] = sqrt(q[c]);          // E_m is the wave's, whatever the row
+                q[c] += dg[b];
+            }
     });
     __builtin_amdgcn_wave_barrier();
     // image of column pair (0, 1) (overwrites E's staging: every read of it is above)
@@ -438,6 +448,18 @@ __global__ __launch_bounds__(64 * LAM_WAVES) __attribute__((amdgpu_waves_per_eu(
     double contrib = (ww - px - 2.0 * wv) * ipsj;
     contrib = valid ? contrib : 0.0;
     contrib = rowsum8(contrib);
+    // ---- guard: the identity's rounding error is ~ kappa_j eps with kappa_j = (yy_j + 2 sum_k |x_k C_jk|
+    //      + |x|'|E||x|) / SS_j <= (sqrt(yy_j) + s_j)^2 / SS_j, s_j = sum_k |x_k| sqrt(E_kk) (|C_jk| <=
+    //      sqrt(E_kk yy_j) and |E_kl| <= sqrt(E_kk E_ll), E a Gram matrix).  Beyond kappa_max (or SS_j <= 0)
+    //      the block's 32 rows take dc:169's residual instead (resid_tile below)
+    double sabs = 0.0;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) sabs = fma(fabs(x[b]), Dg[l + 8 * b < KE ? l + 8 * b : 0], sabs);
+    sabs = rowsum8(sabs);
+    {
+        const double SS = yyj + contrib, rt = sqrt(yyj) + sabs;
+        if (valid && l == 0 && !(SS > 0.0 && rt * rt <= kappa_max * SS)) exact_blk = 1;   // benign race: all store 1
+    }
     // ---- psi (dc:150, tau of the previous iteration, Q11) and the outputs
     if (valid) {
 #pragma unroll
@@ -448,12 +470,17 @@ __global__ __launch_bounds__(64 * LAM_WAVES) __attribute__((amdgpu_waves_per_eu(
             cpart[rowoff + r] = ps_b * (x[b] * x[b]);               // mat = psijh .* Lambda.^2 (dc:156)
             if (rv[b]) psi[rowoff + r] = ps_b;
         }
-        if (l == 0) {
-            const double SS = yyj + contrib;
-            const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;     // dc:170
-            ps[(uint32_t)(m * d.PP + j)] = psn;
-            st_agent(omega + (uint32_t)(m * d.PP + j), 1.0 / psn);  // dc:171 (Q1)
-        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // Lambda out (agent scope) before the vote
+    __syncthreads();
+    if (exact_blk) {   // dc:169 as written for the block's 32 rows: Ytil = Yd - eta Lambda', sum(Ytil.^2)
+        resid_tile<KP, true>(d, Y, X, Z, Lam, ld.Gps, ps, omega, m,
+                             (blk - m * nrb) * LAM_WAVES * LAM_ROWS, reinterpret_cast<double(*)[32]>(SMB));
+    } else if (valid && l == 0) {
+        const double SS = yyj + contrib;
+        const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;     // dc:170
+        st_agent(ps + (uint32_t)(m * d.PP + j), psn);
+        st_agent(omega + (uint32_t)(m * d.PP + j), 1.0 / psn);  // dc:171 (Q1)
     }
     if (ops.nops) {   // this block's rows of shard m are out (their stores complete, agent scope)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -102,12 +102,16 @@ def test_multi_iteration_run_c2_shape(dcfm, flags):
     run.  The start is a stationary state (200 generated-draw iterations on the device, read
     back with get_state) -- the initial state's second iteration is ill-conditioned at c2
     (tests/test_gpu_parity_configs.py), a stationary chain is not; both chains then consume the
-    same injected draws for 6 iterations (thin 2: samples 2, 4, 6, one flush)."""
+    same injected draws for 6 iterations (thin 2: samples 2, 4, 6, one flush).  The reference
+    sampler itself makes occasional long X excursions (quirks Q1 / Q2; e.g. oracle draw seed
+    15, Philox seeds 11 and 22 at this shape: max|X| 1e3-1e7, cond(Q_j) ~ 1e11), where any two
+    implementations part ways; the warm-up seed is one whose chain is stationary, and the test
+    checks that it is (max|X| < 10)."""
     from oracle import SamplerState
     from oracle import vectorised as V
     c = make_case(500, 5000, 8, 20, seed=29, k0=10, dense_truth=False)
     g, K = 8, 20
-    warm = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], 1000, 0, 1, seed=11)
+    warm = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], 1000, 0, 1, seed=12)
     try:
         warm.set_data(c["Yd"])
         warm.set_state({f: v for f, v in state_dict(c["st"]).items() if f != "eta"})
@@ -115,6 +119,7 @@ def test_multi_iteration_run_c2_shape(dcfm, flags):
         st0 = warm.get_state()
     finally:
         warm.close()
+    assert np.abs(st0["X"]).max() < 10.0, "warm-up chain in an X excursion: not a parity start"
     burnin, mcmc, thin, N = 0, 6, 2, 6
     smp = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], burnin, mcmc, thin, inject_draws=True, asm_batch=3,
                        flags=flags)
@@ -129,8 +134,7 @@ def test_multi_iteration_run_c2_shape(dcfm, flags):
     finally:
         smp.close()
     ref = SamplerState(**{f: np.array(v, dtype=np.float64, order="F") for f, v in st0.items()})
-    SL = V.run_chain(c["Yd"], ref, c["rho"], c["hyper"], c["src"].iteration, 1, N, burnin, mcmc, thin,
-                     direct=bool(flags & 0x10))
+    SL = V.run_chain(c["Yd"], ref, c["rho"], c["hyper"], c["src"].iteration, 1, N, burnin, mcmc, thin, direct=True)
     for f in STATE_CMP:
         e = rel_err(got[f], getattr(ref, f))
         assert e < TOL, f"{f} rel err {e:.3e}"

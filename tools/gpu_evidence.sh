@@ -1,13 +1,28 @@
 #!/bin/bash
-# Round evidence on the box for the current build: GPU tests, smoke, the driver's bench + its
-# rocprofv3 trace and PMC passes (gpu_full.sh), then the c4 shape (bench + trace + PMC) and the
-# g = 8 share bench.  Stops at the first failing step.  Usage: bash tools/gpu_evidence.sh TAG
+# Round evidence on the box for the current build: every GPU test + smoke, then per workload the
+# rocprofv3 kernel trace + PMC passes FIRST (tools/profile_round.sh; the summary is copied into
+# the box's profiles/ so the bench line that follows takes roofline.traffic from it), then the
+# bench line.  Workloads: the driver's c3 command, c4, the g = 8 share (bench only), c5.
+# Stops at the first failing step.  Usage: bash tools/gpu_evidence.sh TAG [notest]
 TAG=$1
-bash tools/gpu_full.sh $TAG || exit 1
+mkdir -p gpurun_out
+if [ "$2" != "notest" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/t_$TAG.log 2>&1 || { echo "pytest failed $?"; tail -30 gpurun_out/t_$TAG.log; exit 1; }
+  grep -E "passed|failed" gpurun_out/t_$TAG.log | tail -1
+  timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo "smoke failed"; tail gpurun_out/smoke_$TAG.log; exit 1; }
+  tail -1 gpurun_out/smoke_$TAG.log
+fi
+C3="--gpus 1 --steps 20 --warmup 5"
 C4="--g 8 --P 1250 --n 2000 --K 100 --steps 100 --warmup 10"
 C5="--g 256 --P 391 --n 2000 --K 30 --steps 30 --warmup 5"
-timeout -k 10 300 python3 -u bench.py $C4 > gpurun_out/bench_${TAG}_c4.json 2> gpurun_out/bench_${TAG}_c4.err || { echo "c4 bench failed"; exit 1; }
-bash tools/profile_round.sh ${TAG}_c4 $C4 || exit 1
+run() {   # name, bench args, extra bench args (not part of the profiled command)
+  local N=$1 A=$2 X=$3
+  bash tools/profile_round.sh $N $A || exit 1
+  cp gpurun_out/prof_${N}_pmc.json profiles/${N}_pmc.json
+  timeout -k 10 400 python3 -u bench.py $A $X > gpurun_out/bench_$N.json 2> gpurun_out/bench_$N.err || { echo "bench $N failed"; tail gpurun_out/bench_$N.err; exit 1; }
+}
+run ${TAG} "$C3"
+run ${TAG}_c4 "$C4" "--no-cpu-baseline"
 timeout -k 10 300 python3 -u bench.py --g 8 --thin 100000 --steps 2000 --warmup 100 --no-cpu-baseline --no-profile --converged-mcmc 0 > gpurun_out/bench_${TAG}_g8.json 2> gpurun_out/bench_${TAG}_g8.err || { echo "g8 bench failed"; exit 1; }
-timeout -k 10 400 python3 -u bench.py $C5 --no-cpu-baseline --converged-mcmc 0 > gpurun_out/bench_${TAG}_c5.json 2> gpurun_out/bench_${TAG}_c5.err || { echo "c5 bench failed"; exit 1; }
+run ${TAG}_c5 "$C5" "--no-cpu-baseline --converged-mcmc 0"
 python3 tools/show_bench.py gpurun_out/bench_${TAG}.json gpurun_out/bench_${TAG}_c4.json gpurun_out/bench_${TAG}_g8.json gpurun_out/bench_${TAG}_c5.json

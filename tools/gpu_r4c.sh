@@ -13,3 +13,4 @@ for V in "def:" "ex:--exact-residual" "notail:--asm-tail -1" "ab1:--asm-batch 1"
 done
 [ $# -gt 0 ] && bash tools/gpu_ab.sh $TAG 2 "$@"
 echo all done
+bash tools/diag_l2.sh r4c
