@@ -56,8 +56,7 @@ class DcfmConfig(C.Structure):
         ("bd1", C.c_double), ("ad2", C.c_double), ("bd2", C.c_double),
         ("seed", C.c_uint64),
         ("nranks", C.c_int32), ("rank", C.c_int32), ("device", C.c_int32),
-        ("flags", C.c_uint32), ("asm_batch", C.c_int32), ("asm_tail", C.c_int32),
-        ("reserved", C.c_int32 * 6),
+        ("flags", C.c_uint32), ("asm_batch", C.c_int32), ("reserved", C.c_int32 * 7),
     ]
 
 

@@ -74,18 +74,12 @@ struct dcfm_handle {
                e_free[2] = {nullptr, nullptr}, e_drawn[2] = {nullptr, nullptr}, e_used[2] = {nullptr, nullptr};
     bool fused = false;           // K <= 32 fused launch chain (else the side-stream layout), fixed at create
     bool plam_valid = false;      // b.Plam holds the caller's Plam (no iteration run since set_state)
-    int64_t lg_iter[2] = {-1, -1};   // iteration whose loading-row variates b.ldraw[slot] holds (generated
-                                     // fused chain; counter-based, so valid whatever the state)
-    unsigned long long wc_ops = 0;   // Z-operator computations scheduled (k_wcol's OPS blocks or k_lambda's OPS
-                                     // role): the epoch of their hand-off counters
-    unsigned long long lam_ops = 0;  // k_lambda launches with the OPS role (epoch of its row-block counters)
-    int64_t ops_iter = -1;           // iteration whose Z operators the last k_lambda computed (A, ZM out)
+    unsigned long long wc_ops = 0;   // k_wcol launches with the operator roles (hand-off counter epoch)
     unsigned long long xm_ops = 0;   // k_xdraw launches with the X-operator role (several ranks; its counter's epoch)
     bool asm_pending[2] = {false, false};
     int cur = 0;                  // delta/tau buffer in use
     int lb = 0;                   // Lb buffer being filled
     int B = 16;                   // saved samples per flush
-    int tail = 1;                 // eager flush once this many saved samples of a call remain (< 0: off)
     int batch = 0;                // saved samples pending in Lb[lb]
     int64_t saved = 0;
     bool have_data = false, have_state = false;
@@ -503,7 +497,6 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     d.sgap = packed ? KP * KP + d.NP * KP : 0;
     d.xstride = packed ? d.G * KP + KP * KP + d.NP * KP : d.kp * d.kp;
     h->B = c.asm_batch > 0 ? c.asm_batch : 32;
-    h->tail = c.asm_tail == 0 ? 1 : (c.asm_tail < 0 ? -1 : c.asm_tail);
 
     Bufs &b = h->b;
     const size_t G = d.G, NP = d.NP, PP = d.PP, g = d.g, p = d.p, KP = d.kp;
@@ -548,7 +541,7 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         ALLOC(tk, 1);
         b.ticket = reinterpret_cast<unsigned *>(tk);
         double *sy = nullptr;
-        ALLOC(sy, SYNC_ZM + 2 * G);       // zeroed: the hand-off counters start at 0 (<= 255 chunks, G shards x 2)
+        ALLOC(sy, SYNC_ZM + G);           // zeroed: the hand-off counters start at 0 (<= 255 chunks, G shards)
         b.sync = reinterpret_cast<unsigned long long *>(sy);
     }
     ALLOC(b.C, G * PP * KP);
@@ -570,12 +563,9 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         b.T1 = h->Tb[c.rank + 1];
     }
     ALLOC(b.Sigma, (size_t)(tri(b.T1) - tri(b.T0)) * ASM_TILE * ASM_TILE);
-    // the generated fused chain: k_lambda's LAMGEN blocks draw the next iteration's loading-row
-    // variates into b.ldraw[(it + 1) & 1] (lam_draws)
-    if (h->fused && !d.inject) {
-        ALLOC(b.ldraw[0], (size_t)lam_gen_doubles(d));
-        ALLOC(b.ldraw[1], (size_t)lam_gen_doubles(d));
-    }
+    // the generated fused chain: k_wcol's LAMGEN blocks draw the loading-row variates into b.ldraw
+    // each iteration (lam_draws)
+    if (h->fused && !d.inject) ALLOC(b.ldraw, (size_t)lam_gen_doubles(d));
     if (!d.inject && !h->fused) {   // k_draws batches of the side-stream layouts
         const size_t K = c.K, n = c.n, P = c.P;
         const size_t nz = K * n * g, nx = K * n, nl = K * P * g, gpsi = P * K * g, gdel = K * g, gps = P * g;
@@ -795,7 +785,6 @@ int dcfm_init_state(dcfm_handle *h) {
     HIPC(h, hipGetLastError());
     HIPC(h, hipStreamSynchronize(h->stream));
     h->cur = 0;
-    h->ops_iter = -1;          // the Z operators follow the new Lambda, omega
     h->plam_valid = true;      // Plam = psi o tau' was formed (dc:86), as set_state's caller Plam
     h->have_state = true;
     return reset_numeric(h);
@@ -932,7 +921,6 @@ int dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s) {
     h->cur = 0;
     k_to_dev(d, s->delta, v);   if ((rc = up(h, h->b.delta, v))) return rc;
     k_to_dev(d, s->tauh, v);    if ((rc = up(h, h->b.tau, v))) return rc;
-    h->ops_iter = -1;
     h->plam_valid = true;
     h->have_state = true;
     return reset_numeric(h);
@@ -1022,13 +1010,6 @@ int dcfm_set_draws(dcfm_handle *h, const dcfm_draws_view *dv, int64_t first_iter
 }
 
 // Hand the filled Lb[lb] batch to the assembly stream (overlaps the next iterations).
-// saved iterations t in (a, b] (dc:180: mod(t, thin) == 0 && t > BURNIN)
-static int64_t saves_in(const dcfm_handle *h, int64_t a, int64_t b) {
-    const int64_t th = h->cfg.thin, lo = std::max<int64_t>(a, h->cfg.burnin);
-    if (b <= lo) return 0;
-    return b / th - lo / th;
-}
-
 static int flush_batch(dcfm_handle *h) {
     if (h->batch == 0) return DCFM_OK;
     Dims &d = h->d;
@@ -1091,7 +1072,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     // (k_wcol, k_xdraw); K > 32 (or DCFM_FLAG_UNFUSED): prep and the X operators run on the
     // side stream
     const bool fused = h->fused;
-    const bool lamgen = fused && !d.inject;   // k_lambda draws the next iteration's variates (b.ldraw)
+    const bool lamgen = fused && !d.inject;   // k_wcol draws k_lambda's variates (b.ldraw)
     // fused (K <= 32): per iteration t, k_wcol = [Z operators and shard sum of A of t, column
     // sums of t-1] beside the W pass of t, whose tiles draw Z; one rank: the last chunk also
     // factors Xprec.  Several ranks: k_xred and ONE all-gather of [column sums | A sum | X
@@ -1162,24 +1143,18 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             if (it + batch_n < end_iter && gen_batch(it + batch_n, slot) < 0) return rc_gen;   // next batch
         }
         const DrawsDev &dr = d.inject ? h->dr : h->gen[gen_draws ? slot : 0];
-        if (lamgen && h->lg_iter[it & 1] != it) {   // not drawn ahead by the previous k_lambda
-            KTimer t(h, DCFM_K_DRAWS, s);
-            launch_lamgen(d, b, it, s);
-            h->lg_iter[it & 1] = it;
-        }
-        // the Z operators: from the previous k_lambda's OPS role, else k_wcol's own OPS blocks
-        const int ops_mode = (h->ops_iter == it) ? 2 : 1;
-        if (fused && ops_mode == 1) h->wc_ops += 1;
         if (wc) {   // k_wcol: + the Z draw of the W tiles' rows
             KTimer t(h, DCFM_K_WPASS, s);
-            launch_wcol(d, b, dr, it, ops_mode, delta_pending, true, h->wc_ops, s);
+            h->wc_ops += 1;
+            launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s, lamgen);
         } else if (fused) {   // several ranks: k_wcol (W pass + Z draw, no X factorisation), k_xred
                               // (the local X message), then ONE all-gather of [column sums of it - 1
                               // | local A sum | X message]; k_xdraw factors Xprec from the ranks' A
                               // sums, runs the delta chain of it - 1 and draws X
             {
                 KTimer t(h, DCFM_K_WPASS, s);
-                launch_wcol(d, b, dr, it, ops_mode, delta_pending, true, h->wc_ops, s);
+                h->wc_ops += 1;
+                launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s, lamgen);
             }
             { KTimer t(h, DCFM_K_XRED, s); launch_xred(d, b, s); }
             KTimer t(h, DCFM_K_COMM, s);
@@ -1233,18 +1208,10 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         }
         {
             KTimer t(h, DCFM_K_LAMBDA, s);
-            // fused: the launch's tail also computes the next iteration's Z operators; exact residual:
-            // every row block takes ps, omega from dc:169's residual (K <= 32 in k_lambda itself)
+            // exact residual: every row block takes ps, omega from dc:169's residual (K <= 32: in k_lambda)
             const bool exact = h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL;
-            const bool lops = fused;
-            if (lops) {
-                h->wc_ops += 1;
-                h->lam_ops += 1;
-            }
             launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, lamgen,
-                          lops ? h->lam_ops : 0, exact ? 0.0 : KAPPA_IDENTITY_MAX);
-            if (lamgen) h->lg_iter[(it + 1) & 1] = it + 1;
-            h->ops_iter = lops ? it + 1 : -1;
+                          exact ? 0.0 : KAPPA_IDENTITY_MAX);
         }
         if ((h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL) && d.kp != KP) {   // wide: dc:169's residual, own launch
             KTimer t(h, DCFM_K_RESID, s);
@@ -1287,10 +1254,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             HIPC(h, hipGetLastError());
             h->batch += 1;
             h->saved += 1;
-            // eager tail flush: the samples saved so far go out now, on the assembly stream beside
-            // the call's remaining iterations, so the call's closing flush holds only the last `tail`
-            const bool eager = h->tail >= 0 && h->batch > h->tail && saves_in(h, it, end_iter - 1) == h->tail;
-            if (h->batch == h->B || eager) {
+            if (h->batch == h->B) {
                 int rc = flush_batch(h);
                 if (rc) return rc;
             }

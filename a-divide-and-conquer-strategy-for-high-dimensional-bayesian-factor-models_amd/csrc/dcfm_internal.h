@@ -77,10 +77,10 @@ struct DrawsDev {
 // loading-row variates of one iteration in k_lambda's layout (local shard m, loading row j):
 // NL [G][P][K] (dc:142 zlam), Gpsi [G][P][K] (dc:150), Gps [G][P] (dc:170)
 struct LamDraws { const double *NL, *Gpsi, *Gps; };
-// the previous iteration's k_lambda generates them for the generated fused chain (K <= 32) in
-// extra blocks behind its loading rows: one index space — [0, n_ps) ps gammas, [n_ps, n_psi) psi
-// gammas, [n_psi, n_all) normal pairs — walked grid-stride by b_total blocks of LAM_GEN_THREADS
-// (k_lamgen) or of 64 threads (k_lambda's tail, lam_gen_plan64)
+// k_wcol's extra blocks generate them for the generated fused chain (K <= 32): one index
+// space — [0, n_ps) ps gammas, [n_ps, n_psi) psi gammas, [n_psi, n_all) normal pairs — walked
+// grid-stride by b_total blocks of LAM_GEN_THREADS behind the W tiles (VALU work in the slots
+// and issue cycles the streaming W pass leaves free)
 #ifndef DCFM_LAM_GEN_BLOCKS
 #define DCFM_LAM_GEN_BLOCKS 160
 #endif
@@ -100,13 +100,10 @@ inline LamGen lam_gen_plan(const Dims &d, double *base) {
     g.b_total = full < LAM_GEN_BLOCKS ? full : LAM_GEN_BLOCKS;
     return g;
 }
-// k_lambda's LAMGEN role: blocks of 4 waves, as k_lamgen's
-inline LamGen lam_gen_plan256(const Dims &d, double *base) { return lam_gen_plan(d, base); }
 
 struct Bufs {
     double *Y, *yy, *Lam, *omega, *ps, *psi, *Plam, *X, *Z, *delta, *tau;
-    double *ldraw[2];                  // LamDraws of the generated fused chain (lam_gen_plan), slot it & 1
-                                       // holds iteration it's variates; else null
+    double *ldraw;                     // LamDraws of the generated fused chain (lam_gen_plan), else null
     double *W, *A, *ZM, *Sp, *xin, *xall, *C, *E, *cpart, *sloc, *sall;
     double *Lb[2], *wsum[2], *Sigma;
     double *xa, *xa_all, *XM;          // per-rank sum of A, gathered sums, X-draw operators
@@ -127,9 +124,6 @@ constexpr int XSUM_BLOCKS = 8;
 // Bufs::sync: [0] the X operators (k_xdraw, several ranks), [1] spare, [2, 2 + 256) chunk counters of the A sum, [SYNC_ZM, SYNC_ZM + G) the
 // per-shard Z-operator counters (the fused W pass draws Z once its shard's operators are out)
 constexpr int SYNC_ZM = 2 + 256;
-// ... then [SYNC_ZM + G, SYNC_ZM + 2 G): k_lambda's row blocks of shard m out (its OPS role, LamOps)
-// LDS of the Z-operator code (prep_gram / prep_ops): A, U, Zprec / T, scratch + the 16x16 images
-constexpr int PREP_SMEM_DOUBLES = 4 * KP * (KP + 1) + 3 * 16;
 // blocks of the A sum: G / chunk, chunk = a power of two dividing G, grown while more than
 // XSUM_BLOCKS chunks remain — so each chunk is a subtree of the canonical tree (TreeSum) and
 // the tree over the chunk sums is T(0, G).  G <= XSUM_BLOCKS: one block sums every shard
@@ -170,7 +164,7 @@ void launch_xred(const Dims &d, const Bufs &b, hipStream_t s);
 // K <= 32: the Z operators + shard sum of A (ops), the previous iteration's column sums
 // (colsum) and the Y pass W with the Z draw of its rows (wpass: Z, Sp; needs ops) in one launch
 // (k_wcol); one rank also factors Xprec
-void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, int ops, bool colsum, bool wpass,
+void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool ops, bool colsum, bool wpass,
                  unsigned long long ops_epoch, hipStream_t s, bool lamgen = false);
 // several ranks, K <= 32: k_xdraw with the X operators (block 0, from the ranks' A sums of the
 // packed gather, published through the counter b.sync[0] at xm_epoch) and the row blocks
@@ -186,20 +180,14 @@ void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
 void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &dr = DrawsDev{},
                   const double *delta_in = nullptr, const double *tau_in = nullptr, double *delta_out = nullptr,
                   double *tau_out = nullptr, int64_t delta_iter = 0);
-// gen: K <= 32 reads the variates of iteration iter from b.ldraw[iter & 1] (the generated fused
-// chain) instead of the draw buffers dr (injected draws, k_draws batches), and its LAMGEN blocks
-// (behind the loading rows, in the launch's tail) draw iteration iter + 1's into the other slot
-// ops_epoch > 0 (fused chain): the launch's OPS role computes the next iteration's Z operators (A_m,
-// ZM_m) and signals the hand-off counters as k_wcol's OPS blocks would, as the ops_epoch-th such launch.
+// gen: K <= 32 reads the variates k_wcol generated into b.ldraw (the generated fused chain)
+// instead of the draw buffers dr (injected draws, k_draws batches).
 // K <= 32: a row block whose SS identity may be off by more than ~kappa_max eps (lambda.h guard) takes
 // ps, omega from dc:169's direct residual instead (resid.h); kappa_max = 0: every block (exact mode)
 constexpr double KAPPA_IDENTITY_MAX = 1e3;
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, const double *plam_src, hipStream_t s, bool gen = false,
-                   unsigned long long ops_epoch = 0, double kappa_max = KAPPA_IDENTITY_MAX);
-// the generated fused chain's loading-row variates of iteration iter into b.ldraw[iter & 1] on
-// their own (a run's first iteration when the previous k_lambda did not draw them)
-void launch_lamgen(const Dims &d, const Bufs &b, int64_t iter, hipStream_t s);
+                   double kappa_max = KAPPA_IDENTITY_MAX);
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s);
 // resid.hip (DCFM_FLAG_EXACT_RESIDUAL): ps, omega from the direct residual Yd - eta Lambda'
 // (dc:169-171), after the loading-row kernel, with its ps variates (gen: b.ldraw, else dr)

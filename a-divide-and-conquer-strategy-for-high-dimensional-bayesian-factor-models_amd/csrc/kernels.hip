@@ -49,12 +49,11 @@ namespace dcfm {
 // ZM[m] = {M1, M2, U, NA}.  4 waves split the j reduction of A (fp64 MFMA 2x2 tiles).
 // ============================================================================
 constexpr int PREP_SMEM = 4 * KP * (KP + 1) + 3 * TS16;
-static_assert(PREP_SMEM == PREP_SMEM_DOUBLES, "dcfm_internal.h mirror");
 // prep_gram: A_m (to HBM and LDS part[0]), NA, and Zprec's upper triangle into the
 // lower triangle of part[2]; prep_ops: the Z-draw operators from the LDS image.
 // PUB: A_m, NA and (prep_ops) the Z operators are published with agent-scope stores (read by other
 // blocks of the same launch, k_wcol)
-template <bool PUB = false, bool COH = false>
+template <bool PUB = false>
 __device__ __forceinline__ void prep_gram(const Dims &d, const double *__restrict__ Lam,
                                           const double *__restrict__ omega, double *__restrict__ A,
                                           double *__restrict__ ZM, int m, double *smem) {
@@ -66,18 +65,11 @@ __device__ __forceinline__ void prep_gram(const Dims &d, const double *__restric
     const double *w = omega + (size_t)m * d.PP;
     d4 a00 = {0, 0, 0, 0}, a01 = a00, a10 = a00, a11 = a00;
     // rows j, j+1 of chunk tt: (w_j Lambda_ja) is the A operand [Zmsg, dc:98], Lambda_jb the B operand
-    // COH: Lambda, omega written by other blocks of this launch (k_lambda's OPS role): agent-scope loads
     auto ld = [&](int tt, d2 &wj, double (&l)[4]) {
         const int j = 8 * tt + 2 * q;
-        if constexpr (COH) {
-            wj.x = ld_agent(w + j); wj.y = ld_agent(w + j + 1);
-            l[0] = ld_agent(L + j * KP + r); l[1] = ld_agent(L + j * KP + 16 + r);
-            l[2] = ld_agent(L + (j + 1) * KP + r); l[3] = ld_agent(L + (j + 1) * KP + 16 + r);
-        } else {
-            wj = *reinterpret_cast<const d2 *>(w + j);
-            l[0] = L[j * KP + r]; l[1] = L[j * KP + 16 + r];
-            l[2] = L[(j + 1) * KP + r]; l[3] = L[(j + 1) * KP + 16 + r];
-        }
+        wj = *reinterpret_cast<const d2 *>(w + j);
+        l[0] = L[j * KP + r]; l[1] = L[j * KP + 16 + r];
+        l[2] = L[(j + 1) * KP + r]; l[3] = L[(j + 1) * KP + 16 + r];
     };
     auto mm = [&](const d2 &wj, const double (&l)[4]) {
         const double wl0 = l[0] * wj.x, wh0 = l[1] * wj.x, wl1 = l[2] * wj.y, wh1 = l[3] * wj.y;
@@ -684,19 +676,6 @@ __device__ __forceinline__ void wait_count(unsigned long long *ctr, unsigned lon
     if (threadIdx.x == 0)
         while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
     __syncthreads();
-}
-
-// k_lambda's OPS role (lambda.h LamOps): shard m's Z operators for the next iteration's k_wcol, once
-// this launch's row blocks of the shard are out -- the work k_wcol's OPS blocks do otherwise, in
-// the launch's tail instead of beside the next W pass; same code, same counters (k_wcol's A-sum
-// blocks and W tiles wait on them as before)
-__device__ void lam_ops_role(const Dims &d, const double *Lam, const double *omega, const LamOps &ops, int m,
-                             double *smem) {
-    wait_count(ops.lam_ctr + m, ops.lam_target);
-    prep_gram<true, true>(d, Lam, omega, ops.A, ops.ZM, m, smem);
-    signal_count(ops.sync + 2 + m / ops.chunk);   // A_m is out; the operators follow
-    prep_ops<true>(d, ops.ZM, m, smem);
-    signal_count(ops.sync + SYNC_ZM + m);         // the Z operators are out
 }
 
 // ============================================================================
@@ -1322,7 +1301,7 @@ __device__ __forceinline__ void wcol_body(const Dims &d, const Bufs &b, const Dr
     const int G = d.G, nxs = xsum_blocks(G), chunk = G / nxs;
     unsigned long long *chunk_ctr = b.sync + 2;   // per chunk of shards: A_m published
     int blk = blockIdx.x;
-    if (ops == 1) {
+    if (ops) {
         if (blk < G) {
             prep_gram<true>(d, b.Lam, b.omega, b.A, b.ZM, blk, smem);
             signal_count(chunk_ctr + blk / chunk);   // A_m is out; the operators follow
@@ -1707,19 +1686,16 @@ void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
                            b.Sp, dr, iter);
 }
 // k_wcol launch (K <= 32)
-void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, int ops, bool colsum, bool wpass,
+void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool ops, bool colsum, bool wpass,
                  unsigned long long ops_epoch, hipStream_t s, bool lamgen) {
     static_assert(LAM_GEN_THREADS == 256, "k_wcol blocks are 256 threads");
     LamGen lg = {};
-    if (lamgen && b.ldraw[0]) lg = lam_gen_plan(d, b.ldraw[iter & 1]);
+    if (lamgen && b.ldraw) lg = lam_gen_plan(d, b.ldraw);
     // W pass tiles: 64-row blocks while 128-row blocks would leave CUs idle
     const int wmode = (d.NP / 128) * d.G < 256 ? 2 : 1;
-    // ops: 1 = the Z-operator blocks and the A-sum blocks; 2 = the A-sum blocks only (the operators came
-    // from the previous k_lambda's OPS role)
-    const int nb = (ops == 1 ? d.G : 0) + (ops ? xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) +
-                   (wpass ? (d.NP / (64 * (3 - wmode))) * d.G : 0);
+    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / (64 * (3 - wmode))) * d.G : 0);
     if (nb + lg.b_total == 0) return;
-    hipLaunchKernelGGL(k_wcol, dim3(nb + lg.b_total), dim3(256), 0, s, d, b, dr, iter, ops, colsum ? 1 : 0,
+    hipLaunchKernelGGL(k_wcol, dim3(nb + lg.b_total), dim3(256), 0, s, d, b, dr, iter, ops ? 1 : 0, colsum ? 1 : 0,
                        wpass ? wmode : 0, ops_epoch, d.coll ? 0 : 1, lg);
 }
 void launch_xred(const Dims &d, const Bufs &b, hipStream_t s) {
@@ -1775,33 +1751,22 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &d
     }
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
-                   const double *tau_cur, const double *plam_src, hipStream_t s, bool gen, unsigned long long ops_epoch,
-                   double kappa_max) {
+                   const double *tau_cur, const double *plam_src, hipStream_t s, bool gen, double kappa_max) {
     if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, plam_src, s);
     LamDraws ld;
-    LamGen next = {};     // gen: the next iteration's variates, drawn in the launch's tail
-    if (gen) {   // this iteration's variates, drawn by the previous k_lambda (or k_lamgen)
-        const LamGen g = lam_gen_plan(d, b.ldraw[iter & 1]);
+    if (gen) {   // this iteration's variates, drawn by k_wcol's LAMGEN blocks (lam_draws)
+        const LamGen g = lam_gen_plan(d, b.ldraw);
         ld.NL = g.NL; ld.Gpsi = g.Gpsi; ld.Gps = g.Gps;
-        next = lam_gen_plan256(d, b.ldraw[(iter + 1) & 1]);
     } else {     // [T][g][P][K] / [T][g][P] draw buffers: this iteration, this rank's first shard
         const size_t row0 = ((size_t)(iter - dr.first_iter) * d.g + d.shard0) * d.P;
         ld.NL = dr.NL + row0 * d.K;
         ld.Gpsi = dr.Gpsi + row0 * d.K;
         ld.Gps = dr.Gps + row0;
     }
-    const int nrb = cdiv(d.P, LAM_ROWS * LAM_WAVES);   // row blocks per shard
-    LamOps ops = {};
-    if (ops_epoch) {   // the next iteration's Z operators in the launch's tail (ops_epoch-th k_lambda with it)
-        ops.A = b.A; ops.ZM = b.ZM; ops.sync = b.sync; ops.lam_ctr = b.sync + SYNC_ZM + d.G;
-        ops.nops = d.G;
-        ops.chunk = d.G / xsum_blocks(d.G);
-        ops.lam_target = ops_epoch * (unsigned long long)nrb;
-    }
-    const dim3 grid(nrb * d.G + ops.nops + next.b_total);
+    const dim3 grid(cdiv(d.P, LAM_ROWS * LAM_WAVES), d.G);
 #define LAUNCH_LAM(KE)                                                                                       \
     hipLaunchKernelGGL(k_lambda<KE>, grid, dim3(64 * LAM_WAVES), 0, s, d, b.C, b.E, b.yy, tau_cur, b.Lam, b.psi, \
-                       plam_src, b.ps, b.omega, b.cpart, ld, nrb, next, iter + 1, ops, b.Y, b.X, b.Z, kappa_max)
+                       plam_src, b.ps, b.omega, b.cpart, ld, b.Y, b.X, b.Z, kappa_max)
     // the factor width rounded up to an instantiated one (rows >= K are identity padding)
     if (d.K <= 8) LAUNCH_LAM(8);
     else if (d.K <= 16) LAUNCH_LAM(16);
@@ -1810,13 +1775,6 @@ void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t ite
     else if (d.K <= 30) LAUNCH_LAM(30);
     else LAUNCH_LAM(32);
 #undef LAUNCH_LAM
-}
-__global__ __launch_bounds__(LAM_GEN_THREADS) void k_lamgen(Dims d, LamGen lg, int64_t iter) {
-    lam_draws(d, lg, iter, blockIdx.x * LAM_GEN_THREADS + (int)threadIdx.x, lg.b_total * LAM_GEN_THREADS);
-}
-void launch_lamgen(const Dims &d, const Bufs &b, int64_t iter, hipStream_t s) {
-    const LamGen lg = lam_gen_plan(d, b.ldraw[iter & 1]);
-    hipLaunchKernelGGL(k_lamgen, dim3(lg.b_total), dim3(LAM_GEN_THREADS), 0, s, d, lg, iter);
 }
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s) {
     const dim3 grid(d.G, d.kp / 32);

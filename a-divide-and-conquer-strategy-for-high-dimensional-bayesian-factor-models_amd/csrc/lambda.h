@@ -123,21 +123,8 @@ __device__ __forceinline__ double rowsum8(double v) {
 }
 
 constexpr int LAM_ROWS = 8;   // loading rows per wave
-constexpr int LAM_WAVES = 4;  // waves per block (independent row groups; the block size the OPS and
-                              // LAMGEN roles use)
-// k_lambda's OPS role (fused chain): the next iteration's Z operators of shard m (A_m, cholcov's
-// M1, M2, U, NA; dc:98-107) from this launch's Lambda_m, omega_m, once every row block of shard m
-// is out (counter lam_ctr[m]); defined in kernels.hip with the other operator code
-struct LamOps {
-    double *A, *ZM;
-    unsigned long long *sync;          // Bufs::sync (chunk and Z-operator counters, as k_wcol's OPS blocks)
-    unsigned long long *lam_ctr;       // [G] row blocks of shard m out (Bufs::sync + SYNC_ZM + G)
-    int nops;                          // shards with an OPS block (0: role off)
-    int chunk;                         // shards per A-sum chunk (xsum_blocks)
-    unsigned long long lam_target;     // SYNC_LAM + m count once shard m's row blocks are out
-};
-__device__ void lam_ops_role(const Dims &d, const double *Lam, const double *omega, const LamOps &ops, int m,
-                             double *smem);
+constexpr int LAM_WAVES = 4;  // waves per block: independent row groups that share the block's residual
+                              // fixup (the 32 rows resid_tile takes at once)
 constexpr int LAM_PIPE = 4;   // image columns read ahead of their trailing-update FMAs
 __host__ __device__ constexpr int lam_ncol(int KE, int b) { return 8 * b + 8 < KE ? 8 * b + 8 : KE; }
 
@@ -158,15 +145,12 @@ __device__ __forceinline__ LamPiv lam_pivots(d2 pk, d2 pk1, d2 bb) {
 }
 
 template <int KE>
-// waves_per_eu(2): the row path's 250 VGPRs, and the OPS role's MFMA accumulators must share them
-// (left alone, hipcc put those in 32 AGPRs: 283 registers, one wave per SIMD)
-__global__ __launch_bounds__(64 * LAM_WAVES) __attribute__((amdgpu_waves_per_eu(2))) void k_lambda(Dims d, const double *__restrict__ C, const double *__restrict__ E,
+__global__ __launch_bounds__(64 * LAM_WAVES) void k_lambda(Dims d, const double *__restrict__ C, const double *__restrict__ E,
                                                const double *__restrict__ yy, const double *__restrict__ tau_cur,
                                                double *__restrict__ Lam, double *__restrict__ psi,
                                                const double *__restrict__ plam_src, double *__restrict__ ps,
                                                double *__restrict__ omega, double *__restrict__ cpart,
-                                               LamDraws ld, int nrb, LamGen next, int64_t next_iter,
-                                               LamOps ops, const double *__restrict__ Y,
+                                               LamDraws ld, const double *__restrict__ Y,
                                                const double *__restrict__ X, const double *__restrict__ Z,
                                                double kappa_max) {
     static_assert(KE % 2 == 0 && KE >= 2 && KE <= KP, "even factor width");
@@ -179,18 +163,6 @@ __global__ __launch_bounds__(64 * LAM_WAVES) __attribute__((amdgpu_waves_per_eu(
     constexpr int WSN = LSN + BSN + 2 * VSN + KP;   // one wave's LDS (+ sqrt(diag E_m) for the guard)
     __shared__ __attribute__((aligned(16))) double SMB[LAM_WAVES * WSN];
     __shared__ int exact_blk;                       // some row of the block needs dc:169's residual
-    static_assert(LAM_WAVES * WSN >= PREP_SMEM_DOUBLES, "the OPS role's LDS fits the block's");
-    const int blk = (int)blockIdx.x, nrow = nrb * d.G;
-    if (blk >= nrow) {
-        if (blk < nrow + ops.nops) {          // OPS: the next iteration's Z operators of shard blk - nrow
-            lam_ops_role(d, Lam, omega, ops, blk - nrow, SMB);
-            return;
-        }
-        // LAMGEN: the next iteration's variates, in the launch's tail
-        lam_draws(d, next, next_iter, (blk - nrow - ops.nops) * 64 * LAM_WAVES + (int)threadIdx.x,
-                  next.b_total * 64 * LAM_WAVES);
-        return;
-    }
     const int wave = threadIdx.x >> 6;
     double *SM = SMB + wave * WSN;
     double(*LS)[LAM_ROWS][KP + 1][2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 1][2]>(SM);
@@ -198,13 +170,14 @@ __global__ __launch_bounds__(64 * LAM_WAVES) __attribute__((amdgpu_waves_per_eu(
     double *Vs = SM + LSN + BSN, *Is = Vs + VSN;
     double *Dg = SM + LSN + BSN + 2 * VSN;          // sqrt(E_m[k][k])
     double *Es = SM;
-    const int m = blk / nrb, mg = d.shard0 + m;
+    const int m = blockIdx.y, mg = d.shard0 + m;
+    const int lane = threadIdx.x & 63, grp = lane >> 3, l = lane & 7;
     if (threadIdx.x == 0) exact_blk = 0;
     __syncthreads();
-    const int lane = threadIdx.x & 63, grp = lane >> 3, l = lane & 7;
     Vs += grp * (KP + 2);
     Is += grp * (KP + 2);
-    const int j = ((blk - m * nrb) * LAM_WAVES + wave) * LAM_ROWS + grp;
+    const int j0 = blockIdx.x * LAM_WAVES * LAM_ROWS;   // the block's first loading row
+    const int j = j0 + wave * LAM_ROWS + grp;
     const bool valid = j < d.P;
     const int jj = valid ? j : 0;
     const uint32_t rowoff = (uint32_t)(m * d.PP + jj) * KP, toff = (uint32_t)mg * KP;
@@ -466,7 +439,7 @@ __global__ __launch_bounds__(64 * LAM_WAVES) __attribute__((amdgpu_waves_per_eu(
         for (int b = 0; b < 4; ++b) {
             const int r = l + 8 * b;
             const double ps_b = rv[b] ? (1.0 / (d.df * 0.5 + 0.5 * (x[b] * x[b] * tv[b]))) * G[b] : 0.0;
-            st_agent(Lam + rowoff + r, x[b]);                        // agent-coherent: the OPS role reads it
+            st_agent(Lam + rowoff + r, x[b]);                        // agent scope: resid_tile reads it back
             cpart[rowoff + r] = ps_b * (x[b] * x[b]);               // mat = psijh .* Lambda.^2 (dc:156)
             if (rv[b]) psi[rowoff + r] = ps_b;
         }
@@ -474,19 +447,12 @@ __global__ __launch_bounds__(64 * LAM_WAVES) __attribute__((amdgpu_waves_per_eu(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // Lambda out (agent scope) before the vote
     __syncthreads();
     if (exact_blk) {   // dc:169 as written for the block's 32 rows: Ytil = Yd - eta Lambda', sum(Ytil.^2)
-        resid_tile<KP, true>(d, Y, X, Z, Lam, ld.Gps, ps, omega, m,
-                             (blk - m * nrb) * LAM_WAVES * LAM_ROWS, reinterpret_cast<double(*)[32]>(SMB));
+        resid_tile<KP, true>(d, Y, X, Z, Lam, ld.Gps, ps, omega, m, j0, reinterpret_cast<double(*)[32]>(SMB));
     } else if (valid && l == 0) {
         const double SS = yyj + contrib;
         const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;     // dc:170
-        st_agent(ps + (uint32_t)(m * d.PP + j), psn);
-        st_agent(omega + (uint32_t)(m * d.PP + j), 1.0 / psn);  // dc:171 (Q1)
-    }
-    if (ops.nops) {   // this block's rows of shard m are out (their stores complete, agent scope)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_fetch_add(ops.lam_ctr + m, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ps[(uint32_t)(m * d.PP + j)] = psn;
+        omega[(uint32_t)(m * d.PP + j)] = 1.0 / psn;            // dc:171 (Q1)
     }
 }
 

@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void k_resid(Dims d, const double *__restrict_
 
 void launch_resid(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s, bool gen) {
     const double *Gps;
-    if (gen) Gps = lam_gen_plan(d, b.ldraw[iter & 1]).Gps;   // the generated fused chain's slot
+    if (gen) Gps = lam_gen_plan(d, b.ldraw).Gps;   // the generated fused chain: k_wcol's buffer
     else Gps = dr.Gps + ((size_t)(iter - dr.first_iter) * d.g + d.shard0) * d.P;
     const dim3 grid(d.PP / 32, d.G);
     switch (d.kp) {

@@ -40,7 +40,7 @@ class Sampler:
     """One rank's handle: shards [rank*g_local, (rank+1)*g_local) of a chain."""
 
     def __init__(self, n, P, g, K, rho, burnin, mcmc, thin, *, hyper: Hyper = Hyper(), seed=0,
-                 nranks=1, rank=0, device=0, inject_draws=False, asm_batch=0, flags=0, asm_tail=0):
+                 nranks=1, rank=0, device=0, inject_draws=False, asm_batch=0, flags=0):
         self.lib = _abi.load_library()
         cfg = _abi.DcfmConfig()
         cfg.n, cfg.P, cfg.g, cfg.K = int(n), int(P), int(g), int(K)
@@ -52,7 +52,6 @@ class Sampler:
         cfg.nranks, cfg.rank, cfg.device = int(nranks), int(rank), int(device)
         cfg.flags = (_abi.DCFM_FLAG_INJECT_DRAWS if inject_draws else 0) | int(flags)
         cfg.asm_batch = int(asm_batch)
-        cfg.asm_tail = int(asm_tail)
         self.cfg = cfg
         h = C.c_void_p()
         rc = self.lib.dcfm_create(C.byref(cfg), C.byref(h))

@@ -93,7 +93,7 @@ def config_key(args, world):
     """The bench invocation a PMC summary must match (workload, flush sizes, step counts)."""
     return (f"g{args.g}_P{args.P}_n{args.n}_K{args.K}_thin{args.thin}_asm{args.asm_batch}_"
             f"steps{args.steps}_warmup{args.warmup}_gpus{world}{'_chains' if args.chains else ''}"
-            f"{'_exact' if args.exact_residual else ''}{f'_tail{args.asm_tail}' if args.asm_tail else ''}")
+            f"{'_exact' if args.exact_residual else ''}")
 
 
 # HIP-event role name -> the kernel rocprofv3 records it under (the fused K <= 32 chain's W pass
@@ -192,9 +192,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--thin", type=int, default=5)
     ap.add_argument("--asm-batch", type=int, default=96)
-    ap.add_argument("--asm-tail", type=int, default=0,
-                    help="dcfm_config.asm_tail: 0 = library default (eager flush when one saved sample of the "
-                         "run remains), -1 = off")
     ap.add_argument("--g", type=int, default=64)
     ap.add_argument("--P", type=int, default=312)
     ap.add_argument("--n", "--nobs", dest="n", type=int, default=1000)   # --nobs under torchrun (--n is ambiguous there)
@@ -269,7 +266,7 @@ def main():
 
     smp = dcfm.Sampler(n, P, g, K, rho, burnin, mcmc, thin, seed=1 + (rank if chains else 0),
                        nranks=shard_ranks, rank=0 if chains else rank, device=device,
-                       asm_batch=args.asm_batch, flags=0x10 if args.exact_residual else 0, asm_tail=args.asm_tail)
+                       asm_batch=args.asm_batch, flags=0x10 if args.exact_residual else 0)
     if shard_ranks > 1:
         obj = [dcfm.Sampler.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)

@@ -82,13 +82,7 @@ typedef struct {
     int32_t device;     /* HIP device ordinal this handle runs on                */
     uint32_t flags;     /* DCFM_FLAG_*                                           */
     int32_t asm_batch;  /* saved samples per covariance-assembly flush (0 = 32)  */
-    int32_t asm_tail;   /* eager flush: once only this many saved samples of a dcfm_run
-                           call remain, the pending batch is flushed on the assembly
-                           stream, overlapping the call's remaining iterations, and
-                           the call ends with a flush of just those samples
-                           (0 = 1, the default; < 0 = off: flush only full batches and
-                           at the end)                                           */
-    int32_t reserved[6];
+    int32_t reserved[7];
 } dcfm_config;
 
 /* Sampler state (dc:69-87, updated by dc:90-177).  All column-major.
