@@ -184,7 +184,10 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &d
 // instead of the draw buffers dr (injected draws, k_draws batches).
 // K <= 32: a row block whose SS identity may be off by more than ~kappa_max eps (lambda.h guard) takes
 // ps, omega from dc:169's direct residual instead (resid.h); kappa_max = 0: every block (exact mode)
-constexpr double KAPPA_IDENTITY_MAX = 1e3;
+#ifndef DCFM_KAPPA_MAX
+#define DCFM_KAPPA_MAX 1e3
+#endif
+constexpr double KAPPA_IDENTITY_MAX = DCFM_KAPPA_MAX;
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, const double *plam_src, hipStream_t s, bool gen = false,
                    double kappa_max = KAPPA_IDENTITY_MAX);

@@ -4,7 +4,6 @@
 #include "dcfm_internal.h"
 #include "philox.h"
 #include "linalg.h"
-#include "resid.h"
 
 namespace dcfm {
 
@@ -123,8 +122,52 @@ __device__ __forceinline__ double rowsum8(double v) {
 }
 
 constexpr int LAM_ROWS = 8;   // loading rows per wave
-constexpr int LAM_WAVES = 4;  // waves per block: independent row groups that share the block's residual
-                              // fixup (the 32 rows resid_tile takes at once)
+
+// dc:169-171 as written for the wave's 8 loading rows j0 .. j0+7 (the guard below, or the exact
+// mode): Ytil = Yd - eta Lambda' as fp64 MFMA v_mfma_f64_16x16x4 over 16-row chunks of i, the Y
+// values as the accumulator input and -eta as the A operand (the subtraction of dc:169 inside the
+// accumulation); B = the rows' Lambda from the LDS image Lm (columns 8..15 of the tile zero); lane
+// (c, q) holds Ytil for rows i0 + q + 4v of loading row j0 + c and squares them into its sum, the
+// 4 lanes of a row then summed in a fixed order.  ps_j, omega_j with the row's gamma variate Gps.
+__device__ __forceinline__ void resid_rows8(const Dims &d, const double *__restrict__ Y,
+                                            const double *__restrict__ X, const double *__restrict__ Z,
+                                            const double (*Lm)[KP + 1], double Gps_c, int m, int j0, int lane,
+                                            double *__restrict__ ps, double *__restrict__ omega) {
+    constexpr int NT = KP / 8;
+    const int c = lane & 15, q = lane >> 4;
+    const bool col = c < LAM_ROWS && j0 + c < d.P;
+    d2 lb[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        lb[t].x = col ? Lm[c][8 * t + 2 * q] : 0.0;
+        lb[t].y = col ? Lm[c][8 * t + 2 * q + 1] : 0.0;
+    }
+    const double *Ym = Y + (size_t)m * d.NP * d.PP + (col ? j0 + c : 0);
+    const double *Zm = Z + (size_t)m * d.NP * KP + 2 * q;
+    double ss = 0.0;
+    for (int i0 = 0; i0 < d.NP; i0 += 16) {
+        d4 acc;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[v] = col ? Ym[(size_t)(i0 + q + 4 * v) * d.PP] : 0.0;
+        const double *xr = X + (size_t)(i0 + c) * KP + 2 * q, *zr = Zm + (size_t)(i0 + c) * KP;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const d2 xa = *reinterpret_cast<const d2 *>(xr + 8 * t);
+            const d2 za = *reinterpret_cast<const d2 *>(zr + 8 * t);
+            acc = mfma16x16x4(-eta_of(d.sr, d.s1r, xa.x, za.x), lb[t].x, acc);
+            acc = mfma16x16x4(-eta_of(d.sr, d.s1r, xa.y, za.y), lb[t].y, acc);
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) ss = (i0 + q + 4 * v < d.n) ? fma(acc[v], acc[v], ss) : ss;   // data rows only
+    }
+    ss += __shfl_xor(ss, 16, 64);   // (q0 + q1) + (q2 + q3)
+    ss += __shfl_xor(ss, 32, 64);
+    if (q == 0 && col) {
+        const double psn = (1.0 / (d.bs + 0.5 * ss)) * Gps_c;   // dc:170
+        ps[(uint32_t)(m * d.PP + j0 + c)] = psn;
+        omega[(uint32_t)(m * d.PP + j0 + c)] = 1.0 / psn;        // dc:171 (Q1)
+    }
+}
 constexpr int LAM_PIPE = 4;   // image columns read ahead of their trailing-update FMAs
 __host__ __device__ constexpr int lam_ncol(int KE, int b) { return 8 * b + 8 < KE ? 8 * b + 8 : KE; }
 
@@ -145,7 +188,9 @@ __device__ __forceinline__ LamPiv lam_pivots(d2 pk, d2 pk1, d2 bb) {
 }
 
 template <int KE>
-__global__ __launch_bounds__(64 * LAM_WAVES) void k_lambda(Dims d, const double *__restrict__ C, const double *__restrict__ E,
+// waves_per_eu(2): the residual fixup's MFMA accumulator must share the row path's 250 VGPRs (left
+// alone, hipcc put it in AGPRs: 258 registers, one wave per SIMD)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_lambda(Dims d, const double *__restrict__ C, const double *__restrict__ E,
                                                const double *__restrict__ yy, const double *__restrict__ tau_cur,
                                                double *__restrict__ Lam, double *__restrict__ psi,
                                                const double *__restrict__ plam_src, double *__restrict__ ps,
@@ -160,24 +205,18 @@ __global__ __launch_bounds__(64 * LAM_WAVES) void k_lambda(Dims d, const double 
     constexpr int LSN = 2 * LAM_ROWS * (KP + 1) * 2, BSN = 2 * LAM_ROWS * (KP + 2), VSN = LAM_ROWS * (KP + 2);
     constexpr int EP = KP + 2;
     static_assert(KP * EP <= LSN + BSN, "E staging fits the image area");
-    constexpr int WSN = LSN + BSN + 2 * VSN + KP;   // one wave's LDS (+ sqrt(diag E_m) for the guard)
-    __shared__ __attribute__((aligned(16))) double SMB[LAM_WAVES * WSN];
-    __shared__ int exact_blk;                       // some row of the block needs dc:169's residual
-    const int wave = threadIdx.x >> 6;
-    double *SM = SMB + wave * WSN;
+    __shared__ __attribute__((aligned(16))) double SM[LSN + BSN + 2 * VSN + KP];   // + sqrt(diag E_m): the guard
     double(*LS)[LAM_ROWS][KP + 1][2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 1][2]>(SM);
     double(*BS)[LAM_ROWS][KP + 2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 2]>(SM + LSN);
     double *Vs = SM + LSN + BSN, *Is = Vs + VSN;
     double *Dg = SM + LSN + BSN + 2 * VSN;          // sqrt(E_m[k][k])
     double *Es = SM;
     const int m = blockIdx.y, mg = d.shard0 + m;
-    const int lane = threadIdx.x & 63, grp = lane >> 3, l = lane & 7;
-    if (threadIdx.x == 0) exact_blk = 0;
-    __syncthreads();
+    const int lane = threadIdx.x, grp = lane >> 3, l = lane & 7;
     Vs += grp * (KP + 2);
     Is += grp * (KP + 2);
-    const int j0 = blockIdx.x * LAM_WAVES * LAM_ROWS;   // the block's first loading row
-    const int j = j0 + wave * LAM_ROWS + grp;
+    const int j0 = blockIdx.x * LAM_ROWS;   // the wave's first loading row
+    const int j = j0 + grp;
     const bool valid = j < d.P;
     const int jj = valid ? j : 0;
     const uint32_t rowoff = (uint32_t)(m * d.PP + jj) * KP, toff = (uint32_t)mg * KP;
@@ -424,14 +463,15 @@ __global__ __launch_bounds__(64 * LAM_WAVES) void k_lambda(Dims d, const double 
     // ---- guard: the identity's rounding error is ~ kappa_j eps with kappa_j = (yy_j + 2 sum_k |x_k C_jk|
     //      + |x|'|E||x|) / SS_j <= (sqrt(yy_j) + s_j)^2 / SS_j, s_j = sum_k |x_k| sqrt(E_kk) (|C_jk| <=
     //      sqrt(E_kk yy_j) and |E_kl| <= sqrt(E_kk E_ll), E a Gram matrix).  Beyond kappa_max (or SS_j <= 0)
-    //      the block's 32 rows take dc:169's residual instead (resid_tile below)
+    //      the wave's 8 rows take dc:169's residual instead (resid_rows8)
     double sabs = 0.0;
 #pragma unroll
     for (int b = 0; b < NB; ++b) sabs = fma(fabs(x[b]), Dg[l + 8 * b < KE ? l + 8 * b : 0], sabs);
     sabs = rowsum8(sabs);
+    bool exact;
     {
         const double SS = yyj + contrib, rt = sqrt(yyj) + sabs;
-        if (valid && l == 0 && !(SS > 0.0 && rt * rt <= kappa_max * SS)) exact_blk = 1;   // benign race: all store 1
+        exact = __any(valid && !(SS > 0.0 && rt * rt <= kappa_max * SS));
     }
     // ---- psi (dc:150, tau of the previous iteration, Q11) and the outputs
     if (valid) {
@@ -439,15 +479,19 @@ __global__ __launch_bounds__(64 * LAM_WAVES) void k_lambda(Dims d, const double 
         for (int b = 0; b < 4; ++b) {
             const int r = l + 8 * b;
             const double ps_b = rv[b] ? (1.0 / (d.df * 0.5 + 0.5 * (x[b] * x[b] * tv[b]))) * G[b] : 0.0;
-            st_agent(Lam + rowoff + r, x[b]);                        // agent scope: resid_tile reads it back
+            Lam[rowoff + r] = x[b];
             cpart[rowoff + r] = ps_b * (x[b] * x[b]);               // mat = psijh .* Lambda.^2 (dc:156)
             if (rv[b]) psi[rowoff + r] = ps_b;
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // Lambda out (agent scope) before the vote
-    __syncthreads();
-    if (exact_blk) {   // dc:169 as written for the block's 32 rows: Ytil = Yd - eta Lambda', sum(Ytil.^2)
-        resid_tile<KP, true>(d, Y, X, Z, Lam, ld.Gps, ps, omega, m, j0, reinterpret_cast<double(*)[32]>(SMB));
+    if (exact) {   // dc:169 as written for the wave's rows: Ytil = Yd - eta Lambda', sum(Ytil.^2)
+        double(*Lm)[KP + 1] = reinterpret_cast<double(*)[KP + 1]>(SM);   // the image area, free now
+#pragma unroll
+        for (int b = 0; b < 4; ++b) Lm[grp][l + 8 * b] = x[b];
+        __builtin_amdgcn_wave_barrier();
+        const int cc = lane & 15;
+        const double gps_c = ld.Gps[(uint32_t)(m * d.P) + (j0 + cc < d.P && cc < LAM_ROWS ? j0 + cc : 0)];
+        resid_rows8(d, Y, X, Z, Lm, gps_c, m, j0, lane, ps, omega);
     } else if (valid && l == 0) {
         const double SS = yyj + contrib;
         const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;     // dc:170
