@@ -1208,12 +1208,12 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         }
         {
             KTimer t(h, DCFM_K_LAMBDA, s);
-            // exact residual: every row block takes ps, omega from dc:169's residual (K <= 32: in k_lambda)
+            // exact residual: k_resid redoes every row below (the guard need not fire)
             const bool exact = h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL;
             launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, lamgen,
-                          exact ? 0.0 : KAPPA_IDENTITY_MAX);
+                          exact ? HUGE_VAL : KAPPA_IDENTITY_MAX);
         }
-        if ((h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL) && d.kp != KP) {   // wide: dc:169's residual, own launch
+        if (h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL) {   // dc:169's residual for every loading row
             KTimer t(h, DCFM_K_RESID, s);
             launch_resid(d, b, dr, it, s, lamgen);
         }

@@ -182,8 +182,8 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &d
                   double *tau_out = nullptr, int64_t delta_iter = 0);
 // gen: K <= 32 reads the variates k_wcol generated into b.ldraw (the generated fused chain)
 // instead of the draw buffers dr (injected draws, k_draws batches).
-// K <= 32: a row block whose SS identity may be off by more than ~kappa_max eps (lambda.h guard) takes
-// ps, omega from dc:169's direct residual instead (resid.h); kappa_max = 0: every block (exact mode)
+// K <= 32: a wave whose SS identity may be off by more than ~kappa_max eps for one of its rows (lambda.h
+// guard) takes its rows' ps, omega from dc:169's direct residual instead (resid_rows8, same launch)
 #ifndef DCFM_KAPPA_MAX
 #define DCFM_KAPPA_MAX 1e3
 #endif
@@ -192,8 +192,8 @@ void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t ite
                    const double *tau_cur, const double *plam_src, hipStream_t s, bool gen = false,
                    double kappa_max = KAPPA_IDENTITY_MAX);
 void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s);
-// resid.hip (DCFM_FLAG_EXACT_RESIDUAL): ps, omega from the direct residual Yd - eta Lambda'
-// (dc:169-171), after the loading-row kernel, with its ps variates (gen: b.ldraw, else dr)
+// resid.hip (DCFM_FLAG_EXACT_RESIDUAL): ps, omega from the direct residual Yd - eta Lambda' (dc:169-171)
+// for every loading row, after the loading-row kernel, with its ps variates (gen: b.ldraw, else dr)
 void launch_resid(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s, bool gen);
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                   const double *delta_in, const double *tau_in, double *delta_out,

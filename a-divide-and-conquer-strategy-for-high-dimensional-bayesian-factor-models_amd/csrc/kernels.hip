@@ -1003,137 +1003,6 @@ __global__ __launch_bounds__(64 * cp_waves<KW>()) __attribute__((amdgpu_waves_pe
     }
 }
 
-// ============================================================================
-// k_cpass_w (wide path, KW = 64 / 128): [C_m | E_m] = [Y_m | eta_m]' eta_m with ONE block per
-// 32-column tile of [Y | eta] producing all KW/32 eta column tiles from one pass over its Y tile
-// (k_cpass re-read the Y tile once per eta column tile: c4 fetched 1.94x its algorithmic bytes).
-// The block walks the rows in 16-row chunks in lockstep: the chunk's [Y | eta] tile (16 x 32, one
-// 16-byte load per thread) is staged in a double-buffered LDS image, register-prefetched one chunk
-// ahead; wave w takes eta column tile kt = w / WPK and, with WPK = 2 (KW = 64), half of the chunk's
-// rows (the two halves summed in a fixed order at the end).  Per 4-row step a lane reads its Y pair
-// from LDS and its eta pair (formed from X and Z, prefetched one chunk ahead) and runs the same four
-// v_mfma_f64_16x16x4 as k_cpass.                                     dc:133,138,141
-// ============================================================================
-template <int KW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_cpass_w(Dims d, const double *__restrict__ Y, const double *__restrict__ X,
-                                                 const double *__restrict__ Z, double *__restrict__ C,
-                                                 double *__restrict__ E) {
-    constexpr int NKT = KW / 32, WPK = 4 / NKT, UPW = 4 / WPK;   // waves per eta tile, 4-row steps per wave
-    static_assert(NKT == 2 || NKT == 4, "KW = 64 or 128");
-    __shared__ __attribute__((aligned(16))) double Ys[2][16][32];
-    __shared__ double red[WPK > 1 ? 2 : 1][32][33];
-    const int nt = (d.PP + KW) >> 5;
-    const int wb = xcd_remap(blockIdx.x, gridDim.x);
-    const int m = wb / nt, tile = wb % nt;
-    const int c0 = tile * 32;
-    const bool isE = c0 >= d.PP;
-    const int te = isE ? (c0 - d.PP) >> 5 : 0;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
-    const int kt = wave / WPK, part = wave % WPK;
-    const int lrow = tid >> 4, lcol = 2 * (tid & 15);
-    const double *Ym = Y + (size_t)m * d.NP * d.PP + c0 + lcol;
-    const double *Zm = Z + (size_t)m * d.NP * KW;
-    auto gstage = [&](int ch) -> d2 {   // the chunk's [Y | eta] tile element of this thread
-        const int i = 16 * ch + lrow;
-        if (!isE) return *reinterpret_cast<const d2 *>(Ym + (size_t)i * d.PP);
-        const d2 xa = *reinterpret_cast<const d2 *>(X + (size_t)i * KW + 32 * te + lcol);
-        const d2 za = *reinterpret_cast<const d2 *>(Zm + (size_t)i * KW + 32 * te + lcol);
-        d2 v;
-        v.x = eta_of(d.sr, d.s1r, xa.x, za.x);
-        v.y = eta_of(d.sr, d.s1r, xa.y, za.y);
-        return v;
-    };
-    auto eload = [&](int ch, d2 (&x)[UPW], d2 (&z)[UPW]) {   // this wave's eta pairs of the chunk
-#pragma unroll
-        for (int u = 0; u < UPW; ++u) {
-            const int i = 16 * ch + 4 * (part * UPW + u) + q;
-            x[u] = *reinterpret_cast<const d2 *>(X + (size_t)i * KW + 32 * kt + 2 * r);
-            z[u] = *reinterpret_cast<const d2 *>(Zm + (size_t)i * KW + 32 * kt + 2 * r);
-        }
-    };
-    d4 acc[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-    auto mma = [&](int buf, const d2 (&x)[UPW], const d2 (&z)[UPW]) {
-#pragma unroll
-        for (int u = 0; u < UPW; ++u) {
-            const d2 y = *reinterpret_cast<const d2 *>(&Ys[buf][4 * (part * UPW + u) + q][2 * r]);
-            const double e0 = eta_of(d.sr, d.s1r, x[u].x, z[u].x), e1 = eta_of(d.sr, d.s1r, x[u].y, z[u].y);
-            acc[0][0] = mfma16x16x4(y.x, e0, acc[0][0]);
-            acc[0][1] = mfma16x16x4(y.x, e1, acc[0][1]);
-            acc[1][0] = mfma16x16x4(y.y, e0, acc[1][0]);
-            acc[1][1] = mfma16x16x4(y.y, e1, acc[1][1]);
-        }
-    };
-    const int nch = d.NP / 16;
-    d2 xa[UPW], za[UPW], xb[UPW], zb[UPW];
-    d2 ys = gstage(0);
-    eload(0, xa, za);
-    *reinterpret_cast<d2 *>(&Ys[0][lrow][lcol]) = ys;
-    __syncthreads();
-    for (int ch = 0; ch < nch; ch += 2) {   // two chunks per trip: the register sets alternate
-        const bool m1 = ch + 1 < nch, m2 = ch + 2 < nch;
-        if (m1) {
-            ys = gstage(ch + 1);
-            eload(ch + 1, xb, zb);
-        }
-        mma(0, xa, za);
-        if (m1) *reinterpret_cast<d2 *>(&Ys[1][lrow][lcol]) = ys;
-        __syncthreads();
-        if (!m1) break;
-        if (m2) {
-            ys = gstage(ch + 2);
-            eload(ch + 2, xa, za);
-        }
-        mma(1, xb, zb);
-        if (m2) *reinterpret_cast<d2 *>(&Ys[0][lrow][lcol]) = ys;
-        __syncthreads();
-    }
-    // lane (r, q): D row rho = q + 4g -> column c0 + 2 rho + ta of [Y | eta]; D col r -> k = 32 kt + 2r + tb
-    auto put = [&](int a, int b, double v) {
-        if (isE) {   // E_m in the loading-row kernel's tile layout (etile_index), upper tiles
-            const int R = 32 * te + a, Cc = 32 * kt + b;
-            if ((R >> 4) <= (Cc >> 4)) E[(size_t)m * KW * KW + etile_index(KW / 16, R, Cc)] = v;
-        } else {
-            C[((size_t)m * d.PP + c0 + a) * KW + 32 * kt + b] = v;
-        }
-    };
-    if constexpr (WPK == 1) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int ta = 0; ta < 2; ++ta)
-#pragma unroll
-                for (int tb = 0; tb < 2; ++tb) put(2 * (q + 4 * g) + ta, 2 * r + tb, acc[ta][tb][g]);
-    } else {   // the kt's two row halves: (part 0) + (part 1), one kt at a time through LDS
-#pragma unroll
-        for (int k2 = 0; k2 < NKT; ++k2) {
-            if (kt == k2) {
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-#pragma unroll
-                    for (int ta = 0; ta < 2; ++ta)
-#pragma unroll
-                        for (int tb = 0; tb < 2; ++tb) red[part][2 * (q + 4 * g) + ta][2 * r + tb] = acc[ta][tb][g];
-            }
-            __syncthreads();
-            for (int e = tid; e < 32 * 32; e += 256) {
-                const int a = e >> 5, b = e & 31;
-                const double v = red[0][a][b] + red[1][a][b];
-                if (isE) {
-                    const int R = 32 * te + a, Cc = 32 * k2 + b;
-                    if ((R >> 4) <= (Cc >> 4)) E[(size_t)m * KW * KW + etile_index(KW / 16, R, Cc)] = v;
-                } else {
-                    C[((size_t)m * d.PP + c0 + a) * KW + 32 * k2 + b] = v;
-                }
-            }
-            __syncthreads();
-        }
-    }
-}
-
 // k_lambda (loading rows, dc:140-145,150,156,169-171): lambda.h
 
 // ============================================================================
@@ -1873,21 +1742,12 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &d
             hipLaunchKernelGGL((k_cpass<32, false>), dim3(grid.x + ndel), dim3(64 * cp_waves<32>()), 0, s, d, b.Y, b.X,
                                b.Z, b.C, b.E, dr, b.sall, da, ndel);
         break;
-#ifndef DCFM_CPASS_WIDE_PER_KT   // (A/B switch: the per-eta-tile k_cpass of rounds 1-3)
-    case 64:
-        hipLaunchKernelGGL(k_cpass_w<64>, dim3(grid.x / 2), dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E);
-        break;
-    default:
-        hipLaunchKernelGGL(k_cpass_w<128>, dim3(grid.x / 4), dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E);
-        break;
-#else
     case 64:
         hipLaunchKernelGGL(k_cpass<64>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E, dr, b.sall, da, 0);
         break;
     default:
         hipLaunchKernelGGL(k_cpass<128>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E, dr, b.sall, da, 0);
         break;
-#endif
     }
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,

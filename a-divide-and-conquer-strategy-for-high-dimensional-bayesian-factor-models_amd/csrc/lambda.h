@@ -209,7 +209,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     double(*LS)[LAM_ROWS][KP + 1][2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 1][2]>(SM);
     double(*BS)[LAM_ROWS][KP + 2] = reinterpret_cast<double(*)[LAM_ROWS][KP + 2]>(SM + LSN);
     double *Vs = SM + LSN + BSN, *Is = Vs + VSN;
-    double *Dg = SM + LSN + BSN + 2 * VSN;          // sqrt(E_m[k][k])
+    double *Dg = SM + LSN + BSN + 2 * VSN;          // E_m[k][k]
     double *Es = SM;
     const int m = blockIdx.y, mg = d.shard0 + m;
     const int lane = threadIdx.x, grp = lane >> 3, l = lane & 7;
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 #pragma unroll
         for (int c = 8 * b; c < nc; ++c)
             if (c == l + 8 * b) {
-                if (grp == 0) Dg[c] = sqrt(q[c]);          // E_m is the wave's, whatever the row
+                if (grp == 0) Dg[c] = q[c];                // E_m[k][k] (the wave's, whatever the row)
                 q[c] += dg[b];
             }
     });
@@ -464,13 +464,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     //      + |x|'|E||x|) / SS_j <= (sqrt(yy_j) + s_j)^2 / SS_j, s_j = sum_k |x_k| sqrt(E_kk) (|C_jk| <=
     //      sqrt(E_kk yy_j) and |E_kl| <= sqrt(E_kk E_ll), E a Gram matrix).  Beyond kappa_max (or SS_j <= 0)
     //      the wave's 8 rows take dc:169's residual instead (resid_rows8)
+    //      Square roots as v * rsq(v) from the hardware estimate (a bound needs no correct rounding; the
+    //      factor 1.01 covers its error); a zero yy_j gives NaN, read as "take the residual"
     double sabs = 0.0;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) sabs = fma(fabs(x[b]), Dg[l + 8 * b < KE ? l + 8 * b : 0], sabs);
+    for (int b = 0; b < NB; ++b) {
+        const double e = Dg[l + 8 * b < KE ? l + 8 * b : 0];
+        sabs = (rv[b] && e > 0.0) ? fma(fabs(x[b]), e * __builtin_amdgcn_rsq(e), sabs) : sabs;
+    }
     sabs = rowsum8(sabs);
     bool exact;
     {
-        const double SS = yyj + contrib, rt = sqrt(yyj) + sabs;
+        const double SS = yyj + contrib, rt = 1.01 * (yyj * __builtin_amdgcn_rsq(yyj) + sabs);
         exact = __any(valid && !(SS > 0.0 && rt * rt <= kappa_max * SS));
     }
     // ---- psi (dc:150, tau of the previous iteration, Q11) and the outputs

@@ -1,15 +1,14 @@
-// Residual-precision update by the reference's own formula, as a launch of its own: the wide
-// (K > 32) path with DCFM_FLAG_EXACT_RESIDUAL.  (The narrow path runs the same tile code inside
-// k_lambda: lambda.h.)
+// Residual-precision update by the reference's own formula for every loading row, as a launch of
+// its own after the loading-row kernel (DCFM_FLAG_EXACT_RESIDUAL).  The default K <= 32 chain runs
+// the same arithmetic per wave inside k_lambda where its guard rejects the SS identity (lambda.h).
 //
 // The default chain forms SS_j = sum_i Ytil_ij^2 inside the loading-row kernel by the identity
 // yy_j - 2 lambda_j.C_j + lambda_j E lambda_j' (no Y pass).  That sum cancels when SS_j is
 // small against its terms: its rounding error grows like kappa_j eps with kappa_j = (yy_j +
 // 2 sum_k |lambda_jk C_jk| + |lambda_j| |E| |lambda_j|') / SS_j (measured ~1e6 at the second
 // iteration of config c2, where the X excursions make E large: 1.3e-10 relative in SS).  The
-// direct residual's error grows like sqrt(kappa_j) eps.  With the flag, k_resid runs after
-// k_lambda_w and overwrites ps and omega from the direct residual (resid.h): a third pass over
-// Y, the reference's own third product.
+// direct residual's error grows like sqrt(kappa_j) eps.  k_resid overwrites ps and omega from the
+// direct residual (resid.h): a pass over the tile's Y columns, the reference's own third product.
 //
 // k_resid<KW>: block = (32-column tile of shard m's loading rows, shard m), resid_tile's 4 waves.
 #include "resid.h"

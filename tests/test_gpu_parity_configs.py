@@ -32,10 +32,11 @@ ps and omega (dc:168-172), at every iteration of every case: per row, UNSCALED r
 applied to the GPU's own eta and Lambda; the oracle chain takes the residual too
 (oracle.vectorised direct=True).  Two modes, c1-c4 each:
   exact    DCFM_FLAG_EXACT_RESIDUAL: every loading row's ps, omega from the direct residual on the
-           device (K <= 32: inside k_lambda, resid.h; K > 32: k_resid);
+           device (k_resid, resid.hip);
   default  the throughput path: SS_j by the identity yy_j - 2 lam_j.C_j + lam_j E lam_j' inside the
            loading-row kernel, except where its cancellation could cost more than ~1e3 eps (the
-           kappa guard in lambda.h): those row blocks take the direct residual.  At c2's second
+           kappa guard in lambda.h): those waves take the direct residual for their 8 rows
+           (resid_rows8, same launch).  At c2's second
            iteration the identity alone is 1.3e-10 off (kappa_j ~ 1e6: its error grows like
            kappa_j eps, the residual's like sqrt(kappa_j) eps); the guard sends those rows to the
            residual.  The wide path (c4, K = 100) has no guard: the identity there, checked at
