@@ -26,7 +26,9 @@
 //   Sigma  [ntiles][128][128]  this rank's block of the lower triangle of Sigmaout, tile-packed:
 //                        rank r owns the contiguous tile rows [T0, T1) (balanced by tile count,
 //                        sigma_split), tile (ti, tj), tj <= ti, at index tri(ti) - tri(T0) + tj,
-//                        row-major inside (a % 128, b % 128); ~p^2 / (2 nranks) doubles per rank
+//                        inside in k_assemble's accumulator order (sig_tile_off: each lane's two
+//                        values of a 16x16 MFMA tile adjacent, so a wave moves the tile with 16-byte
+//                        accesses); ~p^2 / (2 nranks) doubles per rank
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -138,9 +140,17 @@ __host__ __device__ inline int xsum_blocks(int G) {
 // Sigma block-sharding helpers (host + device)
 __host__ __device__ inline long long tri(long long t) { return t * (t + 1) / 2; }
 // offset of the stored element (a, b), a >= b, in a rank's tile-packed Sigma (owner of tile row a/128)
+// Inside a tile, element (ra, cb) sits where k_assemble's wave w = 2 (ra / 64) + cb / 64 holds it
+// in the f64 MFMA C/D layout: 16x16 tile (u, v) = ((ra / 16) % 4, (cb / 16) % 4), row ra % 16 =
+// q + 4 g, lane q * 16 + cb % 16; the lane's values g = 2 h, 2 h + 1 are adjacent, so a wave moves
+// one (u, v, h) slice as one 16-byte access per lane, 1 KiB contiguous
+__host__ __device__ inline int sig_tile_off(int u, int v, int g, int w, int lane) {
+    return ((((w * 4 + u) * 4 + v) * 2 + (g >> 1)) * 64 + lane) * 2 + (g & 1);
+}
 __host__ __device__ inline size_t sig_off(int a, int b, int T0) {
-    const int ta = a / ASM_TILE, tb = b / ASM_TILE;
-    return ((size_t)(tri(ta) - tri(T0) + tb) * ASM_TILE + (a % ASM_TILE)) * ASM_TILE + (b % ASM_TILE);
+    const int ta = a / ASM_TILE, tb = b / ASM_TILE, ra = a % ASM_TILE, cb = b % ASM_TILE, rr = ra & 15;
+    return (size_t)(tri(ta) - tri(T0) + tb) * ASM_TILE * ASM_TILE +
+           sig_tile_off((ra >> 4) & 3, (cb >> 4) & 3, rr >> 2, 2 * (ra >> 6) + (cb >> 6), (rr & 3) * 16 + (cb & 15));
 }
 // Packed window of a rank owning rows [R0, R1) in a column stripe: column c holds the rows
 // [lo(c), R1) of Sigmaout(:, c) it owns (lo = 0 for c in [R0, R1): the upper part mirrored from

@@ -1491,13 +1491,19 @@ __device__ __forceinline__ void assemble_tile(const Dims &d, const double *__res
     };
     gload(0);      // ahead of the tile's Sigma loads: staging chunk 0 waits only for its panels
     d4 acc[4][4];
+    // the tile's values of this wave's accumulators: slice (u, v, h) = 64 lanes x 16 B, contiguous
+    auto sl = [&](int u, int v, int h) { return reinterpret_cast<d2 *>(St + sig_tile_off(u, v, 2 * h, wave, lane)); };
     if (cross) {   // acc = the tile's old values (C/D layout: row q + 4g of 16-row tile u)
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int v = 0; v < 4; ++v)
 #pragma unroll
-                for (int g = 0; g < 4; ++g) acc[u][v][g] = __builtin_nontemporal_load(&St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r]);
+                for (int h = 0; h < 2; ++h) {
+                    const d2 o = __builtin_nontemporal_load(sl(u, v, h));
+                    acc[u][v][2 * h] = o.x;
+                    acc[u][v][2 * h + 1] = o.y;
+                }
     } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -1532,10 +1538,15 @@ __device__ __forceinline__ void assemble_tile(const Dims &d, const double *__res
 #pragma unroll
             for (int v = 0; v < 4; ++v)
 #pragma unroll
-                for (int g = 0; g < 4; ++g) __builtin_nontemporal_store(acc[u][v][g], &St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r]);
+                for (int h = 0; h < 2; ++h) {
+                    d2 o;
+                    o.x = acc[u][v][2 * h];
+                    o.y = acc[u][v][2 * h + 1];
+                    __builtin_nontemporal_store(o, sl(u, v, h));
+                }
         return;
     }
-    // epilogue: lower-triangle read-modify-write of the tile (tile-packed, row-major inside),
+    // epilogue: lower-triangle read-modify-write of the tile (tile-packed, accumulator order inside),
     // loads issued together (predicated, no branches around them), shard test from the LDS table
     const int a0 = T.x * ASM_TILE + wa, b0 = T.y * ASM_TILE + wb;
     int sb[4];
@@ -1551,7 +1562,7 @@ __device__ __forceinline__ void assemble_tile(const Dims &d, const double *__res
             for (int v = 0; v < 4; ++v) {
                 const int b = b0 + 16 * v + r;
                 const bool live = a < p && b <= a;
-                old[g][v] = live ? __builtin_nontemporal_load(&St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r]) : 0.0;
+                old[g][v] = live ? __builtin_nontemporal_load(&St[sig_tile_off(u, v, g, wave, lane)]) : 0.0;
             }
         }
 #pragma unroll
@@ -1566,7 +1577,7 @@ __device__ __forceinline__ void assemble_tile(const Dims &d, const double *__res
                     const double coef = (sb[v] == sa) ? 1.0 : d.rho;
                     double val = coef * acc[u][v][g] * inv_eff;
                     if (a == b) val += dg;
-                    __builtin_nontemporal_store(old[g][v] + val, &St[(wa + 16 * u + q + 4 * g) * ASM_TILE + wb + 16 * v + r]);
+                    __builtin_nontemporal_store(old[g][v] + val, &St[sig_tile_off(u, v, g, wave, lane)]);
                 }
             }
         }
