@@ -40,7 +40,7 @@ EXPORTS = (
     "dcfm_comm_unique_id", "dcfm_comm_init", "dcfm_comm_init_loopback", "dcfm_set_data", "dcfm_set_state",
     "dcfm_set_draws", "dcfm_run", "dcfm_synchronize", "dcfm_get_state", "dcfm_get_sigma",
     "dcfm_get_sigma_cols", "dcfm_sigma_block",
-    "dcfm_saved_samples", "dcfm_sigma_error", "dcfm_set_profiling", "dcfm_set_profiling_mask", "dcfm_get_kernel_stats",
+    "dcfm_saved_samples", "dcfm_sigma_error", "dcfm_set_profiling", "dcfm_set_profiling_mask", "dcfm_set_profiling_stride", "dcfm_get_kernel_stats",
     "dcfm_kernel_name",
     "dcfm_rng_fill", "dcfm_set_data_raw", "dcfm_get_data", "dcfm_count_nonzero_columns",
     "dcfm_set_trace", "dcfm_get_trace", "dcfm_init_state",
@@ -113,6 +113,7 @@ def load_library(path: Path | None = None):
         "dcfm_sigma_error": (C.c_int, [vp, _DP, C.c_int32, _DP, C.c_int32, C.c_uint64, _DP]),
         "dcfm_set_profiling": (C.c_int, [vp, C.c_int]),
         "dcfm_set_profiling_mask": (C.c_int, [vp, C.c_uint32]),
+        "dcfm_set_profiling_stride": (C.c_int, [vp, C.c_int32]),
         "dcfm_get_kernel_stats": (C.c_int, [vp, _DP, C.POINTER(C.c_int64)]),
         "dcfm_kernel_name": (C.c_char_p, [C.c_int]),
         "dcfm_rng_fill": (C.c_int, [C.c_int, C.c_uint64, C.c_int, C.c_double, C.c_int32, C.c_int32,

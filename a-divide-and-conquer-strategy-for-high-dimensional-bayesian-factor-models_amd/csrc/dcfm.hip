@@ -102,6 +102,8 @@ struct dcfm_handle {
     int64_t trace_cap = 0, trace_n = 0;
     bool prof = false;
     uint32_t prof_mask = 0;       // kernel ids (bit DCFM_K_*) timed with events
+    int prof_stride = 1;          // time one in prof_stride launches of each (dcfm_set_profiling_stride)
+    int64_t prof_seq[DCFM_K_COUNT] = {};   // launches seen per kernel id since the mask was set
     std::vector<ProfRec> recs;
     std::vector<hipEvent_t> evpool;
     double kms[DCFM_K_COUNT] = {};
@@ -287,7 +289,7 @@ struct KTimer {
     hipStream_t s;
     hipEvent_t a = nullptr;
     KTimer(dcfm_handle *h_, int k, hipStream_t s_) : h(h_), kid(k), s(s_) {
-        if (h->prof && (h->prof_mask >> k & 1u)) {
+        if (h->prof && (h->prof_mask >> k & 1u) && h->prof_seq[k]++ % h->prof_stride == 0) {
             a = get_event(h);
             if (a) (void)hipEventRecord(a, s);
         }
@@ -1606,12 +1608,22 @@ int dcfm_set_profiling_mask(dcfm_handle *h, uint32_t mask) {
     if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
     collect_prof(h);
     h->prof_mask = mask;
+    h->prof_stride = 1;
+    std::fill(h->prof_seq, h->prof_seq + DCFM_K_COUNT, (int64_t)0);
     const bool enable = mask != 0;
     h->prof = enable;
     if (enable) {
         std::fill(h->kms, h->kms + DCFM_K_COUNT, 0.0);
         std::fill(h->kcnt, h->kcnt + DCFM_K_COUNT, 0);
     }
+    return DCFM_OK;
+}
+
+int dcfm_set_profiling_stride(dcfm_handle *h, int32_t stride) {
+    if (!h) return fail(h, DCFM_ERR_INVALID, "null handle");
+    if (stride < 1) return fail(h, DCFM_ERR_INVALID, "profiling stride %d < 1", (int)stride);
+    h->prof_stride = stride;
+    std::fill(h->prof_seq, h->prof_seq + DCFM_K_COUNT, (int64_t)0);
     return DCFM_OK;
 }
 

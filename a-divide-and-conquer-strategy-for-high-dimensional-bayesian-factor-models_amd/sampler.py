@@ -245,12 +245,15 @@ class Sampler:
     def set_profiling(self, on: bool):
         self._check(self.lib.dcfm_set_profiling(self.h, 1 if on else 0))
 
-    def set_profiling_kernels(self, names):
-        """Time only these kernels (names of _abi.KERNEL_IDS); empty = off."""
+    def set_profiling_kernels(self, names, stride: int = 1):
+        """Time only these kernels (names of _abi.KERNEL_IDS); empty = off.  stride > 1 times
+        one in `stride` launches of each (the event records cost device time per launch)."""
         mask = 0
         for nm in names:
             mask |= 1 << _abi.KERNEL_IDS[nm]
         self._check(self.lib.dcfm_set_profiling_mask(self.h, mask))
+        if stride != 1:
+            self._check(self.lib.dcfm_set_profiling_stride(self.h, int(stride)))
 
     def kernel_stats(self) -> dict:
         ms = (C.c_double * _abi.K_COUNT)()
