@@ -30,7 +30,6 @@ sys.path.insert(0, str(ROOT))
 METRIC = "Gibbs iters/sec (node) at p=20k,n=1k,g=64; cov-assembly MFMA util %"
 FP64_MFMA_PEAK_TFLOPS = 78.6      # MI355X dense fp64 matrix (spec; = fp64 vector)
 HBM_PEAK_GBS = 8000.0             # MI355X HBM3E spec
-PROF_SAMPLES = 5                  # timed launches of the roofline kernel in the timed region (sampled)
 
 
 def synth_data(n, p, k0=10, sparsity=0.7, seed=20161209, factors=False):
@@ -201,6 +200,9 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=10)
     ap.add_argument("--no-faithful", action="store_true", help="skip the faithful-loop CPU leg (~30 s)")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--timed-samples", type=int, default=0,
+                    help="time only this many launches of the roofline kernel inside the timed region "
+                         "(0 = every launch; sampling measured no wall-clock difference: DESIGN §5)")
     ap.add_argument("--exact-residual", action="store_true",
                     help="DCFM_FLAG_EXACT_RESIDUAL: ps / omega from dc:169's direct residual (k_resid, one "
                          "more Y pass) instead of the SS identity; the parity mode, timed for its cost")
@@ -323,11 +325,9 @@ def main():
     if n_trace >= 4:
         trace = smp.get_trace()
         smp.set_trace(0)                    # the timed region records nothing
-    # (2) the timed region: events only around the roofline kernel (live duration), on a sample
-    #     of its launches — every timed launch puts two event records on the stream, ~5 us of
-    #     device time each (measured as idle before and after the kernel in a rocprofv3 trace:
-    #     DESIGN §5), so timing all 20 launches of the driver's command cost ~5 % of the region
-    prof_stride = 1 if dominant == "k_assemble" else max(1, args.steps // PROF_SAMPLES)
+    # (2) the timed region: events only around the roofline kernel (live duration); on every
+    #     launch by default (--timed-samples N: on N of them)
+    prof_stride = 1 if dominant == "k_assemble" or args.timed_samples <= 0 else max(1, args.steps // args.timed_samples)
     if dominant:
         smp.set_profiling_kernels([dominant], stride=prof_stride)
     barrier(); sync()
@@ -461,7 +461,7 @@ def main():
                 "launches": int(cnt), "launches_in_region": int(region_n), "timed_every": prof_stride,
                 "note": "achieved = algorithmic work per launch / mean HIP-event duration of this kernel, "
                         "events recorded around it alone inside the timed region, on one in timed_every "
-                        "of its launches (each event record costs ~5 us of device time)"}
+                        "of its launches"}
 
     wtag = {(64, 312, 1000, 30): "c3", (8, 1250, 2000, 100): "c4", (256, 391, 2000, 30): "c5"}.get(
         (g, P, n, K), "custom")

@@ -230,9 +230,9 @@ int  dcfm_set_profiling(dcfm_handle *h, int enable);
 /* Time only the kernels whose bit (1u << DCFM_K_*) is set: two events per timed
  * launch cost host time, so a throughput run times just the kernel it reports. */
 int  dcfm_set_profiling_mask(dcfm_handle *h, uint32_t mask);
-/* Time one in `stride` launches of each timed kernel (the first of every `stride`; default 1):
- * each timed launch puts two event records on its stream (~5 us of device time each), so a
- * throughput run samples the kernel it reports.  Reset to 1 by dcfm_set_profiling[_mask]. */
+/* Time one in `stride` launches of each timed kernel (the first of every `stride`; default 1),
+ * e.g. to keep event records off most launches of a long run.  Reset to 1 by
+ * dcfm_set_profiling[_mask]. */
 int  dcfm_set_profiling_stride(dcfm_handle *h, int32_t stride);
 int  dcfm_get_kernel_stats(dcfm_handle *h, double ms[DCFM_K_COUNT], int64_t launches[DCFM_K_COUNT]);
 const char *dcfm_kernel_name(int id);
