@@ -93,7 +93,8 @@ def config_key(args, world):
     """The bench invocation a PMC summary must match (workload, flush sizes, step counts)."""
     return (f"g{args.g}_P{args.P}_n{args.n}_K{args.K}_thin{args.thin}_asm{args.asm_batch}_"
             f"steps{args.steps}_warmup{args.warmup}_gpus{world}{'_chains' if args.chains else ''}"
-            f"{'_exact' if args.exact_residual else ''}")
+            f"{'_exact' if args.exact_residual else ''}"
+            f"{'_flags%x' % args.layout_flags if args.layout_flags else ''}")
 
 
 # HIP-event role name -> the kernel rocprofv3 records it under (the fused K <= 32 chain's W pass
@@ -203,6 +204,9 @@ def main():
     ap.add_argument("--timed-samples", type=int, default=0,
                     help="time only this many launches of the roofline kernel inside the timed region "
                          "(0 = every launch; sampling measured no wall-clock difference: DESIGN §5)")
+    ap.add_argument("--layout-flags", type=lambda v: int(v, 0), default=0,
+                    help="extra dcfm_config.flags layout bits (DCFM_FLAG_ONE_STREAM 0x4, "
+                         "DCFM_FLAG_FLAT_PRIORITY 0x8, DCFM_FLAG_UNFUSED 0x2) for layout comparisons")
     ap.add_argument("--exact-residual", action="store_true",
                     help="DCFM_FLAG_EXACT_RESIDUAL: ps / omega from dc:169's direct residual (k_resid, one "
                          "more Y pass) instead of the SS identity; the parity mode, timed for its cost")
@@ -269,7 +273,7 @@ def main():
 
     smp = dcfm.Sampler(n, P, g, K, rho, burnin, mcmc, thin, seed=1 + (rank if chains else 0),
                        nranks=shard_ranks, rank=0 if chains else rank, device=device,
-                       asm_batch=args.asm_batch, flags=0x10 if args.exact_residual else 0)
+                       asm_batch=args.asm_batch, flags=(0x10 if args.exact_residual else 0) | args.layout_flags)
     if shard_ranks > 1:
         obj = [dcfm.Sampler.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
