@@ -537,6 +537,11 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
     }
     ALLOC(b.XM, 2 * KP * KP);
     ALLOC(b.agree, 3);
+    {
+        double *rf = nullptr;
+        ALLOC(rf, (G * (PP / 32) + 1) / 2);   // zeroed: no tile flagged
+        b.rflag = reinterpret_cast<int *>(rf);
+    }
     ALLOC(b.xpart, (size_t)G * KP * KP);  // k_wcol: xsum_blocks(G) <= G chunk sums
     {
         double *tk = nullptr;
@@ -1218,6 +1223,9 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         if (h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL) {   // dc:169's residual for every loading row
             KTimer t(h, DCFM_K_RESID, s);
             launch_resid(d, b, dr, it, s, lamgen);
+        } else if (d.kp != KP) {                          // K > 32: the tiles k_lambda_w's guard flagged
+            KTimer t(h, DCFM_K_RESID, s);
+            launch_resid_flagged(d, b, dr, it, s);
         }
         h->plam_valid = false;
         if (fused) {

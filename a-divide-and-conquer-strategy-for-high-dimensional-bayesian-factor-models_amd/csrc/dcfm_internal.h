@@ -116,6 +116,8 @@ struct Bufs {
                                        // [SYNC_ZM + m] = k_wcol Z operators of shard m out
     double *msg_all;                   // packed gather target (fused, nranks > 1), else null
     double *agree;                     // 3 doubles: the failure counts of a collective call (dcfm.hip agree)
+    int *rflag;                        // K > 32: [G][PP / 32] 32-row tiles whose SS identity the guard of
+                                       // k_lambda_w rejected (k_resid_flagged redoes them and clears the flag)
     int2 *tiles;
     int ntiles, LDB;
     int T0, T1;                        // owned tile rows of Sigma (block-sharded, see above)
@@ -205,6 +207,9 @@ void launch_colsum(const Dims &d, const Bufs &b, hipStream_t s);
 // resid.hip (DCFM_FLAG_EXACT_RESIDUAL): ps, omega from the direct residual Yd - eta Lambda' (dc:169-171)
 // for every loading row, after the loading-row kernel, with its ps variates (gen: b.ldraw, else dr)
 void launch_resid(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s, bool gen);
+// K > 32, default mode: the same for the 32-row tiles k_lambda_w's guard flagged (b.rflag); the other
+// blocks exit at once
+void launch_resid_flagged(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                   const double *delta_in, const double *tau_in, double *delta_out,
                   double *tau_out, hipStream_t s);
@@ -248,7 +253,7 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s);
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s);
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *tau_cur,
-                   const double *plam_src, hipStream_t s);
+                   const double *plam_src, hipStream_t s, double kappa_max);
 void launch_delta(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *delta_in,
                   const double *tau_in, double *delta_out, double *tau_out, hipStream_t s);
 }  // namespace wide

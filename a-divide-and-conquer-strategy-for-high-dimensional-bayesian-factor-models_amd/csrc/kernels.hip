@@ -1763,7 +1763,7 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &d
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
                    const double *tau_cur, const double *plam_src, hipStream_t s, bool gen, double kappa_max) {
-    if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, plam_src, s);
+    if (d.kp != KP) return wide::launch_lambda(d, b, dr, iter, tau_cur, plam_src, s, kappa_max);
     LamDraws ld;
     if (gen) {   // this iteration's variates, drawn by k_wcol's LAMGEN blocks (lam_draws)
         const LamGen g = lam_gen_plan(d, b.ldraw);

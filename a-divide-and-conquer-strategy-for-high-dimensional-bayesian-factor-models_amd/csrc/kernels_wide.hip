@@ -16,6 +16,7 @@
 //              Cholesky of Q_j (8x8 blocks per thread), fused forward   dc:156,169-171
 //              solve, blocked back solve; psi, SS identity, ps, omega
 //   k_delta    MGP chain over up to 128 factors (2 per lane)            dc:155-165
+#include <cmath>
 #include <cstdlib>
 
 #include "dcfm_internal.h"
@@ -359,10 +360,11 @@ __global__ __launch_bounds__(64) void k_lambda_w(
     Dims d, const double *__restrict__ C, const double *__restrict__ E, const double *__restrict__ yy,
     const double *__restrict__ tau_cur, const double *__restrict__ plam_src, double *__restrict__ Lam,
     double *__restrict__ psi, double *__restrict__ ps, double *__restrict__ omega, double *__restrict__ cpart,
-    DrawsDev dr, int64_t iter) {
+    DrawsDev dr, int64_t iter, double kappa_max, int *__restrict__ rflag) {
     constexpr int NT = NB * (NB + 1) / 2, LD = 17, TZ = 16 * LD, NH = KW / 64;
     __shared__ double Sd[TZ], Ud[TZ];
     __shared__ double vb[KW], vx[KW], ein[5][KW];   // per row index r: NL, Gpsi, tau, C, Plam
+    __shared__ double edg[KW], udg[KW];             // the guard: E_m[r][r], 1 / L_rr (L = chol(Q_j))
     __shared__ double lds_l[32], lds_u[16];
     const int j = blockIdx.x, m = blockIdx.y, mg = d.shard0 + m;
     const int lane = threadIdx.x, c16 = lane & 15, q = lane >> 4;
@@ -395,6 +397,12 @@ __global__ __launch_bounds__(64) void k_lambda_w(
                 T[utix<NB>(Kc, I)] = d4{e0.x, e0.y, e1.x, e1.y};
             }
         });
+    });
+    static_for<NB>([&](auto JC) {                       // diag(E_m): lane (c16, q) holds T[q + 4g][c16]
+        constexpr int J = decltype(JC)::value;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            if (q + 4 * g == c16) edg[16 * J + c16] = T[utix<NB>(J, J)][g];
     });
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
@@ -445,6 +453,7 @@ __global__ __launch_bounds__(64) void k_lambda_w(
         __syncthreads();
         chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
         __syncthreads();
+        if (q == 0) udg[16 * J + c16] = Ud[c16 * LD + c16];                    // 1 / L_kk (the guard)
         double u[4], bq[4];
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
@@ -528,7 +537,11 @@ __global__ __launch_bounds__(64) void k_lambda_w(
         if (lane + 64 * h >= 16 * NB) vx[lane + 64 * h] = 0.0;
     __syncthreads();
     // ---- epilogue: Lambda_j, psi_j (dc:150), cpart (dc:156), SS_j (dc:169), ps_j, omega_j
-    double ssr = 0.0;
+    //      + the guard of the SS identity (as k_lambda's, lambda.h): kappa_j = max(yy_j + (1 + c_j) |w|^2 / ps_j
+    //      + sum_r Plam_jr x_r^2 / ps_j + 2 sum_r |x_r C_jr|,  (sqrt(yy_j) + sum_r |x_r| sqrt(E_rr))^2) / SS_j,
+    //      c_j = max_r Q_rr / L_rr^2; a row beyond kappa_max (or SS_j <= 0) flags its 32-row tile, whose
+    //      ps, omega k_resid_flagged then takes from dc:169's residual
+    double ssr = 0.0, mag = 0.0, ww = 0.0, sab = 0.0, cs = 1.0;
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
         const int r = lane + 64 * h;
@@ -538,19 +551,35 @@ __global__ __launch_bounds__(64) void k_lambda_w(
             const double scale = 1.0 / (d.df * 0.5 + 0.5 * (xv * xv * ein[2][r]));
             psir = scale * ein[1][r];
             psi[rowoff + r] = psir;
-            const double w = vb[r];
-            ssr += fma(w, w, -ein[4][r] * xv * xv) / psj - 2.0 * xv * ein[3][r];
+            const double w = vb[r], px = ein[4][r] * xv * xv, xc = xv * ein[3][r];
+            ssr += fma(w, w, -px) / psj - 2.0 * xc;
+            ww = fma(w, w, ww);
+            mag += px / psj + 2.0 * fabs(xc);
+            const double e = edg[r], ik = udg[r];
+            sab = e > 0.0 ? fma(fabs(xv), e * __builtin_amdgcn_rsq(e), sab) : sab;
+            cs = fmax(cs, fma(psj, e, ein[4][r]) * ik * ik);
         }
         Lam[rowoff + r] = xv;
         cpart[rowoff + r] = psir * (xv * xv);          // mat = psijh .* Lambda.^2 (dc:156)
     }
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) ssr += __shfl_xor(ssr, o, 64);
+    for (int o = 32; o >= 1; o >>= 1) {
+        ssr += __shfl_xor(ssr, o, 64);
+        mag += __shfl_xor(mag, o, 64);
+        ww += __shfl_xor(ww, o, 64);
+        sab += __shfl_xor(sab, o, 64);
+        cs = fmax(cs, __shfl_xor(cs, o, 64));
+    }
     if (lane == 0) {
         const double SS = yyj + ssr;
         const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;      // dc:170
         ps[(size_t)m * d.PP + j] = psn;
         omega[(size_t)m * d.PP + j] = 1.0 / psn;                 // dc:171 (Q1)
+        if (rflag) {
+            const double rt = 1.01 * (yyj * __builtin_amdgcn_rsq(yyj) + sab);
+            const double num = fmax(rt * rt, 1.01 * (yyj + mag + (1.0 + cs) * ww / psj));
+            if (!(SS > 0.0 && num <= kappa_max * SS)) rflag[m * (d.PP / 32) + j / 32] = 1;
+        }
     }
 }
 
@@ -705,11 +734,12 @@ void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
                                            dr, iter));
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *tau_cur,
-                   const double *plam_src, hipStream_t s) {
+                   const double *plam_src, hipStream_t s, double kappa_max) {
     const dim3 grid(d.P, d.G);
+    int *rflag = std::isinf(kappa_max) ? nullptr : b.rflag;   // exact mode: k_resid redoes every row
 #define LT(KWV, NBV)                                                                                             \
     hipLaunchKernelGGL((k_lambda_w<KWV, NBV>), grid, dim3(64), 0, s, d, b.C, b.E, b.yy, tau_cur, plam_src, b.Lam, \
-                       b.psi, b.ps, b.omega, b.cpart, dr, iter)
+                       b.psi, b.ps, b.omega, b.cpart, dr, iter, kappa_max, rflag)
     switch ((d.K + 15) / 16) {            // K = 33..128: 3..8 tile rows
     case 3: LT(64, 3); break;
     case 4: LT(64, 4); break;

@@ -447,23 +447,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     // ---- SS_j = yy_j - 2 x.C_j + x'E x (dc:169 by identity, no Y pass).  x = L_Q'^{-1} w, so
     //      x'Q_j x = |w|^2 and x'E x = (|w|^2 - sum_r Plam_jr x_r^2) / ps_j: no E re-read;
     //      ps_j x.C_j = x.blam = x.(L_Q v) = (L_Q'x).v = w.v: no C re-read.
-    double ww = 0.0, wv = 0.0, px = 0.0;
+    double ww = 0.0, wv = 0.0, wva = 0.0, px = 0.0, cs = 1.0;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-        const double vr = Vs[l + 8 * b < KE ? l + 8 * b : 0];
+        const int r = l + 8 * b < KE ? l + 8 * b : 0;
+        const double vr = Vs[r];
         const double w = vr + z[b];
         ww = rv[b] ? fma(w, w, ww) : ww;
         wv = rv[b] ? fma(w, vr, wv) : wv;
+        wva = rv[b] ? wva + fabs(w * vr) : wva;
         x[b] = rv[b] ? x[b] * isj : 0.0;                           // Lambda_j = L^{-T} w / sqrt(ps_j)
         px = fma(pl2[b] * x[b], x[b], px);
+        // the pivot's share of its diagonal, Q_kk / L_kk^2 >= 1 (normalised system E + diag(Plam / ps))
+        const double ik = Is[r];
+        cs = rv[b] ? fmax(cs, (Dg[r] + pl2[b] * ipsj) * ik * ik) : cs;
     }
     double contrib = (ww - px - 2.0 * wv) * ipsj;
     contrib = valid ? contrib : 0.0;
     contrib = rowsum8(contrib);
-    // ---- guard: the identity's rounding error is ~ kappa_j eps with kappa_j = (yy_j + 2 sum_k |x_k C_jk|
-    //      + |x|'|E||x|) / SS_j <= (sqrt(yy_j) + s_j)^2 / SS_j, s_j = sum_k |x_k| sqrt(E_kk) (|C_jk| <=
-    //      sqrt(E_kk yy_j) and |E_kl| <= sqrt(E_kk E_ll), E a Gram matrix).  Beyond kappa_max (or SS_j <= 0)
-    //      the wave's 8 rows take dc:169's residual instead (resid_rows8)
+    // ---- guard: the identity's rounding error is ~ kappa_j eps, kappa_j = (the magnitudes it sums) / SS_j.
+    //      Two bounds on those magnitudes, the larger taken:
+    //      * as computed: yy_j + (|w|^2 + sum_r Plam_jr x_r^2 + 2 sum_r |w_r v_r|) / ps_j, with |w|^2 weighted
+    //        by 1 + c_j, c_j = max_k Q_kk / L_kk^2 (>= 1, scale-invariant): w = L'x holds only to the back
+    //        solve's backward error, which grows with the elimination's loss of the diagonal;
+    //      * a priori: yy_j + 2 sum_k |x_k C_jk| + |x|'|E||x| <= (sqrt(yy_j) + s_j)^2, s_j = sum_k |x_k|
+    //        sqrt(E_kk) (|C_jk| <= sqrt(E_kk yy_j) and |E_kl| <= sqrt(E_kk E_ll), E a Gram matrix).
+    //      Beyond kappa_max (or SS_j <= 0) the wave's 8 rows take dc:169's residual instead (resid_rows8).
     //      Square roots as v * rsq(v) from the hardware estimate (a bound needs no correct rounding; the
     //      factor 1.01 covers its error); a zero yy_j gives NaN, read as "take the residual"
     double sabs = 0.0;
@@ -472,11 +481,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const double e = Dg[l + 8 * b < KE ? l + 8 * b : 0];
         sabs = (rv[b] && e > 0.0) ? fma(fabs(x[b]), e * __builtin_amdgcn_rsq(e), sabs) : sabs;
     }
+    cs = fmax(cs, dpp8_d<0xB1>(cs));
+    cs = fmax(cs, dpp8_d<0x4E>(cs));
+    cs = fmax(cs, dpp8_d<0x141>(cs));
+    double mag = valid ? (fma(cs + 1.0, ww, px) + 2.0 * wva) * ipsj : 0.0;
     sabs = rowsum8(sabs);
+    mag = rowsum8(mag);
     bool exact;
     {
         const double SS = yyj + contrib, rt = 1.01 * (yyj * __builtin_amdgcn_rsq(yyj) + sabs);
-        exact = __any(valid && !(SS > 0.0 && rt * rt <= kappa_max * SS));
+        const double num = fmax(rt * rt, 1.01 * (yyj + mag));
+        exact = __any(valid && !(SS > 0.0 && num <= kappa_max * SS));
     }
     // ---- psi (dc:150, tau of the previous iteration, Q11) and the outputs
     if (valid) {

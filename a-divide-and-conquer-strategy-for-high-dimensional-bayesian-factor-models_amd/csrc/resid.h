@@ -2,8 +2,9 @@
 // (divideconquer.m:168-172):   Ytil = Yd(:,:,m) - eta(:,:,m)*Lambda(:,:,m)';
 //                              ps(:,:,m) = gamrnd(as + 0.5*n, 1./(bs + 0.5*sum(Ytil.^2)));
 //                              Omega(:,:,m) = diag(1./ps(:,:,m));
-// Used by k_lambda (lambda.h: the tail of a row block whose SS identity is not accurate enough,
-// or every block with DCFM_FLAG_EXACT_RESIDUAL) and by k_resid (resid.hip: the wide path).
+// Used by k_resid (resid.hip: every tile with DCFM_FLAG_EXACT_RESIDUAL) and k_resid_flagged (the
+// K > 32 tiles whose SS identity k_lambda_w's guard rejected).  k_lambda's guard (K <= 32) runs
+// the same arithmetic per wave for its 8 rows (resid_rows8 in lambda.h), not this tile.
 //
 // 256 threads = 4 waves splitting the rows i in 16-row chunks.  Per chunk a wave forms Ytil for
 // 16 rows x 32 columns as fp64 MFMA v_mfma_f64_16x16x4 with the Y tile as the C operand and -eta

@@ -1,6 +1,8 @@
 // Residual-precision update by the reference's own formula for every loading row, as a launch of
-// its own after the loading-row kernel (DCFM_FLAG_EXACT_RESIDUAL).  The default K <= 32 chain runs
-// the same arithmetic per wave inside k_lambda where its guard rejects the SS identity (lambda.h).
+// its own after the loading-row kernel (DCFM_FLAG_EXACT_RESIDUAL), or (K > 32, default mode) for the
+// 32-row tiles whose SS identity k_lambda_w's guard rejected (k_resid_flagged).  The default K <= 32
+// chain runs the same arithmetic per wave inside k_lambda where its guard rejects the identity
+// (lambda.h, resid_rows8).
 //
 // The default chain forms SS_j = sum_i Ytil_ij^2 inside the loading-row kernel by the identity
 // yy_j - 2 lambda_j.C_j + lambda_j E lambda_j' (no Y pass).  That sum cancels when SS_j is
@@ -22,6 +24,29 @@ __global__ __launch_bounds__(256) void k_resid(Dims d, const double *__restrict_
                                                double *__restrict__ omega) {
     __shared__ double red[4][32];
     resid_tile<KW>(d, Y, X, Z, Lam, Gps, ps, omega, blockIdx.y, blockIdx.x * 32, red);
+}
+
+// K > 32 default mode: only the 32-row tiles whose guard k_lambda_w tripped (b.rflag); the flag is
+// read by every thread before resid_tile's barrier and cleared by thread 0 after it
+template <int KW>
+__global__ __launch_bounds__(256) void k_resid_flagged(Dims d, const double *__restrict__ Y, const double *__restrict__ X,
+                                                       const double *__restrict__ Z, const double *__restrict__ Lam,
+                                                       const double *__restrict__ Gps, double *__restrict__ ps,
+                                                       double *__restrict__ omega, int *__restrict__ rflag) {
+    __shared__ double red[4][32];
+    int *f = rflag + blockIdx.y * (d.PP / 32) + blockIdx.x;
+    if (*f == 0) return;
+    resid_tile<KW>(d, Y, X, Z, Lam, Gps, ps, omega, blockIdx.y, blockIdx.x * 32, red);
+    if (threadIdx.x == 0) *f = 0;
+}
+
+void launch_resid_flagged(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
+    const double *Gps = dr.Gps + ((size_t)(iter - dr.first_iter) * d.g + d.shard0) * d.P;
+    const dim3 grid(d.PP / 32, d.G);
+    switch (d.kp) {
+    case 64: hipLaunchKernelGGL(k_resid_flagged<64>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.Lam, Gps, b.ps, b.omega, b.rflag); break;
+    default: hipLaunchKernelGGL(k_resid_flagged<128>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.Lam, Gps, b.ps, b.omega, b.rflag); break;
+    }
 }
 
 void launch_resid(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s, bool gen) {

@@ -4,8 +4,9 @@ c3 = p 19,968 (= 312 x 64), n 1,000, g 64, K 30 (k = 1,920), rho 
 BURNIN 500, MCMC 1,500, thin 5 (300 saved samples).  Same paired design as
 make_c2_parity.py: replicate r fixes the synthetic data set (oracle.synth.make_data,
 DATA_SEED) and the driver's init / partition draws (oracle.DrawSource(CASE_SEED + r)); the
-oracle chain (oracle/vectorised.py, NumPy draws from the same DrawSource) runs BURNIN + MCMC
-iterations and its posterior-mean Sigmaout is compared with the truth in the reference's
+oracle chain (oracle/vectorised.py, NumPy draws from the same DrawSource; ps from dc:169's
+direct residual Yd - eta Lambda', ``direct=True``, the reference's formula as written) runs
+BURNIN + MCMC iterations and its posterior-mean Sigmaout is compared with the truth in the reference's
 output space (Q7, dc:36-39,50-59).
 
 At p = 19,968 a dense copy of the truth or of the difference would be 3.2 GB each, so the
@@ -15,8 +16,8 @@ column block by column block, the Frobenius norm sums the lower triangle twice m
 diagonal, and the operator norm is the largest |eigenvalue| of the symmetric difference by
 ARPACK (scipy eigsh, tol 1e-10) on the triangle.
 
-Run from the repo root, one process per replicate (about 40 minutes each on 2 host threads):
-  for r in 0 1 2; do OMP_NUM_THREADS=2 python3 tests/golden/make_c3_parity.py --rep $r & done; wait
+Run from the repo root, one process per replicate (about 50 minutes each on 2 host threads):
+  for r in 0 1 2 3 4 5; do OMP_NUM_THREADS=2 python3 tests/golden/make_c3_parity.py --rep $r & done; wait
   python3 tests/golden/make_c3_parity.py --merge
 """
 from __future__ import annotations
@@ -40,7 +41,7 @@ from oracle import vectorised as V  # noqa: E402
 
 PARAMS = dict(n=1000, p=19968, g=64, K=30, k0=10, rho=0.5, burnin=500, mcmc=1500, thin=5)
 CASE_SEED = 190
-R = 3
+R = 6
 OUT = ROOT / "tests" / "golden" / "c3_parity.json"
 BLK = 2048
 
@@ -90,9 +91,9 @@ def one_rep(r):
     U, s = truth_lowrank(L0, sig2, Y, c["keep"], c["init"].varind)
     N = P["burnin"] + P["mcmc"]
     T = V.run_chain(c["Yd"], c["st"].copy(), c["rho"], c["hyper"], c["src"].iteration, 1, N,
-                    P["burnin"], P["mcmc"], P["thin"])
+                    P["burnin"], P["mcmc"], P["thin"], direct=True)
     fro, op, tfro, top = lower_errors(T, U, s)
-    rec = dict(rep=r, case_seed=CASE_SEED + r, fro=fro, op=op, fro_rel=fro / tfro, op_rel=op / top,
+    rec = dict(rep=r, case_seed=CASE_SEED + r, direct=True, fro=fro, op=op, fro_rel=fro / tfro, op_rel=op / top,
                truth_fro=tfro, truth_op=top, seconds=round(time.time() - t0, 1))
     (OUT.parent / f"c3_parity_rep{r}.json").write_text(json.dumps(rec) + "\n")
     print(json.dumps(rec), flush=True)
@@ -103,7 +104,7 @@ def merge():
     for r in range(R):
         f = OUT.parent / f"c3_parity_rep{r}.json"
         reps.append(json.loads(f.read_text()))
-    OUT.write_text(json.dumps(dict(params=PARAMS, case_seed0=CASE_SEED, replicates=reps), indent=1) + "\n")
+    OUT.write_text(json.dumps(dict(params=PARAMS, case_seed0=CASE_SEED, direct=True, replicates=reps), indent=1) + "\n")
     for r in range(R):
         (OUT.parent / f"c3_parity_rep{r}.json").unlink()
 
