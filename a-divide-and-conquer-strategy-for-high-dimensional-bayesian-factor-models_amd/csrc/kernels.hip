@@ -197,7 +197,10 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
     prep_shard(d, Lam, omega, A, ZM, blockIdx.x, smem);
 }
 
-constexpr int WP_RING = 4;   // W pass register ring depth (chunks)
+#ifndef DCFM_WP_RING
+#define DCFM_WP_RING 4
+#endif
+constexpr int WP_RING = DCFM_WP_RING;   // W pass register ring depth (chunks)
 // ============================================================================
 // k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA, Y pass 1
 // one wave = (shard m, 16 MT rows i = MT M-tiles) x 32 k (even / odd k tiles) of
@@ -1281,7 +1284,10 @@ extern "C" int dcfm_debug_wstamps(unsigned long long *out, int nblocks) {
 __device__ __forceinline__ void wcol_body(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, int ops, int colsum,
                                           int wpass, unsigned long long ops_epoch, int xchol, const LamGen &lg,
                                           double *smem);
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_wcol(Dims d, Bufs b, DrawsDev dr, int64_t iter, int ops, int colsum,
+#ifndef DCFM_WCOL_WPE
+#define DCFM_WCOL_WPE 3
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DCFM_WCOL_WPE))) void k_wcol(Dims d, Bufs b, DrawsDev dr, int64_t iter, int ops, int colsum,
                                               int wpass, unsigned long long ops_epoch, int xchol, LamGen lg) {
     __shared__ double smem[PREP_SMEM];
 #ifdef DCFM_WSTAMPS
@@ -1703,7 +1709,11 @@ void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
     LamGen lg = {};
     if (lamgen && b.ldraw) lg = lam_gen_plan(d, b.ldraw);
     // W pass tiles: 64-row blocks while 128-row blocks would leave CUs idle
+#ifdef DCFM_WCOL_WMODE
+    const int wmode = DCFM_WCOL_WMODE;   // dev A/B: forced block height
+#else
     const int wmode = (d.NP / 128) * d.G < 256 ? 2 : 1;
+#endif
     const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / (64 * (3 - wmode))) * d.G : 0);
     if (nb + lg.b_total == 0) return;
     hipLaunchKernelGGL(k_wcol, dim3(nb + lg.b_total), dim3(256), 0, s, d, b, dr, iter, ops ? 1 : 0, colsum ? 1 : 0,

@@ -26,6 +26,131 @@ __global__ __launch_bounds__(256) void k_resid(Dims d, const double *__restrict_
     resid_tile<KW>(d, Y, X, Z, Lam, Gps, ps, omega, blockIdx.y, blockIdx.x * 32, red);
 }
 
+// k_resid64 (K <= 32, DCFM_FLAG_EXACT_RESIDUAL): block = (64 loading rows j0 .. j0+63 of shard m) x
+// RW waves; wave w takes the 16-row chunks ch = w, w + RW, ... of i.  Per chunk a wave forms Ytil
+// for 16 rows x 64 columns as four independent fp64 MFMA chains (column tiles h = 0..3, the Y
+// values the accumulator input, -eta the shared A operand: the subtraction of dc:169 inside the
+// accumulation), with the next chunk's Y, X and Z loads in flight behind them; lane (c, q) squares
+// Ytil for rows i0 + q + 4v of columns j0 + 16h + c into its sums.  The 4 lanes of a column, then
+// the RW waves, are summed in a fixed order.  (resid_tile's 32-column tiles ran two chains per
+// wave: 65 us at c3 against this kernel's four.)
+constexpr int RW = 8;
+__global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(2))) void k_resid64(
+    Dims d, const double *__restrict__ Y, const double *__restrict__ X, const double *__restrict__ Z,
+    const double *__restrict__ Lam, const double *__restrict__ Gps, double *__restrict__ ps,
+    double *__restrict__ omega) {
+    __shared__ double red[RW][64];
+    __shared__ __attribute__((aligned(16))) double Ls[64][KP + 2];   // Lambda rows j0 .. j0+63 (B operands)
+    const int m = blockIdx.y, j0 = blockIdx.x * 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 15, q = lane >> 4;
+    for (int e = threadIdx.x; e < 64 * (KP / 2); e += 64 * RW) {
+        const int r = e / (KP / 2), k2 = 2 * (e % (KP / 2)), j = j0 + r;
+        d2 v = {0.0, 0.0};
+        if (j < d.PP) v = *reinterpret_cast<const d2 *>(Lam + ((size_t)m * d.PP + j) * KP + k2);
+        *reinterpret_cast<d2 *>(&Ls[r][k2]) = v;
+    }
+    bool cv[4];
+    int ho[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        cv[h] = j0 + 16 * h + c < d.PP;
+        ho[h] = cv[h] ? 16 * h : 0;
+    }
+    __syncthreads();
+    d2 lb[4][4];   // B operands Lambda[j0 + 16h + c][8t + 2q .. +1], register-resident for the block
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) lb[h][t] = *reinterpret_cast<const d2 *>(&Ls[16 * h + c][8 * t + 2 * q]);
+    // Y of the block as a buffer resource: one 32-bit offset per row, the column tiles as offsets
+    // (64-bit addresses per load cost two VGPRs each and made hipcc spill)
+    const auto ysrc = __builtin_amdgcn_make_buffer_rsrc((void *)(Y + (size_t)m * d.NP * d.PP + j0), (short)0,
+                                                        (int)(((size_t)d.NP * d.PP - j0) * 8), 0x00020000);
+    const double *Zm = Z + (size_t)m * d.NP * KP + 2 * q;
+    const double *Xq = X + 2 * q;
+    double ss[4] = {0.0, 0.0, 0.0, 0.0};
+    // Y of the next chunk is loaded a chunk ahead (two register sets); X and Z of the next chunk as soon
+    // as this chunk's eta is formed (their registers are free then), so both are in flight behind the MFMAs
+    double yA[4][4], yB[4][4];
+    d2 xv[4], zv[4];
+    auto load_y = [&](int ch, double (&y)[4][4]) {
+        const int i0 = 16 * ch;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {   // unconditional loads: an invalid column tile (j >= PP) re-reads tile 0
+            const uint32_t ro = (uint32_t)((i0 + q + 4 * v) * d.PP + c) * 8u;
+#pragma unroll
+            for (int h = 0; h < 4; ++h)
+                y[h][v] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ysrc, ro + 8u * ho[h], 0, 0));
+        }
+    };
+    auto load_xz = [&](int ch) {
+        const int i0 = 16 * ch;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            xv[t] = *reinterpret_cast<const d2 *>(Xq + (size_t)(i0 + c) * KP + 8 * t);
+            zv[t] = *reinterpret_cast<const d2 *>(Zm + (size_t)(i0 + c) * KP + 8 * t);
+        }
+    };
+    const int nch = d.NP / 16;
+    if (w < nch) {
+        load_y(w, yA);
+        load_xz(w);
+    }
+#pragma unroll 1
+    for (int ch = w; ch < nch; ch += RW) {
+        double e[4][2];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            e[t][0] = -eta_of(d.sr, d.s1r, xv[t].x, zv[t].x);
+            e[t][1] = -eta_of(d.sr, d.s1r, xv[t].y, zv[t].y);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const bool more = ch + RW < nch;
+        if (more) {
+            load_xz(ch + RW);
+            load_y(ch + RW, yB);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        d4 acc[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) acc[h] = d4{yA[h][0], yA[h][1], yA[h][2], yA[h][3]};   // invalid tiles: unused sums
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+            for (int h = 0; h < 4; ++h) acc[h] = mfma16x16x4(e[t][0], lb[h][t].x, acc[h]);
+#pragma unroll
+            for (int h = 0; h < 4; ++h) acc[h] = mfma16x16x4(e[t][1], lb[h][t].y, acc[h]);
+        }
+        const int i0 = 16 * ch;
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) ss[h] = (i0 + q + 4 * v < d.n) ? fma(acc[h][v], acc[h][v], ss[h]) : ss[h];
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) yA[h][v] = yB[h][v];
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {   // the column's 4 lane rows: (q0 + q1) + (q2 + q3)
+        ss[h] += __shfl_xor(ss[h], 16, 64);
+        ss[h] += __shfl_xor(ss[h], 32, 64);
+        if (q == 0) red[w][16 * h + c] = ss[h];
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int t = threadIdx.x, j = j0 + t;
+        const double SS = ((red[0][t] + red[1][t]) + (red[2][t] + red[3][t])) +
+                          ((red[4][t] + red[5][t]) + (red[6][t] + red[7][t]));
+        if (j < d.P) {
+            const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps[(size_t)m * d.P + j];   // dc:170
+            ps[(size_t)m * d.PP + j] = psn;
+            omega[(size_t)m * d.PP + j] = 1.0 / psn;                                  // dc:171 (Q1)
+        }
+    }
+}
+static_assert(RW == 8, "k_resid64's wave tree is written for 8 waves");
+
 // K > 32 default mode: only the 32-row tiles whose guard k_lambda_w tripped (b.rflag); the flag is
 // read by every thread before resid_tile's barrier and cleared by thread 0 after it
 template <int KW>
@@ -53,6 +178,11 @@ void launch_resid(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
     const double *Gps;
     if (gen) Gps = lam_gen_plan(d, b.ldraw).Gps;   // the generated fused chain: k_wcol's buffer
     else Gps = dr.Gps + ((size_t)(iter - dr.first_iter) * d.g + d.shard0) * d.P;
+    if (d.kp == KP && (size_t)d.NP * d.PP * 8 < ((size_t)1 << 31)) {   // k_resid64's buffer offsets are 32-bit
+        hipLaunchKernelGGL(k_resid64, dim3((d.PP + 63) / 64, d.G), dim3(64 * RW), 0, s, d, b.Y, b.X, b.Z, b.Lam, Gps,
+                           b.ps, b.omega);
+        return;
+    }
     const dim3 grid(d.PP / 32, d.G);
     switch (d.kp) {
     case 32: hipLaunchKernelGGL(k_resid<32>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.Lam, Gps, b.ps, b.omega); break;

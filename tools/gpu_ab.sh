@@ -3,9 +3,12 @@
 # bench command interleaved R times, then one rocprofv3 kernel trace per variant.
 # Usage: bash tools/gpu_ab.sh TAG R V1 V2 ...      (restores the in-tree build at the end)
 TAG=$1; R=$2; shift 2
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+cd "$ROOT"
 PKG=a-divide-and-conquer-strategy-for-high-dimensional-bayesian-factor-models_amd
 mkdir -p gpurun_out; export TMPDIR=/tmp
 cp $PKG/libdcfm.so /tmp/libdcfm_intree.so
+trap 'cp /tmp/libdcfm_intree.so "$ROOT/$PKG/libdcfm.so"' EXIT   # the product build comes back on any exit
 BENCH="bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --converged-mcmc 0 $BENCH_EXTRA"
 for r in $(seq 1 $R); do
   for V in "$@"; do
@@ -16,7 +19,7 @@ for r in $(seq 1 $R); do
 done
 for V in "$@"; do
   cp build/ab/libdcfm_$V.so $PKG/libdcfm.so
-  (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/abprof_${TAG}_$V -o run -- python3 $GRAFT_REPO_ROOT/$BENCH > $GRAFT_REPO_ROOT/gpurun_out/abprof_${TAG}_$V.log 2>&1) || { echo "trace $V failed"; cp /tmp/libdcfm_intree.so $PKG/libdcfm.so; exit 1; }
+  (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/abprof_${TAG}_$V -o run -- python3 $ROOT/$BENCH > $ROOT/gpurun_out/abprof_${TAG}_$V.log 2>&1) || { echo "trace $V failed"; cp /tmp/libdcfm_intree.so $PKG/libdcfm.so; exit 1; }
   python3 tools/kavg.py gpurun_out/abprof_${TAG}_$V
   find gpurun_out -path "*abprof_${TAG}_$V*" -name "*.csv" -size +512k -exec gzip -9 {} \;
 done
