@@ -329,9 +329,75 @@ constexpr int ZROWS = 128, ZTHREADS = 512;     // rows and threads per k_zdraw b
 // +1] as one 16-byte pair); every element keeps its products and their order, so the values
 // are those of the unpermuted product.  Shared by k_zdraw (W from HBM) and k_wcol's
 // fused W pass (W' still in the W-pass accumulators), which therefore give the same bits.
+#ifndef DCFM_ZD_SPLIT
+#define DCFM_ZD_SPLIT 0
+#endif
 __device__ __forceinline__ void zdraw_rows(const Dims &d, const double (*Ms)[KP][KP + 1], const d2 (&wv)[4],
                                            const d2 (&xv)[4], const d2 (&ev)[4], double *__restrict__ Zr,
                                            double *__restrict__ Sr, bool live, int c, int q) {
+#if DCFM_ZD_SPLIT
+    // each product's k-steps split over two accumulators (even / odd t): 12 + 4 independent MFMA
+    // chains of half the length (the epilogue runs with no other wave's MFMAs to hide behind)
+    d4 zw[2][2], zx[2][2], ze[2][2], as[2][2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) zw[mt][h] = zx[mt][h] = ze[mt][h] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        double mo[2][3][2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int mat = 0; mat < 3; ++mat)
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) mo[e][mat][mt] = Ms[mat][16 * mt + c][8 * t + 2 * q + e];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const double we = e ? wv[t].y : wv[t].x, xe = e ? xv[t].y : xv[t].x;
+            const double ee = e ? ev[t].y : ev[t].x;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                zw[mt][t & 1] = mfma16x16x4(mo[e][0][mt], we, zw[mt][t & 1]);
+                zx[mt][t & 1] = mfma16x16x4(mo[e][1][mt], xe, zx[mt][t & 1]);
+                ze[mt][t & 1] = mfma16x16x4(mo[e][2][mt], ee, ze[mt][t & 1]);
+            }
+        }
+    }
+    d4 az[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+        az[mt] = ((zw[mt][0] + zw[mt][1]) + (zx[mt][0] + zx[mt][1])) + (ze[mt][0] + ze[mt][1]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) as[mt][0][g] = mt ? wv[g].y : wv[g].x;     // W[i][8g + 2q + mt]
+        as[mt][1] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+    const int prow = 8 * (c >> 2) + 2 * (c & 3);
+#pragma unroll
+    for (int mt2 = 0; mt2 < 2; ++mt2)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int kk = 16 * mt2 + 4 * g + q;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) as[mt][g & 1] = mfma16x16x4(Ms[3][prow + mt][kk], az[mt2][g], as[mt][g & 1]);
+        }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) as[mt][0] = as[mt][0] + as[mt][1];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int k = 16 * mt + q + 4 * g;
+            if (live) Zr[k] = (k < d.K) ? az[mt][g] : 0.0;
+        }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        d2 v;
+        v.x = live ? as[0][0][g] : 0.0;
+        v.y = live ? as[1][0][g] : 0.0;
+        *reinterpret_cast<d2 *>(Sr + 8 * g + 2 * q) = v;
+    }
+#else
     d4 zw[2], zx[2], ze[2], as[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) zw[mt] = zx[mt] = ze[mt] = d4{0.0, 0.0, 0.0, 0.0};
@@ -387,6 +453,7 @@ __device__ __forceinline__ void zdraw_rows(const Dims &d, const double (*Ms)[KP]
         v.y = live ? as[1][g] : 0.0;
         *reinterpret_cast<d2 *>(Sr + 8 * g + 2 * q) = v;
     }
+#endif
 }
 // eps[i][kk], kk = 8t + 2q + e of the Z draw (dc:104 normrnd): the injected draw buffer, or
 // generated here — Philox pair 4t + q of (SITE_Z, shard, row i) = normals kk, kk + 1
@@ -406,7 +473,9 @@ __device__ __forceinline__ void z_eps(const Dims &d, const DrawsDev &dr, int64_t
         for (int t = 0; t < 4; ++t) {
             const int kk = 8 * t + 2 * q;
             double n0 = 0.0, n1 = 0.0;
+#ifndef DCFM_DEV_NO_ZNORM   // timing-only dev build: zero normals
             if (live && kk < d.K) rng.normal2(SITE_Z, (uint32_t)mg, (uint32_t)i, (uint32_t)(4 * t + q), (uint32_t)iter, n0, n1);
+#endif
             ev[t].x = n0;
             ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
         }
@@ -1410,6 +1479,9 @@ __device__ __forceinline__ void wcol_body(const Dims &d, const Bufs &b, const Dr
         blk -= nw;
     }
     // the loading-row variates of this iteration (generated chain), behind every other role
+#ifdef DCFM_DEV_NO_LAMGEN   // timing-only dev build: the variates of iterations > 3 are not drawn (stale, finite)
+    if (iter > 3) return;
+#endif
     if (blk < lg.b_total) lam_draws(d, lg, iter, blk * LAM_GEN_THREADS + (int)threadIdx.x, lg.b_total * LAM_GEN_THREADS);
 }
 

@@ -34,7 +34,10 @@ __global__ __launch_bounds__(256) void k_resid(Dims d, const double *__restrict_
 // Ytil for rows i0 + q + 4v of columns j0 + 16h + c into its sums.  The 4 lanes of a column, then
 // the RW waves, are summed in a fixed order.  (resid_tile's 32-column tiles ran two chains per
 // wave: 65 us at c3 against this kernel's four.)
-constexpr int RW = 8;
+#ifndef DCFM_RESID_RW
+#define DCFM_RESID_RW 8
+#endif
+constexpr int RW = DCFM_RESID_RW;
 __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(2))) void k_resid64(
     Dims d, const double *__restrict__ Y, const double *__restrict__ X, const double *__restrict__ Z,
     const double *__restrict__ Lam, const double *__restrict__ Gps, double *__restrict__ ps,
@@ -140,8 +143,8 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(2))) vo
     __syncthreads();
     if (threadIdx.x < 64) {
         const int t = threadIdx.x, j = j0 + t;
-        const double SS = ((red[0][t] + red[1][t]) + (red[2][t] + red[3][t])) +
-                          ((red[4][t] + red[5][t]) + (red[6][t] + red[7][t]));
+        double SS = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+        if constexpr (RW == 8) SS += (red[4][t] + red[5][t]) + (red[6][t] + red[7][t]);
         if (j < d.P) {
             const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps[(size_t)m * d.P + j];   // dc:170
             ps[(size_t)m * d.PP + j] = psn;
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(2))) vo
         }
     }
 }
-static_assert(RW == 8, "k_resid64's wave tree is written for 8 waves");
+static_assert(RW == 4 || RW == 8, "k_resid64's wave tree is written for 4 or 8 waves");
 
 // K > 32 default mode: only the 32-row tiles whose guard k_lambda_w tripped (b.rflag); the flag is
 // read by every thread before resid_tile's barrier and cleared by thread 0 after it

@@ -22,8 +22,10 @@ against an oracle chain stepped from the same state); tests/test_gpu_parity.py k
 the stationary case.
 
 The wide path (K > 32) has the same guard on its SS identity (k_lambda_w + k_resid_flagged): a
-c4-shape chain of generated draws runs >= 1,000 iterations through excursions without a
-non-finite value (DCFM_ERR_NUMERIC would surface from dcfm_run)."""
+c4-shape chain of generated draws runs 1,200 iterations through its excursion without a non-finite
+value (DCFM_ERR_NUMERIC would surface from dcfm_run).  Excursions that escalate end where the
+reference's own algebra ends -- chol of a loading system that is no longer positive definite
+(test_breakdown_is_the_references)."""
 import numpy as np
 import pytest
 
@@ -32,6 +34,7 @@ from helpers import STATE_CMP, make_case, stacked_draws, stagewise_errors, state
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-10
+DCFM_ERR_NUMERIC = 5        # include/dcfm.h
 BW_TOL = 1e-13
 
 
@@ -103,9 +106,12 @@ def test_fused_run_in_x_excursion_regime(dcfm, record_property):
     print("EXCURSION", {"warmup_xmax": xmax0, "chain_xmax": xmax, **{k: f"{v:.2e}" for k, v in worst.items()}})
 
 
-# c4 shape (p 10,000, n 2,000, g 8, K 100), generated draws.  The Philox seed is one whose chain makes
-# X excursions (tools/dev/excursion_probe.py); every dcfm_run raises on a non-finite state.
-C4_SEED = 5
+# c4 shape (p 10,000, n 2,000, g 8, K 100), generated draws.  At this shape about a third of the Philox
+# seeds (tools/dev/excursion_probe.py, seeds 1-40, 1,200 iterations) start an X excursion that escalates
+# within ~50-100 iterations to the reference's own breakdown (below); the surviving chains wander at
+# most to max|X| ~ 8 (typical ~3).  Seed 37 is the surviving chain with the largest and longest
+# excursion (max|X| 5-8 for 1,000 iterations): the guarded wide path runs it without a non-finite value.
+C4_SEED = 37
 C4_ITERS = 1200
 
 
@@ -119,7 +125,7 @@ def test_c4_generated_chain_through_excursions(dcfm, record_property):
         smp.set_state({f: v for f, v in state_dict(c["st"]).items() if f != "eta"})
         step = 100
         for it in range(1, C4_ITERS + 1, step):
-            smp.run(it, step)              # raises DCFM_ERR_NUMERIC on a NaN / Inf in the state
+            smp.run(it, step)              # DCFM_ERR_NUMERIC on a NaN / Inf in the state
             st = smp.get_state(("X", "ps"))
             assert np.all(np.isfinite(st["X"])) and np.all(st["ps"] > 0)
             xmax.append(float(np.abs(st["X"]).max()))
@@ -127,4 +133,99 @@ def test_c4_generated_chain_through_excursions(dcfm, record_property):
     finally:
         smp.close()
     record_property("xmax_per_100", xmax)
+    assert max(xmax) > 5.0, "seed no longer makes an excursion: pick another (tools/dev/excursion_probe.py)"
     print("C4_CHAIN", {"seed": C4_SEED, "xmax": [f"{v:.3g}" for v in xmax], "psmin": f"{min(psmin):.3g}"})
+
+
+def _first_breakdown(dcfm, c, g, K, seed, iters=800, chunk=20):
+    """(last finite state, first non-finite iteration) of the generated chain, or None."""
+    st = {f: v for f, v in state_dict(c["st"]).items() if f != "eta"}
+
+    def chain(state, first, count, step):
+        smp = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], 10 ** 6, 0, 1, seed=seed)
+        good, it = state, first
+        try:
+            smp.set_data(c["Yd"])
+            smp.set_state(state)
+            while it < first + count:
+                try:
+                    smp.run(it, step)
+                    s = smp.get_state()
+                except dcfm.DcfmError as e:
+                    assert e.code == DCFM_ERR_NUMERIC, e
+                    return good, it
+                good = {f: v for f, v in s.items() if f != "eta"}
+                it += step
+        finally:
+            smp.close()
+        return good, None
+
+    good, it = chain(st, 1, iters, chunk)
+    if it is None:
+        return None
+    good, it = chain(good, it, chunk, 1)
+    return good, it
+
+
+def test_breakdown_is_the_references(dcfm, record_property):
+    """Where an excursion escalates (c2 shape: Philox seeds 4, 11, 22 of 40; max|X| 1e7-1e8, cond(E_m)
+    ~1e18), the chain ends in DCFM_ERR_NUMERIC.  That is the reference's own end: from the GPU chain's
+    last finite state, with the failing iteration's variates (dcfm_rng_fill at the sweep's counters), the
+    faithful per-row oracle (MATLAB semantics: chol(Qlam,'lower') of dc:142 raises on a matrix that is not
+    positive definite) fails at the same iteration, and the library fed the same state and variates
+    (injected) fails there too.  The guard of the SS identity is not involved: the exact-residual mode
+    breaks down at the same point (tools/dev/nan_hunt.py)."""
+    from numpy.linalg import LinAlgError
+
+    from oracle import IterDraws
+    from oracle import dc_oracle as F
+    from test_gpu_generated_draws import _draws
+
+    c = make_case(500, 5000, 8, 20, seed=29, k0=10, dense_truth=False)
+    g, K = 8, 20
+    found = None
+    for seed in (11, 4, 22):
+        found = _first_breakdown(dcfm, c, g, K, seed)
+        if found is not None:
+            break
+    assert found is not None, "no probed seed breaks down any more: re-probe (tools/dev/excursion_probe.py)"
+    good, it = found
+    dr = _draws(dcfm, seed, c["n"], c["P"], g, K, it, 1, dcfm.Hyper())
+    # the library, injected: the same failure
+    smp = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], 10 ** 6, 0, 1, seed=seed, inject_draws=True)
+    try:
+        smp.set_data(c["Yd"])
+        smp.set_state(good)
+        smp.set_draws(dr, it, 1)
+        with pytest.raises(dcfm.DcfmError) as ei:
+            smp.run(it, 1)
+            smp.get_state(("X",))
+        assert ei.value.code == DCFM_ERR_NUMERIC
+    finally:
+        smp.close()
+    # the reference's algebra from the same state and variates
+    st = _as_oracle({**good, "eta": np.zeros((c["n"], K, g))})
+    F.update_eta(st, c["rho"])
+    d = IterDraws(**{k: np.asarray(v)[..., 0] for k, v in dr.items()})
+    failed = None
+    with np.errstate(all="ignore"):
+        for name, fn in (("Z", lambda: F.update_Z(st, c["Yd"], c["rho"], d)),
+                         ("X", lambda: F.update_X(st, c["Yd"], c["rho"], d)),
+                         ("eta", lambda: F.update_eta(st, c["rho"])),
+                         ("Lambda", lambda: F.update_Lambda(st, c["Yd"], d)),
+                         ("psi", lambda: F.update_psi(st, c["hyper"], d)),
+                         ("delta", lambda: F.update_delta_tau(st, c["hyper"], d)),
+                         ("ps", lambda: F.update_ps(st, c["Yd"], c["hyper"], d))):
+            try:
+                fn()
+            except LinAlgError:
+                failed = name
+                break
+            if not all(np.all(np.isfinite(v)) for v in st.as_dict().values()):
+                failed = name
+                break
+    record_property("breakdown", {"seed": seed, "iteration": it, "oracle_stage": failed,
+                                  "xmax_before": float(np.abs(good["X"]).max())})
+    print("BREAKDOWN", {"seed": seed, "iteration": it, "oracle_stage": failed,
+                        "xmax_before": float(np.abs(good["X"]).max())})
+    assert failed is not None, f"the oracle completes iteration {it} where the library fails"

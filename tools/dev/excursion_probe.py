@@ -43,11 +43,11 @@ def main():
             for it in range(1, a.iters + 1, a.step):
                 try:
                     smp.run(it, a.step)
+                    st = smp.get_state(("X", "ps"))
                 except Exception as e:  # noqa: BLE001
                     print(f"seed {seed}: iteration {it}..{it + a.step - 1}: {e}", flush=True)
                     ok = False
                     break
-                st = smp.get_state(("X", "ps"))
                 xs.append(float(np.abs(st["X"]).max()))
         finally:
             smp.close()
