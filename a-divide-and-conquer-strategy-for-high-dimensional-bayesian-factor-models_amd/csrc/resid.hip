@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void k_resid(Dims d, const double *__restrict_
 // the RW waves, are summed in a fixed order.  (resid_tile's 32-column tiles ran two chains per
 // wave: 65 us at c3 against this kernel's four.)
 #ifndef DCFM_RESID_RW
-#define DCFM_RESID_RW 8
+#define DCFM_RESID_RW 4
 #endif
 constexpr int RW = DCFM_RESID_RW;
 __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(2))) void k_resid64(
