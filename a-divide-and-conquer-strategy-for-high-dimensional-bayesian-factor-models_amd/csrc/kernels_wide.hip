@@ -488,8 +488,8 @@ __global__ __launch_bounds__(64) void k_lambda_w(
                 double pv = 0.0;                          // (R_{J,I}' v_J)[c16]: sum over rows q + 4g
 #pragma unroll
                 for (int g = 0; g < 4; ++g) pv = fma(R[g], vj[g], pv);
-                pv += __shfl_xor(pv, 16, 64);
-                pv += __shfl_xor(pv, 32, 64);
+                pv += xor16_d(pv);
+                pv += xor32_d(pv);
                 if (q == 0) vb[16 * I + c16] -= pv;
             }
         });
@@ -525,8 +525,8 @@ __global__ __launch_bounds__(64) void k_lambda_w(
             if constexpr (J < NB - 1) y -= rowsum16(pg[g]);
             sx = fma(T[utix<NB>(J, J)][g], y, sx);        // (U_JJ' y)[c16]: sum over rows q + 4g
         }
-        sx += __shfl_xor(sx, 16, 64);
-        sx += __shfl_xor(sx, 32, 64);
+        sx += xor16_d(sx);
+        sx += xor32_d(sx);
         xr[J] = sx;
     });
 #pragma unroll
@@ -562,14 +562,21 @@ __global__ __launch_bounds__(64) void k_lambda_w(
         Lam[rowoff + r] = xv;
         cpart[rowoff + r] = psir * (xv * xv);          // mat = psijh .* Lambda.^2 (dc:156)
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        ssr += __shfl_xor(ssr, o, 64);
-        mag += __shfl_xor(mag, o, 64);
-        ww += __shfl_xor(ww, o, 64);
-        sab += __shfl_xor(sab, o, 64);
-        cs = fmax(cs, __shfl_xor(cs, o, 64));
-    }
+    // wave sums: DPP within the 16-lane rows, then the four row totals by readlane in a fixed order
+    // (a butterfly of lane shuffles here cost ~9 us per c4 launch: six LDS-latency rounds per row)
+    auto wsum = [](double v) {
+        v = rowsum16(v);
+        return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+    };
+    ssr = wsum(ssr);
+    mag = wsum(mag);
+    ww = wsum(ww);
+    sab = wsum(sab);
+    cs = fmax(cs, dpp_d<0xB1>(cs));
+    cs = fmax(cs, dpp_d<0x4E>(cs));
+    cs = fmax(cs, dpp_d<0x124>(cs));
+    cs = fmax(cs, dpp_d<0x128>(cs));
+    cs = fmax(fmax(readlane_d(cs, 0), readlane_d(cs, 16)), fmax(readlane_d(cs, 32), readlane_d(cs, 48)));
     if (lane == 0) {
         const double SS = yyj + ssr;
         const double psn = (1.0 / (d.bs + 0.5 * SS)) * Gps;      // dc:170

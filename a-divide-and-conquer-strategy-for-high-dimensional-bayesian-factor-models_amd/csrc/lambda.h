@@ -160,8 +160,8 @@ __device__ __forceinline__ void resid_rows8(const Dims &d, const double *__restr
 #pragma unroll
         for (int v = 0; v < 4; ++v) ss = (i0 + q + 4 * v < d.n) ? fma(acc[v], acc[v], ss) : ss;   // data rows only
     }
-    ss += __shfl_xor(ss, 16, 64);   // (q0 + q1) + (q2 + q3)
-    ss += __shfl_xor(ss, 32, 64);
+    ss += xor16_d(ss);   // (q0 + q1) + (q2 + q3)
+    ss += xor32_d(ss);
     if (q == 0 && col) {
         const double psn = (1.0 / (d.bs + 0.5 * ss)) * Gps_c;   // dc:170
         ps[(uint32_t)(m * d.PP + j0 + c)] = psn;

@@ -406,6 +406,24 @@ __device__ __forceinline__ double dpp_d(double v) {
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
 }
+// v of lane l ^ 16 / l ^ 32 (the partner row of the wave) by gfx950's v_permlane16_swap /
+// v_permlane32_swap: a register exchange between rows, where a lane shuffle (ds_bpermute) costs an LDS
+// round trip.  With both operands v the swap leaves the partner's value in the second result for the
+// lanes whose partner is above them and in the first for the others.
+__device__ __forceinline__ double xor16_d(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const bool up = (__lane_id() & 16) == 0;
+    return __hiloint2double(up ? b[1] : b[0], up ? a[1] : a[0]);
+}
+__device__ __forceinline__ double xor32_d(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const bool up = __lane_id() < 32;
+    return __hiloint2double(up ? b[1] : b[0], up ? a[1] : a[0]);
+}
 __device__ __forceinline__ double rowsum16(double v) {
     v += dpp_d<0xB1>(v);     // quad_perm [1,0,3,2]
     v += dpp_d<0x4E>(v);     // quad_perm [2,3,0,1]

@@ -75,8 +75,8 @@ __device__ __forceinline__ void resid_tile(const Dims &d, const double *__restri
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {   // the column's 4 lane rows: (q0 + q1) + (q2 + q3)
-        ss[h] += __shfl_xor(ss[h], 16, 64);
-        ss[h] += __shfl_xor(ss[h], 32, 64);
+        ss[h] += xor16_d(ss[h]);
+        ss[h] += xor32_d(ss[h]);
     }
     if (q == 0) {
         red[w][c] = ss[0];

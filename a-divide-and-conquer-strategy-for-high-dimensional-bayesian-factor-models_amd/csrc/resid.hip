@@ -136,8 +136,8 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
 #pragma unroll
     for (int h = 0; h < 4; ++h) {   // the column's 4 lane rows: (q0 + q1) + (q2 + q3)
-        ss[h] += __shfl_xor(ss[h], 16, 64);
-        ss[h] += __shfl_xor(ss[h], 32, 64);
+        ss[h] += xor16_d(ss[h]);
+        ss[h] += xor32_d(ss[h]);
         if (q == 0) red[w][16 * h + c] = ss[h];
     }
     __syncthreads();
