@@ -198,9 +198,12 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 }
 
 #ifndef DCFM_WP_RING
-#define DCFM_WP_RING 4
+#define DCFM_WP_RING 3
 #endif
 constexpr int WP_RING = DCFM_WP_RING;   // W pass register ring depth (chunks)
+#ifndef DCFM_WP_SPLIT
+#define DCFM_WP_SPLIT 1
+#endif
 // ============================================================================
 // k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA, Y pass 1
 // one wave = (shard m, 16 MT rows i = MT M-tiles) x 32 k (even / odd k tiles) of
@@ -243,6 +246,15 @@ __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restric
         l0[k] = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q) * KW);
         l1[k] = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q + 1) * KW);
     };
+#if DCFM_WP_SPLIT
+    // the two k-steps of a chunk accumulate into separate sets (8 independent MFMA chains per wave
+    // instead of 4), added at the end: W = (sum over even j) + (sum over odd j)
+    d4 acc2[MT][2];
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc2[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+#endif
     auto mma = [&](int k) {
         const double b00 = ww[k].x * l0[k].x, b01 = ww[k].x * l0[k].y;
         const double b10 = ww[k].y * l1[k].x, b11 = ww[k].y * l1[k].y;
@@ -252,12 +264,21 @@ __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restric
             acc[MT - 1][0] = mfma16x16x4(b00, y1[k].x, acc[MT - 1][0]);
             acc[MT - 1][1] = mfma16x16x4(b01, y1[k].x, acc[MT - 1][1]);
         }
+#if DCFM_WP_SPLIT
+        acc2[0][0] = mfma16x16x4(b10, y0[k].y, acc2[0][0]);
+        acc2[0][1] = mfma16x16x4(b11, y0[k].y, acc2[0][1]);
+        if (MT == 2) {
+            acc2[MT - 1][0] = mfma16x16x4(b10, y1[k].y, acc2[MT - 1][0]);
+            acc2[MT - 1][1] = mfma16x16x4(b11, y1[k].y, acc2[MT - 1][1]);
+        }
+#else
         acc[0][0] = mfma16x16x4(b10, y0[k].y, acc[0][0]);
         acc[0][1] = mfma16x16x4(b11, y0[k].y, acc[0][1]);
         if (MT == 2) {
             acc[MT - 1][0] = mfma16x16x4(b10, y1[k].y, acc[MT - 1][0]);
             acc[MT - 1][1] = mfma16x16x4(b11, y1[k].y, acc[MT - 1][1]);
         }
+#endif
     };
 #pragma unroll
     for (int k = 0; k < R - 1; ++k)
@@ -270,6 +291,12 @@ __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restric
             if (t + k < nch) mma(k);
         }
     }
+#if DCFM_WP_SPLIT
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] += acc2[a][b];
+#endif
 }
 
 template <int KW, int MT = 2>

@@ -9,7 +9,9 @@ initial state with independent on-device Philox draws.  d_r = err_gpu,r - err_or
 independent across r with mean 0 under parity, and mean(d) / (sd(d) / sqrt(R)) is Student-t with
 R - 1 degrees of freedom.  The test passes when
     |mean d| < t_{R-1, 0.995} sd(d) / sqrt(R)     (two-sided 99 %: fails 1 time in 100 under parity)
-and |mean d| < 1 % of the error (a fixed cap, so a noisy replicate set cannot widen the bar).
+and |mean d| < CAP of the error (a fixed cap, so a noisy replicate set cannot widen the bar: 1 % for the
+Frobenius error; 5 % for the operator norm, whose Monte Carlo spread is ~8x larger -- at c3 the oracle's
+own replicates span 0.535-0.550).
 Every replicate's GPU and oracle errors, the bars and the t statistics are written to
 gpurun_out/<name>_parity_gpu.json (committed under profiles/ with the round's evidence)."""
 from __future__ import annotations
@@ -24,7 +26,7 @@ from scipy import stats
 import oracle
 from helpers import make_case, state_dict
 
-CAP = 0.01
+CAP = {"fro_rel": 0.01, "op_rel": 0.05}
 ALPHA = 0.01
 
 
@@ -62,10 +64,10 @@ def run_paired(dcfm, fixture: Path, name: str, seed0: int, dense_truth: bool, re
         se = float(np.std(d, ddof=1)) / np.sqrt(R)
         bar = tcrit * se
         summary[key] = {"mean_diff": float(np.mean(d)), "se": se, "t": float(np.mean(d)) / se if se > 0 else 0.0,
-                        "bar": bar, "bar_rel": bar / base, "cap": CAP * base, "mean_oracle": base,
+                        "bar": bar, "bar_rel": bar / base, "cap": CAP[key] * base, "mean_oracle": base,
                         "oracle_sd": float(np.std([r[f"oracle_{key}"] for r in rows], ddof=1)),
                         "gpu_sd": float(np.std([r[f"gpu_{key}"] for r in rows], ddof=1))}
-        verdicts[key] = abs(float(np.mean(d))) < min(bar, CAP * base)
+        verdicts[key] = abs(float(np.mean(d))) < min(bar, CAP[key] * base)
     out = Path(os.environ.get("DCFM_PARITY_OUT", "gpurun_out"))
     out.mkdir(parents=True, exist_ok=True)
     (out / f"{name}_parity_gpu.json").write_text(json.dumps(summary, indent=1) + "\n")
