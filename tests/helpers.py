@@ -109,3 +109,31 @@ def elem_rel_err(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64).reshape(a.shape)
     return float(np.max(np.abs(a - b) / np.abs(b))) if b.size else 0.0
+
+
+def residual_rounding_bound(got, Yd):
+    """Per-row bound on the rounding error of dc:169's residual evaluation at the state `got` (MATLAB
+    layout), relative to ps_j: Ytil_ij = Yd_ij - sum_k eta_ik Lambda_jk carries |delta_ij| <= (K + 1) eps
+    M_ij, M_ij = |Yd_ij| + sum_k |eta_ik Lambda_jk|, so SS_j = sum_i Ytil_ij^2 carries <= 2 (K + 1) eps
+    sum_i |Ytil_ij| M_ij, and ps_j = Gps / (bs + SS_j / 2) at most the same relative error.  Two correct
+    evaluations (any summation order) differ by at most twice that.  Returns g x P (the ps layout's
+    shards x rows); ~1e-14 at a stationary state, far larger inside the reference's X excursions, where
+    eta Lambda' cancels against Yd."""
+    from oracle import vectorised as V
+    D = V._as_data(Yd)
+    eta = np.moveaxis(np.asarray(got["eta"], dtype=np.float64), 2, 0)          # g x n x K
+    lam = np.moveaxis(np.asarray(got["Lambda"], dtype=np.float64), 2, 0)       # g x P x K
+    K = lam.shape[-1]
+    R = D.Ys - eta @ np.swapaxes(lam, 1, 2)
+    M = np.abs(D.Ys) + np.abs(eta) @ np.swapaxes(np.abs(lam), 1, 2)
+    SS = np.einsum("mij,mij->mj", R, R)
+    return 4.0 * (K + 1) * np.finfo(np.float64).eps * np.einsum("mij,mij->mj", np.abs(R), M) / SS
+
+
+def scaled_rel_err(a, b, bound, tol):
+    """max_i |a_i - b_i| / |b_i| / max(tol, bound_i) * tol: the per-element relative error, each measured
+    against the larger of tol and that element's own rounding bound (< tol passes)."""
+    a = np.asarray(a, dtype=np.float64).reshape(-1)
+    b = np.asarray(b, dtype=np.float64).reshape(-1)
+    bd = np.maximum(tol, np.asarray(bound, dtype=np.float64).reshape(-1))
+    return float(np.max(np.abs(a - b) / np.abs(b) / bd) * tol) if b.size else 0.0
