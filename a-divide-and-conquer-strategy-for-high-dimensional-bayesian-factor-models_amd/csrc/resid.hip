@@ -37,8 +37,14 @@ __global__ __launch_bounds__(256) void k_resid(Dims d, const double *__restrict_
 #ifndef DCFM_RESID_RW
 #define DCFM_RESID_RW 4
 #endif
+#ifndef DCFM_RESID_LDSB
+#define DCFM_RESID_LDSB 0
+#endif
+#ifndef DCFM_RESID_WPE
+#define DCFM_RESID_WPE 2
+#endif
 constexpr int RW = DCFM_RESID_RW;
-__global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(2))) void k_resid64(
+__global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(DCFM_RESID_WPE))) void k_resid64(
     Dims d, const double *__restrict__ Y, const double *__restrict__ X, const double *__restrict__ Z,
     const double *__restrict__ Lam, const double *__restrict__ Gps, double *__restrict__ ps,
     double *__restrict__ omega) {
@@ -52,19 +58,20 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(2))) vo
         if (j < d.PP) v = *reinterpret_cast<const d2 *>(Lam + ((size_t)m * d.PP + j) * KP + k2);
         *reinterpret_cast<d2 *>(&Ls[r][k2]) = v;
     }
-    bool cv[4];
-    int ho[4];
+    // column tile h holds columns jc(h) = 32 (h >> 1) + 2c + (h & 1) of the group: a lane's columns of tiles
+    // 2hp and 2hp + 1 are adjacent, one 16-byte Y load; PP is a multiple of 32, so a pair is valid whole
+    auto jc = [&](int h) { return 32 * (h >> 1) + 2 * c + (h & 1); };
+    int ho[2];
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        cv[h] = j0 + 16 * h + c < d.PP;
-        ho[h] = cv[h] ? 16 * h : 0;
-    }
+    for (int hp = 0; hp < 2; ++hp) ho[hp] = (j0 + 32 * hp < d.PP) ? 32 * hp : 0;   // invalid: re-read pair 0
     __syncthreads();
+#if !DCFM_RESID_LDSB
     d2 lb[4][4];   // B operands Lambda[j0 + 16h + c][8t + 2q .. +1], register-resident for the block
 #pragma unroll
     for (int h = 0; h < 4; ++h)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) lb[h][t] = *reinterpret_cast<const d2 *>(&Ls[16 * h + c][8 * t + 2 * q]);
+        for (int t = 0; t < 4; ++t) lb[h][t] = *reinterpret_cast<const d2 *>(&Ls[jc(h)][8 * t + 2 * q]);
+#endif
     // Y of the block as a buffer resource: one 32-bit offset per row, the column tiles as offsets
     // (64-bit addresses per load cost two VGPRs each and made hipcc spill)
     const auto ysrc = __builtin_amdgcn_make_buffer_rsrc((void *)(Y + (size_t)m * d.NP * d.PP + j0), (short)0,
@@ -79,11 +86,14 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(2))) vo
     auto load_y = [&](int ch, double (&y)[4][4]) {
         const int i0 = 16 * ch;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {   // unconditional loads: an invalid column tile (j >= PP) re-reads tile 0
-            const uint32_t ro = (uint32_t)((i0 + q + 4 * v) * d.PP + c) * 8u;
+        for (int v = 0; v < 4; ++v) {   // unconditional loads: an invalid column pair (j >= PP) re-reads pair 0
+            const uint32_t ro = (uint32_t)((i0 + q + 4 * v) * d.PP + 2 * c) * 8u;
 #pragma unroll
-            for (int h = 0; h < 4; ++h)
-                y[h][v] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(ysrc, ro + 8u * ho[h], 0, 0));
+            for (int hp = 0; hp < 2; ++hp) {
+                const d2 yv = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(ysrc, ro + 8u * ho[hp], 0, 0));
+                y[2 * hp][v] = yv.x;
+                y[2 * hp + 1][v] = yv.y;
+            }
         }
     };
     auto load_xz = [&](int ch) {
@@ -119,10 +129,20 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(2))) vo
         for (int h = 0; h < 4; ++h) acc[h] = d4{yA[h][0], yA[h][1], yA[h][2], yA[h][3]};   // invalid tiles: unused sums
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
+#if DCFM_RESID_LDSB   // B operands read from the LDS image per k-step (64 fewer VGPRs: 3 waves per SIMD)
+            d2 lt[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) lt[h] = *reinterpret_cast<const d2 *>(&Ls[jc(h)][8 * t + 2 * q]);
+#pragma unroll
+            for (int h = 0; h < 4; ++h) acc[h] = mfma16x16x4(e[t][0], lt[h].x, acc[h]);
+#pragma unroll
+            for (int h = 0; h < 4; ++h) acc[h] = mfma16x16x4(e[t][1], lt[h].y, acc[h]);
+#else
 #pragma unroll
             for (int h = 0; h < 4; ++h) acc[h] = mfma16x16x4(e[t][0], lb[h][t].x, acc[h]);
 #pragma unroll
             for (int h = 0; h < 4; ++h) acc[h] = mfma16x16x4(e[t][1], lb[h][t].y, acc[h]);
+#endif
         }
         const int i0 = 16 * ch;
 #pragma unroll
@@ -138,7 +158,7 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(2))) vo
     for (int h = 0; h < 4; ++h) {   // the column's 4 lane rows: (q0 + q1) + (q2 + q3)
         ss[h] += xor16_d(ss[h]);
         ss[h] += xor32_d(ss[h]);
-        if (q == 0) red[w][16 * h + c] = ss[h];
+        if (q == 0) red[w][jc(h)] = ss[h];
     }
     __syncthreads();
     if (threadIdx.x < 64) {
