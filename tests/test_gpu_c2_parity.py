@@ -4,9 +4,9 @@ operator-norm error against the synthetic truth, within Monte Carlo error (dc:18
 
 Oracle leg: tests/golden/make_c2_parity.py -> tests/golden/c2_parity.json, 8 replicates of the
 vectorised oracle chain with dc:169's direct residual (exact eigvalsh operator norm).  GPU leg: the
-same data and initial state, independent Philox draws, errors from dcfm_sigma_error.  Bar:
-tests/stat_parity.py (paired t test at 99 %, capped at 1 % of the error); the per-replicate numbers
-go to gpurun_out/c2_parity_gpu.json."""
+same data and initial state, 16 chains per case with independent Philox draws, errors from
+dcfm_sigma_error.  Bar: tests/stat_parity.py (the oracle chains' errors against the GPU chains'
+distribution per case, two-sided 1 %); every chain's numbers go to gpurun_out/c2_parity_gpu.json."""
 from pathlib import Path
 
 import pytest

@@ -5,9 +5,10 @@ operator-norm error against the synthetic truth, within Monte Carlo error (dc:18
 Oracle leg: tests/golden/make_c3_parity.py -> tests/golden/c3_parity.json, 6 replicates of the
 vectorised oracle chain with dc:169's direct residual (~50 min each on 2 host threads; Frobenius
 norm from the lower triangle, operator norm by ARPACK).  GPU leg: the same data and initial state,
-independent Philox draws, errors from dcfm_sigma_error (Sigmaout never leaves the device; operator
-norm by 120 Lanczos steps).  Bar: tests/stat_parity.py (paired t test at 99 %, capped at 1 % of the
-error); the per-replicate numbers go to gpurun_out/c3_parity_gpu.json."""
+16 chains per case with independent Philox draws, errors from dcfm_sigma_error (Sigmaout never leaves
+the device; operator norm by 120 Lanczos steps).  Bar: tests/stat_parity.py (the oracle chains' errors
+against the GPU chains' distribution per case, two-sided 1 %); every chain's numbers go to
+gpurun_out/c3_parity_gpu.json."""
 from pathlib import Path
 
 import pytest
