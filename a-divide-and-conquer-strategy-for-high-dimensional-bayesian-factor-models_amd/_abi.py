@@ -26,6 +26,7 @@ DCFM_FLAG_ONE_STREAM = 0x4     # every launch on one stream
 DCFM_FLAG_FLAT_PRIORITY = 0x8  # default priority for every stream
 DCFM_FLAG_COMM_SELF = 0x20   # one rank on the collective path with a real 1-rank RCCL communicator
 DCFM_FLAG_EXACT_RESIDUAL = 0x10  # ps / omega from the direct residual (dc:169), one more Y pass
+DCFM_FLAG_GUARD_ALL = 0x40       # the SS-identity guard rejects every row (its residual fallback, tests)
 
 KERNEL_IDS = {
     "k_prep": 0, "k_wpass": 1, "k_zdraw": 2, "k_xred": 3, "k_xdraw": 4, "k_cpass": 5,

@@ -1217,8 +1217,9 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             KTimer t(h, DCFM_K_LAMBDA, s);
             // exact residual: k_resid redoes every row below (the guard need not fire)
             const bool exact = h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL;
+            const double kmax = (h->cfg.flags & DCFM_FLAG_GUARD_ALL) ? 0.0 : KAPPA_IDENTITY_MAX;
             launch_lambda(d, b, dr, it, b.tau + h->cur * nkg, h->plam_valid ? b.Plam : nullptr, s, lamgen,
-                          exact ? HUGE_VAL : KAPPA_IDENTITY_MAX);
+                          exact ? HUGE_VAL : kmax);
         }
         if (h->cfg.flags & DCFM_FLAG_EXACT_RESIDUAL) {   // dc:169's residual for every loading row
             KTimer t(h, DCFM_K_RESID, s);

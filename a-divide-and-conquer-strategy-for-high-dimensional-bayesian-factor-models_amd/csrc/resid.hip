@@ -13,6 +13,8 @@
 // direct residual (resid.h): a pass over the tile's Y columns, the reference's own third product.
 //
 // k_resid<KW>: block = (32-column tile of shard m's loading rows, shard m), resid_tile's 4 waves.
+#include <algorithm>
+
 #include "resid.h"
 
 namespace dcfm {
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(DCFM_RE
 }
 static_assert(RW == 4 || RW == 8, "k_resid64's wave tree is written for 4 or 8 waves");
 
-// K > 32 default mode: only the 32-row tiles whose guard k_lambda_w tripped (b.rflag); the flag is
+// K > 32 default mode: only the 32-row tiles whose guard k_lambda_w tripped (b.rflag); a flag is
 // read by every thread before resid_tile's barrier and cleared by thread 0 after it
 template <int KW>
 __global__ __launch_bounds__(256) void k_resid_flagged(Dims d, const double *__restrict__ Y, const double *__restrict__ X,
@@ -182,15 +184,21 @@ __global__ __launch_bounds__(256) void k_resid_flagged(Dims d, const double *__r
                                                        const double *__restrict__ Gps, double *__restrict__ ps,
                                                        double *__restrict__ omega, int *__restrict__ rflag) {
     __shared__ double red[4][32];
-    int *f = rflag + blockIdx.y * (d.PP / 32) + blockIdx.x;
-    if (*f == 0) return;
-    resid_tile<KW>(d, Y, X, Z, Lam, Gps, ps, omega, blockIdx.y, blockIdx.x * 32, red);
-    if (threadIdx.x == 0) *f = 0;
+    const int nt = d.PP / 32;
+    for (int t = blockIdx.x; t < nt; t += gridDim.x) {   // a few blocks per shard walk its tiles
+        int *f = rflag + blockIdx.y * nt + t;
+        if (*f == 0) continue;                            // block-uniform
+        resid_tile<KW>(d, Y, X, Z, Lam, Gps, ps, omega, blockIdx.y, t * 32, red);
+        if (threadIdx.x == 0) *f = 0;
+        __syncthreads();                                  // red is reused by the next flagged tile
+    }
 }
 
 void launch_resid_flagged(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
     const double *Gps = dr.Gps + ((size_t)(iter - dr.first_iter) * d.g + d.shard0) * d.P;
-    const dim3 grid(d.PP / 32, d.G);
+    // tiles are flagged rarely (the reference's transients and excursions): 16 blocks per shard walk them
+    // (one block per tile cost ~6 us of dispatch per iteration at c4 with every block exiting at once)
+    const dim3 grid(std::min(d.PP / 32, 16), d.G);
     switch (d.kp) {
     case 64: hipLaunchKernelGGL(k_resid_flagged<64>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.Lam, Gps, b.ps, b.omega, b.rflag); break;
     default: hipLaunchKernelGGL(k_resid_flagged<128>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.Lam, Gps, b.ps, b.omega, b.rflag); break;

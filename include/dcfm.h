@@ -61,6 +61,10 @@ extern "C" {
                                         sum((Yd - eta*Lambda').^2), one extra pass over Y
                                         (k_resid), instead of the SS identity inside the
                                         loading-row kernel (parity runs)   */
+#define DCFM_FLAG_GUARD_ALL    0x40u  /* the SS-identity guard rejects every row: the default
+                                        path's own residual fallback (K <= 32: resid_rows8 in
+                                        the loading-row kernel; K > 32: every tile through
+                                        k_resid_flagged) for every row (tests)            */
 
 typedef struct dcfm_handle dcfm_handle;
 

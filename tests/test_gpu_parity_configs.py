@@ -39,8 +39,11 @@ applied to the GPU's own eta and Lambda; the oracle chain takes the residual too
            (resid_rows8, same launch).  At c2's second
            iteration the identity alone is 1.3e-10 off (kappa_j ~ 1e6: its error grows like
            kappa_j eps, the residual's like sqrt(kappa_j) eps); the guard sends those rows to the
-           residual.  The wide path (c4, K = 100) has no guard: the identity there, checked at
-           the same bar.
+           residual; the wide path (c4, K = 100) has the same guard, its rejected rows' 32-row tiles
+           redone by dc:169 in k_resid_flagged.
+  guard_all DCFM_FLAG_GUARD_ALL: the guard rejects every row, so every row goes through the default
+           path's own fallback (c2: resid_rows8 inside k_lambda; c4: every tile through
+           k_resid_flagged) -- the code the default path runs only in transients, at the same bar.
 """
 import numpy as np
 import pytest
@@ -60,7 +63,10 @@ CONFIGS = {
     "c4": (2000, 10000, 8, 100, False),
 }
 EXACT = 0x10          # DCFM_FLAG_EXACT_RESIDUAL
-CASES = [(name, mode) for mode in ("exact", "default") for name in CONFIGS]
+GUARD_ALL = 0x40      # DCFM_FLAG_GUARD_ALL: the guard's residual fallback for every row (narrow and wide)
+MODE_FLAGS = {"exact": EXACT, "default": 0, "guard_all": GUARD_ALL}
+CASES = ([(name, mode) for mode in ("exact", "default") for name in CONFIGS] +
+         [("c2", "guard_all"), ("c4", "guard_all")])
 
 
 def _sigma_err(smp, SigL, p, w=2048):
@@ -92,7 +98,6 @@ def _ps_direct_err(got, start_it, D, c, it):
 @pytest.mark.parametrize("name,mode", CASES)
 def test_baseline_shape_parity(dcfm, name, mode):
     n, p, g, K, stagewise = CONFIGS[name]
-    exact = mode == "exact"
     burnin, mcmc, thin = 1, 1, 1
     N = burnin + mcmc
     effsamp = mcmc / thin
@@ -100,7 +105,7 @@ def test_baseline_shape_parity(dcfm, name, mode):
     st, Yd = c["st"], c["Yd"]
     D = V.Data(Yd)
     smp = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], burnin, mcmc, thin, inject_draws=True,
-                       flags=EXACT if exact else 0)
+                       flags=MODE_FLAGS[mode])
     try:
         smp.set_data(Yd)
         smp.set_state({f: v for f, v in state_dict(st).items() if f != "eta"})

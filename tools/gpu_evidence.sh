@@ -8,7 +8,7 @@
 TAG=$1; PHASE=${2:-c3}
 mkdir -p gpurun_out
 if [ "$PHASE" = "c3" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/t_$TAG.log 2>&1 || { echo "pytest failed $?"; tail -30 gpurun_out/t_$TAG.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rA --timeout 300 --timeout-method thread --junitxml=gpurun_out/t_$TAG.xml > gpurun_out/t_$TAG.log 2>&1 || { echo "pytest failed $?"; tail -30 gpurun_out/t_$TAG.log; exit 1; }
   grep -E "passed|failed" gpurun_out/t_$TAG.log | tail -1
   timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo "smoke failed"; tail gpurun_out/smoke_$TAG.log; exit 1; }
   tail -1 gpurun_out/smoke_$TAG.log
@@ -25,6 +25,8 @@ run() {   # name, bench args, extra bench args (not part of the profiled command
 if [ "$PHASE" = "c3" ]; then
   run ${TAG} "$C3"
   python3 tools/show_bench.py gpurun_out/bench_${TAG}.json
+  run ${TAG}_exact "$C3 --exact-residual" "--no-cpu-baseline --converged-mcmc 0"
+  python3 tools/show_bench.py gpurun_out/bench_${TAG}_exact.json
   exit 0
 fi
 run ${TAG}_c4 "$C4" "--no-cpu-baseline"
