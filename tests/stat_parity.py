@@ -20,9 +20,10 @@ The test passes when
     |z| < 2.576,   z = sum_r d_r / sqrt(sum_r s_r^2 (1 + 1/M))     (two-sided 1 %)
 for both norms.  The bar in error units, 2.576 sqrt(sum_r s_r^2 (1 + 1/M)) / R, is what R oracle
 replicates can resolve; it is reported with each oracle value's percentile among its case's GPU
-chains.  Where the chains' errors are clearly bimodal (c3), the same comparison runs within each mode
-(each oracle value against the GPU chains of its own mode) together with a binomial test of the mode
-shares -- a bar of a fraction of a percent where the unconditional one is a few percent.  Everything
+chains (a Kolmogorov-Smirnov test of those percentiles against Uniform(0, 1) at 1 %).  Where the
+chains' errors fall into well-separated modes (c2, c3), the same comparison also runs within the modes
+(each oracle value against the GPU chains of the major mode it falls in) -- a bar of a fraction of a
+percent where the unconditional one is a few percent.  Everything
 goes to gpurun_out/<name>_parity_gpu.json (kept under profiles/ per round)."""
 from __future__ import annotations
 
@@ -31,6 +32,7 @@ import os
 from pathlib import Path
 
 import numpy as np
+from scipy import stats
 
 import oracle
 from helpers import make_case, state_dict
@@ -40,46 +42,50 @@ DCFM_ERR_NUMERIC = 5           # include/dcfm.h
 M_CHAINS = 16
 
 
-def _two_means(x, iters=50):
-    """1-D k-means with two centres (initialised at the quartiles, so a few outlying chains do not take a
-    centre of their own)."""
-    c = np.quantile(x, [0.25, 0.75])
-    for _ in range(iters):
-        lab = np.abs(x[:, None] - c[None, :]).argmin(axis=1)
-        c = np.array([x[lab == k].mean() if np.any(lab == k) else c[k] for k in range(2)])
-    return c, lab
+def _clusters(x, gap_factor=20.0):
+    """Modes of the GPU chains' errors: the sorted values split wherever consecutive values lie more than
+    gap_factor times the median consecutive spacing apart.  Returns [(lo, hi, values)]."""
+    v = np.sort(np.asarray(x))
+    gaps = np.diff(v)
+    thr = gap_factor * max(float(np.median(gaps)), 1e-12)
+    cuts = np.nonzero(gaps > thr)[0]
+    parts = np.split(v, cuts + 1)
+    return [(float(p_[0]), float(p_[-1]), p_) for p_ in parts], thr
 
 
 def _robust_sd(x):
     return 1.4826 * float(np.median(np.abs(x - np.median(x))))
 
 
-def _mode_conditional(rows, key, m_chains):
-    """Where the GPU chains' errors are clearly bimodal (two clusters, each >= 10 % of the chains, whose
-    medians lie more than 8 robust sds (1.4826 MAD) apart), the sharper check: each oracle value against the
-    GPU chains of ITS mode (median and robust sd of the mode, z as above), and the oracle's share of the
-    upper mode against the GPU's (exact binomial test).  None if not bimodal."""
-    from scipy import stats
+def _mode_conditional(rows, key):
+    """Where the GPU chains' errors fall into well-separated modes (c2, c3: a few posterior modes that a
+    chain settles in), the sharper check: each oracle value against the GPU chains of the major mode
+    (>= 10 % of the chains) it falls in -- the mode's median and robust sd (1.4826 MAD), z as in the
+    unconditional test -- for the oracle values that fall in one.  None if fewer than 3 do."""
     g = np.concatenate([np.asarray(r[f"gpu_{key}"]) for r in rows])
-    c, lab = _two_means(g)
-    if min(np.mean(lab == 0), np.mean(lab == 1)) < 0.1:
+    parts, thr = _clusters(g)
+    major = [(lo, hi, v) for lo, hi, v in parts if len(v) >= 0.1 * len(g) and len(v) >= 5]
+    if len(major) < 2:
         return None
-    med = np.array([np.median(g[lab == k]) for k in range(2)])
-    sds = np.array([_robust_sd(g[lab == k]) for k in range(2)])
-    if abs(med[1] - med[0]) < 8.0 * float(np.sqrt(np.mean(sds ** 2))):
-        return None
-    ns = np.array([np.sum(lab == k) for k in range(2)])
     o = np.array([r[f"oracle_{key}"] for r in rows])
-    ol = np.abs(o[:, None] - c[None, :]).argmin(axis=1)
-    d = o - med[ol]
-    scale = float(np.sqrt(np.sum(sds[ol] ** 2 * (1.0 + 1.0 / ns[ol]))))
-    up = int(np.argmax(c))
-    k_or, p_gpu = int(np.sum(ol == up)), float(np.mean(lab == up))
-    return {"medians": med.tolist(), "robust_sd": sds.tolist(), "gpu_counts": ns.tolist(),
-            "oracle_modes": ol.tolist(), "z": float(np.sum(d) / scale), "mean_diff": float(np.mean(d)),
-            "bar": Z99 * scale / len(o), "bar_rel": Z99 * scale / len(o) / float(np.mean(o)),
-            "oracle_upper": k_or, "gpu_upper_share": p_gpu,
-            "p_mix": float(stats.binomtest(k_or, len(o), p_gpu).pvalue)}
+    d, var, which = [], [], []
+    for ov in o:
+        k = next((k for k, (lo, hi, v) in enumerate(major) if lo - thr <= ov <= hi + thr), None)
+        which.append(k)
+        if k is None:
+            continue
+        v = major[k][2]
+        sd = _robust_sd(v)
+        d.append(ov - float(np.median(v)))
+        var.append(sd * sd * (1.0 + 1.0 / len(v)))
+    if len(d) < 3:
+        return None
+    scale = float(np.sqrt(np.sum(var)))
+    return {"modes": [{"median": float(np.median(v)), "robust_sd": _robust_sd(v), "count": int(len(v))}
+                      for lo, hi, v in major],
+            "minor_chains": int(len(g) - sum(len(v) for _, _, v in major)), "oracle_mode": which,
+            "n_used": len(d), "z": float(np.sum(d) / scale), "mean_diff": float(np.mean(d)),
+            "bar": Z99 * scale / len(d), "bar_rel": Z99 * scale / len(d) / float(np.mean(o))}
 
 
 def run_paired(dcfm, fixture: Path, name: str, seed0: int, dense_truth: bool, record_property=None,
@@ -138,10 +144,13 @@ def run_paired(dcfm, fixture: Path, name: str, seed0: int, dense_truth: bool, re
                         "mean_oracle": base, "mean_gpu": float(np.mean(mu)), "gpu_sd_per_case": sd.tolist(),
                         "oracle_percentile_among_gpu_chains": pct}
         verdicts[key] = abs(z) < Z99
-        modal = _mode_conditional(rows, key, m_chains)
+        # the oracle values' percentiles among their cases' GPU chains are Uniform(0, 1) under parity
+        summary[key]["ks_p"] = float(stats.kstest(pct, "uniform").pvalue)
+        verdicts[key] = verdicts[key] and summary[key]["ks_p"] > 0.01
+        modal = _mode_conditional(rows, key)
         if modal is not None:
             summary[key]["modes"] = modal
-            verdicts[key] = verdicts[key] and abs(modal["z"]) < Z99 and modal["p_mix"] > 0.01
+            verdicts[key] = verdicts[key] and abs(modal["z"]) < Z99
     out = Path(os.environ.get("DCFM_PARITY_OUT", "gpurun_out"))
     out.mkdir(parents=True, exist_ok=True)
     (out / f"{name}_parity_gpu.json").write_text(json.dumps(summary, indent=1) + "\n")
@@ -150,8 +159,9 @@ def run_paired(dcfm, fixture: Path, name: str, seed0: int, dense_truth: bool, re
             for f in ("z", "mean_diff", "bar", "bar_rel"):
                 record_property(f"{key}_{f}", summary[key][f])
     print(f"{name.upper()}_PARITY", json.dumps({k: {**{kk: summary[k][kk] for kk in ("z", "mean_diff", "bar_rel")},
+                                                     "ks_p": summary[k]["ks_p"],
                                                      **({"modes": {kk: summary[k]["modes"][kk] for kk in
-                                                                   ("z", "bar_rel", "p_mix", "medians")}}
+                                                                   ("z", "bar_rel", "n_used")}}
                                                         if "modes" in summary[k] else {})}
                                                  for k in ("fro_rel", "op_rel")}))
     assert summary["p_oracle_none_broke"] > 0.01, ("breakdown rate", n_broke, R * m_chains)
