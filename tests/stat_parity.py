@@ -53,37 +53,35 @@ def _clusters(x, gap_factor=20.0):
     return [(float(p_[0]), float(p_[-1]), p_) for p_ in parts], thr
 
 
-def _robust_sd(x):
-    return 1.4826 * float(np.median(np.abs(x - np.median(x))))
-
-
 def _mode_conditional(rows, key):
     """Where the GPU chains' errors fall into well-separated modes (c2, c3: a few posterior modes that a
     chain settles in), the sharper check: each oracle value against the GPU chains of the major mode
-    (>= 10 % of the chains) it falls in -- the mode's median and robust sd (1.4826 MAD), z as in the
-    unconditional test -- for the oracle values that fall in one.  None if fewer than 3 do."""
+    (>= 10 % of the chains; outlying chains fall in modes of their own) nearest to it, if it lies within
+    10 of that mode's sds -- the mode's mean and sd, z as in the unconditional test -- for the oracle
+    values that do.  None if fewer than 3 do."""
     g = np.concatenate([np.asarray(r[f"gpu_{key}"]) for r in rows])
     parts, thr = _clusters(g)
-    major = [(lo, hi, v) for lo, hi, v in parts if len(v) >= 0.1 * len(g) and len(v) >= 5]
+    major = [v for lo, hi, v in parts if len(v) >= 0.1 * len(g) and len(v) >= 5]
     if len(major) < 2:
         return None
+    mus = np.array([float(np.mean(v)) for v in major])
+    sds = np.array([float(np.std(v, ddof=1)) for v in major])
+    ns = np.array([len(v) for v in major])
     o = np.array([r[f"oracle_{key}"] for r in rows])
     d, var, which = [], [], []
     for ov in o:
-        k = next((k for k, (lo, hi, v) in enumerate(major) if lo - thr <= ov <= hi + thr), None)
-        which.append(k)
-        if k is None:
+        k = int(np.argmin(np.abs(ov - mus)))
+        if abs(ov - mus[k]) > 10.0 * sds[k]:
+            which.append(None)
             continue
-        v = major[k][2]
-        sd = _robust_sd(v)
-        d.append(ov - float(np.median(v)))
-        var.append(sd * sd * (1.0 + 1.0 / len(v)))
+        which.append(k)
+        d.append(ov - mus[k])
+        var.append(sds[k] ** 2 * (1.0 + 1.0 / ns[k]))
     if len(d) < 3:
         return None
     scale = float(np.sqrt(np.sum(var)))
-    return {"modes": [{"median": float(np.median(v)), "robust_sd": _robust_sd(v), "count": int(len(v))}
-                      for lo, hi, v in major],
-            "minor_chains": int(len(g) - sum(len(v) for _, _, v in major)), "oracle_mode": which,
+    return {"modes": [{"mean": float(m), "sd": float(sd), "count": int(n)} for m, sd, n in zip(mus, sds, ns)],
+            "minor_chains": int(len(g) - ns.sum()), "oracle_mode": which,
             "n_used": len(d), "z": float(np.sum(d) / scale), "mean_diff": float(np.mean(d)),
             "bar": Z99 * scale / len(d), "bar_rel": Z99 * scale / len(d) / float(np.mean(o))}
 
