@@ -36,6 +36,17 @@
 
 namespace dcfm {
 
+#ifdef DCFM_WSTAMPS   // dev build: per-block [start, end] (s_memrealtime, 100 MHz) of the last full k_wcol,
+                      // and inside the block [2] OPS: A_m out / W tile: pass done, [3] OPS: U out / W tile:
+                      // operators arrived
+__device__ unsigned long long g_wstamps[8192][4];
+extern "C" int dcfm_debug_wstamps(unsigned long long *out, int nblocks) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), (size_t)nblocks * 32, 0, hipMemcpyDeviceToHost);
+}
+#define WSTAMP(s) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_wstamps[blockIdx.x][s] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define WSTAMP(s) do { } while (0)
+#endif
 
 // device helpers (MFMA, lane broadcast, rsqrt, register Cholesky): linalg.h
 
@@ -153,6 +164,7 @@ __device__ __forceinline__ void prep_ops(const Dims &d, double *__restrict__ ZM,
         chol_inv32(part[2], part[1], part[3], lds_l, lds_u, lane);
     }
     __syncthreads();
+    if (PUB) WSTAMP(3);
     {   // T = U U' (fp64 MFMA, one 16x16 tile per wave) -> part[2]; M1 = s1r T; U
         const int ti = wave >> 1, tj = wave & 1, j = lane & 15, q = lane >> 4;
         const d4 T = mfma_tile32<true>(part[1], part[1], ti, tj, lane);
@@ -1329,9 +1341,11 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
     const int i0 = rb * 64 * MT + wave * 16 * MT;
     d4 acc[MT][2];
     wpass_acc<KP, MT>(d, b.Y, b.Lam, b.omega, m, i0, 0, acc, [] {});
+    WSTAMP(2);
     // the operators are normally out long before the pass ends; their loads and the rows' X are
     // issued first, the first tile's normals drawn while they are in flight
     wait_count(b.sync + SYNC_ZM + m, zm_epoch);
+    WSTAMP(3);
     constexpr int NU = 4 * KP * KP / 256;
     double zv[NU];
     {
@@ -1371,12 +1385,6 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
     }
 }
 
-#ifdef DCFM_WSTAMPS   // dev build: per-block [start, end] (s_memrealtime, 100 MHz) of the last full k_wcol
-__device__ unsigned long long g_wstamps[8192][2];
-extern "C" int dcfm_debug_wstamps(unsigned long long *out, int nblocks) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), (size_t)nblocks * 16, 0, hipMemcpyDeviceToHost);
-}
-#endif
 __device__ __forceinline__ void wcol_body(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, int ops, int colsum,
                                           int wpass, unsigned long long ops_epoch, int xchol, const LamGen &lg,
                                           double *smem);
@@ -1406,6 +1414,7 @@ __device__ __forceinline__ void wcol_body(const Dims &d, const Bufs &b, const Dr
     if (ops) {
         if (blk < G) {
             prep_gram<true>(d, b.Lam, b.omega, b.A, b.ZM, blk, smem);
+            WSTAMP(2);
             signal_count(chunk_ctr + blk / chunk);   // A_m is out; the operators follow
             prep_ops<true>(d, b.ZM, blk, smem);
             signal_count(b.sync + SYNC_ZM + blk);    // the Z operators are out (the W tiles draw Z)

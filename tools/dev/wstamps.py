@@ -22,30 +22,38 @@ smp.run(1, 26)
 smp.synchronize()
 lib = smp.lib
 lib.dcfm_debug_wstamps.argtypes = [C.c_void_p, C.c_int]
-buf = np.zeros((8192, 2), dtype=np.uint64)
+buf = np.zeros((8192, 4), dtype=np.uint64)
 lib.dcfm_debug_wstamps(buf.ctypes.data, 8192)
 nb = int(np.max(np.nonzero(buf[:, 0])[0])) + 1
 b = buf[:nb].astype(np.int64)
 t0 = b[:, 0].min()
 st, en = (b[:, 0] - t0) / 100.0, (b[:, 1] - t0) / 100.0
+s2, s3 = (b[:, 2] - t0) / 100.0, (b[:, 3] - t0) / 100.0
 G = g
-nxs = 1
-while G // nxs > 8 and (G // nxs) % 2 == 0:
-    nxs *= 2
+nxs = 1 if G <= 8 else G
+if G > 8:
+    chunk = 1
+    while G // chunk > 8 and (G // chunk) % 2 == 0:
+        chunk *= 2
+    nxs = G // chunk
 NP = (n + 127) // 128 * 128
-nw = NP // 128 * G
-roles = [("OPS", 0, G), ("colsum", G, 2 * G)]
-# the A-sum blocks: whatever lies between colsum and the W tiles
-nsum = nb - 2 * G - nw
-lamb = 0
-# the W tiles are the run of nw blocks after the sums; lam blocks follow
-for ns in range(0, 65):
-    pass
-print(f"blocks with stamps: {nb}")
-for name, lo, hi in roles:
-    print(f"{name:8s} [{lo},{hi}) start med {np.median(st[lo:hi]):7.2f} max {st[lo:hi].max():7.2f}  end med {np.median(en[lo:hi]):7.2f} max {en[lo:hi].max():7.2f} us")
-# print the rest in windows of 64 blocks
-for lo in range(2 * G, nb, 64):
-    hi = min(nb, lo + 64)
-    print(f"blk [{lo},{hi}) start min {st[lo:hi].min():7.2f} med {np.median(st[lo:hi]):7.2f} max {st[lo:hi].max():7.2f}  end min {en[lo:hi].min():7.2f} med {np.median(en[lo:hi]):7.2f} max {en[lo:hi].max():7.2f} us")
+wmode = 2 if (NP // 128) * G < 256 else 1
+nw = NP // (64 * (3 - wmode)) * G
+w0 = 2 * G + nxs
+
+
+def line(name, lo, hi, *cols):
+    out = f"{name:10s} [{lo},{hi})"
+    for lab, v in cols:
+        out += f"  {lab} med {np.median(v[lo:hi]):6.2f} max {v[lo:hi].max():6.2f}"
+    print(out)
+
+
+print(f"blocks with stamps: {nb}  (G {G}, A-sum blocks {nxs}, W tiles {nw} of {64 * (3 - wmode)} rows)")
+line("OPS", 0, G, ("start", st), ("A out", s2), ("U out", s3), ("end", en))
+line("colsum", G, 2 * G, ("start", st), ("end", en))
+line("A-sum", 2 * G, w0, ("start", st), ("end", en))
+line("W tiles", w0, w0 + nw, ("start", st), ("pass", s2), ("ops in", s3), ("end", en))
+if nb > w0 + nw:
+    line("lam gen", w0 + nw, nb, ("start", st), ("end", en))
 print(f"launch span {en.max():.2f} us")
