@@ -38,10 +38,10 @@ namespace dcfm {
 
 #ifdef DCFM_WSTAMPS   // dev build: per-block [start, end] (s_memrealtime, 100 MHz) of the last full k_wcol,
                       // and inside the block [2] OPS: A_m out / W tile: pass done, [3] OPS: U out / W tile:
-                      // operators arrived
-__device__ unsigned long long g_wstamps[8192][4];
+                      // operators arrived, [4] W tile: operators staged, [5] W tile: first 16-row draw done
+__device__ unsigned long long g_wstamps[8192][8];
 extern "C" int dcfm_debug_wstamps(unsigned long long *out, int nblocks) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), (size_t)nblocks * 32, 0, hipMemcpyDeviceToHost);
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), (size_t)nblocks * 64, 0, hipMemcpyDeviceToHost);
 }
 #define WSTAMP(s) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_wstamps[blockIdx.x][s] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
@@ -1368,6 +1368,7 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
         Ms[mat][rem / KP][rem % KP] = zv[u];
     }
     __syncthreads();
+    WSTAMP(4);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
@@ -1381,6 +1382,7 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
         }
         zdraw_rows(d, Ms, wv, xv[a], ev[a], b.Z + ((size_t)m * d.NP + i) * KP, b.Sp + ((size_t)m * d.NP + i) * KP,
                    i < d.n, c, q);
+        if (a == 0) WSTAMP(5);
         __builtin_amdgcn_sched_barrier(0);   // one tile's draw at a time (registers)
     }
 }
@@ -1395,13 +1397,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DCFM_WCOL_W
                                               int wpass, unsigned long long ops_epoch, int xchol, LamGen lg) {
     __shared__ double smem[PREP_SMEM];
 #ifdef DCFM_WSTAMPS
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_readcyclecounter();
 #endif
     wcol_body(d, b, dr, iter, ops, colsum, wpass, ops_epoch, xchol, lg, smem);
 #ifdef DCFM_WSTAMPS
     if (wpass && threadIdx.x == 0 && blockIdx.x < 8192) {
         g_wstamps[blockIdx.x][0] = t0;
         g_wstamps[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+        g_wstamps[blockIdx.x][6] = c0;                                 // shader clock: the block's mean frequency
+        g_wstamps[blockIdx.x][7] = __builtin_readcyclecounter();
     }
 #endif
 }

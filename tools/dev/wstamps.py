@@ -22,13 +22,13 @@ smp.run(1, 26)
 smp.synchronize()
 lib = smp.lib
 lib.dcfm_debug_wstamps.argtypes = [C.c_void_p, C.c_int]
-buf = np.zeros((8192, 4), dtype=np.uint64)
+buf = np.zeros((8192, 8), dtype=np.uint64)
 lib.dcfm_debug_wstamps(buf.ctypes.data, 8192)
 nb = int(np.max(np.nonzero(buf[:, 0])[0])) + 1
 b = buf[:nb].astype(np.int64)
 t0 = b[:, 0].min()
 st, en = (b[:, 0] - t0) / 100.0, (b[:, 1] - t0) / 100.0
-s2, s3 = (b[:, 2] - t0) / 100.0, (b[:, 3] - t0) / 100.0
+s2, s3, s4, s5 = ((b[:, k] - t0) / 100.0 for k in (2, 3, 4, 5))
 G = g
 nxs = 1 if G <= 8 else G
 if G > 8:
@@ -53,7 +53,9 @@ print(f"blocks with stamps: {nb}  (G {G}, A-sum blocks {nxs}, W tiles {nw} of {6
 line("OPS", 0, G, ("start", st), ("A out", s2), ("U out", s3), ("end", en))
 line("colsum", G, 2 * G, ("start", st), ("end", en))
 line("A-sum", 2 * G, w0, ("start", st), ("end", en))
-line("W tiles", w0, w0 + nw, ("start", st), ("pass", s2), ("ops in", s3), ("end", en))
+line("W tiles", w0, w0 + nw, ("start", st), ("pass", s2), ("ops in", s3), ("staged", s4), ("draw 1", s5), ("end", en))
 if nb > w0 + nw:
     line("lam gen", w0 + nw, nb, ("start", st), ("end", en))
+clk = (b[:, 7] - b[:, 6]) / np.maximum(b[:, 1] - b[:, 0], 1) * 100e6 / 1e9   # GHz
+print(f"W tiles shader clock (GHz): med {np.median(clk[w0:w0 + nw]):.3f} min {clk[w0:w0 + nw].min():.3f} max {clk[w0:w0 + nw].max():.3f}")
 print(f"launch span {en.max():.2f} us")
