@@ -30,37 +30,53 @@ namespace wide {
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // ============================================================================
-// k_gram: A_m = (w o Lambda_m)' Lambda_m, 32x32 tile (ta, tb) per block; the 4
-// waves split the rows j, partial tiles summed in LDS in a fixed order.  dc:98-99
-// Lane (r, q), k-step s: rows j = j0 + 4s + q; A operand w_j L[j][32ta+2r+ea],
+// k_gram: A_m = (w o Lambda_m)' Lambda_m, 32x32 tile (ta, tb) per block; the GRAM_WAVES
+// waves take the k-steps (4 rows j each) round-robin, one register prefetch ahead, and the
+// partial tiles are summed in LDS in a fixed order (pairwise tree).  16 waves: the c4 launch
+// is 128 blocks, each wave's chain a latency-bound run of dependent loads and MFMAs (4 waves:
+// 40 us, on the critical path between k_lambda and the W pass).                     dc:98-99
+// Lane (r, q), k-step s: rows j = 4s + q; A operand w_j L[j][32ta+2r+ea],
 // B operand L[j][32tb+2r+eb]  ->  acc[ea][eb][g] = A[32ta+2(q+4g)+ea][32tb+2r+eb].
 // ============================================================================
+#ifndef DCFM_GRAM_WAVES
+#define DCFM_GRAM_WAVES 16
+#endif
+constexpr int GRAM_WAVES = DCFM_GRAM_WAVES;
 template <int KW>
-__global__ __launch_bounds__(256) void k_gram(Dims d, const double *__restrict__ Lam,
-                                              const double *__restrict__ omega, double *__restrict__ A) {
+__global__ __launch_bounds__(64 * GRAM_WAVES) void k_gram(Dims d, const double *__restrict__ Lam,
+                                                          const double *__restrict__ omega, double *__restrict__ A) {
     constexpr int KT = KW / 32;
-    __shared__ double red[4][32][33];
+    __shared__ double red[GRAM_WAVES][32][33];
     const int m = blockIdx.y, ta = blockIdx.x / KT, tb = blockIdx.x % KT;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = lane & 15, q = lane >> 4;
     const double *L = Lam + (size_t)m * d.PP * KW;
     const double *w = omega + (size_t)m * d.PP;
-    const int rows = d.PP >> 2, j0 = wave * rows;
+    const int nks = d.PP >> 2;                 // k-steps of 4 rows
     d4 acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-    for (int s = 0; s < rows; s += 4) {
-        const int j = j0 + s + q;
-        const double wj = w[j];
-        const d2 la = *reinterpret_cast<const d2 *>(L + (size_t)j * KW + 32 * ta + 2 * r);
-        const d2 lb = *reinterpret_cast<const d2 *>(L + (size_t)j * KW + 32 * tb + 2 * r);
+    auto ld = [&](int s, double &wj, d2 &la, d2 &lb) {
+        const int j = 4 * (s < nks ? s : nks - 1) + q;   // clamped: the prefetch past the end is unused
+        wj = w[j];
+        la = *reinterpret_cast<const d2 *>(L + (size_t)j * KW + 32 * ta + 2 * r);
+        lb = *reinterpret_cast<const d2 *>(L + (size_t)j * KW + 32 * tb + 2 * r);
+    };
+    double wj;
+    d2 la, lb;
+    ld(wave, wj, la, lb);
+    for (int s = wave; s < nks; s += GRAM_WAVES) {
+        double wn;
+        d2 lan, lbn;
+        ld(s + GRAM_WAVES, wn, lan, lbn);
         const double a0 = la.x * wj, a1 = la.y * wj;
         acc[0][0] = mfma16x16x4(a0, lb.x, acc[0][0]);
         acc[0][1] = mfma16x16x4(a0, lb.y, acc[0][1]);
         acc[1][0] = mfma16x16x4(a1, lb.x, acc[1][0]);
         acc[1][1] = mfma16x16x4(a1, lb.y, acc[1][1]);
+        wj = wn; la = lan; lb = lbn;
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g)
@@ -70,9 +86,16 @@ __global__ __launch_bounds__(256) void k_gram(Dims d, const double *__restrict__
             for (int eb = 0; eb < 2; ++eb) red[wave][2 * (q + 4 * g) + ea][2 * r + eb] = acc[ea][eb][g];
     __syncthreads();
     double *out = A + (size_t)m * KW * KW + (size_t)(32 * ta) * KW + 32 * tb;
-    for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+    for (int e = threadIdx.x; e < 32 * 32; e += 64 * GRAM_WAVES) {
         const int a = e >> 5, b = e & 31;
-        out[(size_t)a * KW + b] = (red[0][a][b] + red[1][a][b]) + (red[2][a][b] + red[3][a][b]);
+        double v[GRAM_WAVES];
+#pragma unroll
+        for (int u = 0; u < GRAM_WAVES; ++u) v[u] = red[u][a][b];
+#pragma unroll
+        for (int h = 1; h < GRAM_WAVES; h <<= 1)   // pairwise: ((v0 + v1) + (v2 + v3)) + ...
+#pragma unroll
+            for (int u = 0; u < GRAM_WAVES; u += 2 * h) v[u] += v[u + h];
+        out[(size_t)a * KW + b] = v[0];
     }
 }
 
@@ -84,13 +107,18 @@ __global__ __launch_bounds__(256) void k_gram(Dims d, const double *__restrict__
 //   R'\(R\bz) + R'\z is T bz + U z (quirk Q2), with bz = s1r (W - sr A X) formed in
 //   k_zdraw from A directly.  Tiled LDS Cholesky / inverse / U U' (tile_linalg.h).
 // ============================================================================
+#ifndef DCFM_TILE_THREADS
+#define DCFM_TILE_THREADS 1024
+#endif
+constexpr int TILE_THREADS = DCFM_TILE_THREADS;   // k_prep / k_xchol: 16 waves share the tile steps (c4: 4 waves
+                                                  // 99 / 77 us, 16 with the look-ahead 40 / 48 us)
 template <int KW>
-__global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__ A, double *__restrict__ ZM) {
+__global__ __launch_bounds__(TILE_THREADS) void k_prep(Dims d, const double *__restrict__ A, double *__restrict__ ZM) {
     constexpr int NB = KW / tile::TS, NT = tile::ntiles(NB);
     __shared__ double Ts[NT * tile::TSZ], Us[NT * tile::TSZ], lds_l[32], lds_u[16];
     const int m = blockIdx.x, N = d.K, nb = (N + tile::TS - 1) / tile::TS, t = threadIdx.x;
     const double *Am = A + (size_t)m * KW * KW;
-    for (int e = t; e < tile::ntiles(nb) * tile::TS * tile::TS; e += 256) {
+    for (int e = t; e < tile::ntiles(nb) * tile::TS * tile::TS; e += TILE_THREADS) {
         int I, J;
         tile::tri_pair(e >> 8, I, J);
         const int r = (e >> 4) & 15, c = e & 15, R = 16 * I + r, Cc = 16 * J + c;
@@ -110,11 +138,11 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 // Rx = cholcov(Xprec) (dc:118); XM = {Tx = sqrt(rho) Ux Ux', Ux = Rx^{-T}}.
 // ============================================================================
 template <int KW>
-__global__ __launch_bounds__(256) void k_xchol(Dims d, const double *__restrict__ xa_all, double *__restrict__ XM) {
+__global__ __launch_bounds__(TILE_THREADS) void k_xchol(Dims d, const double *__restrict__ xa_all, double *__restrict__ XM) {
     constexpr int NB = KW / tile::TS, NT = tile::ntiles(NB);
     __shared__ double Ts[NT * tile::TSZ], Us[NT * tile::TSZ], lds_l[32], lds_u[16];
     const int N = d.K, nb = (N + tile::TS - 1) / tile::TS, t = threadIdx.x;
-    for (int e = t; e < tile::ntiles(nb) * tile::TS * tile::TS; e += 256) {
+    for (int e = t; e < tile::ntiles(nb) * tile::TS * tile::TS; e += TILE_THREADS) {
         int I, J;
         tile::tri_pair(e >> 8, I, J);
         const int r = (e >> 4) & 15, c = e & 15, R = 16 * I + r, Cc = 16 * J + c;
@@ -631,35 +659,62 @@ __device__ __forceinline__ void scan_prod_nv(double (&v)[NV], int l) {
     v[0] = wave_scan_prod(v[0], l);
     if (NV == 2) v[NV - 1] = wave_scan_prod(v[NV - 1], l) * readlane_d(v[0], 63);
 }
+// The chain over h as the narrow kernel runs it (kernels.hip delta_chain): with y_h = 1 / F_h the
+// recurrence is affine, y_{h+1} = alpha_h y_h + beta_h, alpha_h = b_h dold_h / G_h, beta_h = c_h dold_h /
+// G_h, c_h = (0.5 / dref_h) T_h, and dn_h = G_h y_h / (b_h y_h + c_h); the maps compose by a wave scan
+// (log2 steps) instead of K dependent steps of lane reads (measured 48.7 us per iteration at c4, a
+// serial chain on the critical path).  NV = 2: index l + 64 of the second slice composes with the
+// first slice's total map (lane 63).  Every term is positive: the reassociation moves the result
+// by a few ulps only (dc:157-163).
+__device__ __forceinline__ void affine_scan(double &A, double &B, int l) {   // inclusive, lane 0 first
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double Ap = __shfl_up(A, o, 64), Bp = __shfl_up(B, o, 64);
+        if (l >= o) {
+            B = fma(A, Bp, B);
+            A = A * Ap;
+        }
+    }
+}
 template <int NV>
 __device__ __forceinline__ void delta_chain_nv(const Dims &d, int l, const double (&T)[NV], const double (&G)[NV],
                                const double (&idold)[NV], const double (&idref)[NV], double (&dnew)[NV]) {
-    double F = 1.0;
+    double bh[NV], c[NV], A[NV], B[NV];
+    bool act[NV];
 #pragma unroll
-    for (int s = 0; s < NV; ++s) dnew[s] = 1.0;
-    for (int h = 0; h < d.K; ++h) {
-        const bool hi = (NV == 2) && h >= 64;
-        const int hl = h & 63;
-        const double Th = readlane_d(hi ? T[NV - 1] : T[0], hl), ih = readlane_d(hi ? idref[NV - 1] : idref[0], hl);
-        const double ioh = readlane_d(hi ? idold[NV - 1] : idold[0], hl), Gh = readlane_d(hi ? G[NV - 1] : G[0], hl);
-        const double bd = (h == 0 ? d.bd1 : d.bd2) + (0.5 * ih) * (F * Th);   // dc:157,161
-        const double dn = (1.0 / bd) * Gh;                                      // dc:158,163
-        if (l == hl) {
-            if (hi) dnew[NV - 1] = dn;
-            else dnew[0] = dn;
-        }
-        F = F * (dn * ioh);
+    for (int s = 0; s < NV; ++s) {
+        const int idx = l + 64 * s;
+        act[s] = idx < d.K;
+        bh[s] = (idx == 0) ? d.bd1 : d.bd2;
+        c[s] = (0.5 * idref[s]) * T[s];
+        const double inv = 1.0 / (idold[s] * G[s]);              // dold_h / G_h
+        A[s] = act[s] ? bh[s] * inv : 1.0;                        // identity map on idle indices
+        B[s] = act[s] ? c[s] * inv : 0.0;
+        affine_scan(A[s], B[s], l);
+    }
+    if (NV == 2) {   // the second slice after the whole first one
+        const double A0 = readlane_d(A[0], 63), B0 = readlane_d(B[0], 63);
+        B[NV - 1] = fma(A[NV - 1], B0, B[NV - 1]);
+        A[NV - 1] = A[NV - 1] * A0;
+    }
+    double yin[NV];
+#pragma unroll
+    for (int s = 0; s < NV; ++s) yin[s] = A[s] + B[s];            // y_{idx+1} (y_0 = 1)
+#pragma unroll
+    for (int s = 0; s < NV; ++s) {
+        const double yprev = __shfl_up(yin[s], 1, 64);
+        const double y = (l == 0) ? (s == 0 ? 1.0 : readlane_d(yin[0], 63)) : yprev;   // y_idx
+        dnew[s] = act[s] ? G[s] * y / fma(bh[s], y, c[s]) : 1.0;
     }
 }
 
+// one wave = global shard m, lane t (< 64 active)
 template <int KW>
-__global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__ sall,
-                                               const double *__restrict__ delta_in, const double *__restrict__ tau_in,
-                                               double *__restrict__ delta_out, double *__restrict__ tau_out,
-                                               DrawsDev dr, int64_t iter) {
+__device__ __forceinline__ void delta_shard_w(const Dims &d, const double *__restrict__ sall,
+                                              const double *__restrict__ delta_in, const double *__restrict__ tau_in,
+                                              double *__restrict__ delta_out, double *__restrict__ tau_out,
+                                              const DrawsDev &dr, int64_t iter, int m, int t) {
     constexpr int NV = KW / 64;
-    const int m = blockIdx.x;   // global shard
-    const int t = threadIdx.x;
     if (t < 64) {
         const int l = t;
         double d0[NV], T0[NV], G0[NV], id0[NV], d0new[NV];
@@ -708,6 +763,14 @@ __global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__
     }
 }
 
+template <int KW>
+__global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__ sall,
+                                               const double *__restrict__ delta_in, const double *__restrict__ tau_in,
+                                               double *__restrict__ delta_out, double *__restrict__ tau_out,
+                                               DrawsDev dr, int64_t iter) {
+    delta_shard_w<KW>(d, sall, delta_in, tau_in, delta_out, tau_out, dr, iter, blockIdx.x, threadIdx.x);
+}
+
 // ============================================================================
 // launchers (kernels.hip dispatches here when d.kp != 32)
 // ============================================================================
@@ -724,12 +787,13 @@ __global__ __launch_bounds__(64) void k_delta(Dims d, const double *__restrict__
 
 void launch_prep(const Dims &d, const Bufs &b, hipStream_t s) {
     WIDE_DISPATCH(d.kp, {
-        hipLaunchKernelGGL(k_gram<KW>, dim3((KW / 32) * (KW / 32), d.G), dim3(256), 0, s, d, b.Lam, b.omega, b.A);
-        hipLaunchKernelGGL(k_prep<KW>, dim3(d.G), dim3(256), 0, s, d, b.A, b.ZM);
+        hipLaunchKernelGGL(k_gram<KW>, dim3((KW / 32) * (KW / 32), d.G), dim3(64 * GRAM_WAVES), 0, s, d, b.Lam, b.omega,
+                           b.A);
+        hipLaunchKernelGGL(k_prep<KW>, dim3(d.G), dim3(TILE_THREADS), 0, s, d, b.A, b.ZM);
     });
 }
 void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
-    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_xchol<KW>, dim3(1), dim3(256), 0, s, d,
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_xchol<KW>, dim3(1), dim3(TILE_THREADS), 0, s, d,
                                            d.coll ? b.xa_all : b.xa, b.XM));
 }
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {

@@ -6,11 +6,12 @@
 // index I(I+1)/2 + J, each tile column-major with a 17-double pitch
 // (element (r, c) at c*TLD + r).  nb = ceil(K/16) tile rows; rows >= K are an
 // identity pad.
-//   * diagonal tile: one wave, chol_inv16 (its inverse U_JJ as well);
+//   * diagonal tile: one wave, chol_inv16 (its inverse U_JJ as well), one column ahead of
+//     the trailing update (potrf_inv's look-ahead);
 //   * panel below it: L_IJ = A_IJ U_JJ' as v_mfma_f64_16x16x4;
 //   * trailing update A_IK -= L_IJ L_KJ' as v_mfma_f64_16x16x4 (4 k-steps per
-//     tile, tiles dealt over the 4 waves).
-// Three barriers per tile column: a K = 100 factorisation is 7 tile columns.
+//     tile, tiles dealt over the other waves).
+// Two barriers per tile column: a K = 100 factorisation is 7 tile columns.
 #pragma once
 #include "linalg.h"
 
@@ -42,31 +43,23 @@ __device__ __forceinline__ void tile_nt_acc(double *C, const double *A, const do
     for (int g = 0; g < 4; ++g) C[i * TLD + kq + 4 * g] = acc[g];
 }
 
-// trailing update after tile column J: A_IK -= L_IJ L_KJ' for J < K <= I < nb
-__device__ __forceinline__ void trailing(double *T, int J, int nb, int wave, int lane) {
-    const int m = nb - 1 - J, ntr = m * (m + 1) / 2, nw = blockDim.x >> 6;
-    for (int tt = wave; tt < ntr; tt += nw) {
-        int a, b;
-        tri_pair(tt, a, b);
-        const int I = J + 1 + a, K = J + 1 + b;
-        tile_nt_acc(T + tix(I, K) * TSZ, T + tix(I, J) * TSZ, T + tix(K, J) * TSZ, -1.0, lane);
-    }
-}
-
 // Blocked right-looking Cholesky of the tiled lower triangle together with the diagonal
-// blocks of its inverse (any multiple of 64 threads).  Per tile column J: wave 0 factors
-// the diagonal tile and writes U_JJ = L_JJ^{-1} (chol_inv16, LDL' form) into U; the panel
-// tiles become L_IJ = A_IJ U_JJ' (one MFMA product each, tiles dealt over the waves); the
-// trailing tiles take A_IK -= L_IJ L_KJ'.  The diagonal tiles stay symmetric (the trailing
-// product updates the whole tile), so chol_inv16's row-major read of the column-major tile
-// sees the same values.
+// blocks of its inverse (any multiple of 64 threads, at least two waves).  Per tile column J: the
+// panel tiles become L_IJ = A_IJ U_JJ' (one MFMA product each, tiles dealt over the waves); then
+// wave 0 takes the next diagonal tile's update A_{J+1,J+1} -= L_{J+1,J} L_{J+1,J}' and factors it
+// (chol_inv16, LDL' form: U_{J+1,J+1} = L^{-1} into U) while the other waves run the rest of the
+// trailing update A_IK -= L_IJ L_KJ' (look-ahead: the one-wave factorisation, the serial part,
+// overlaps the trailing update instead of following it).  Every tile sees the same operations in
+// the same order as without the look-ahead.  The diagonal tiles stay symmetric (the trailing
+// product updates the whole tile), so chol_inv16's row-major read of the column-major tile sees the
+// same values.
 __device__ __forceinline__ void potrf_inv(double *T, double *U, int nb, double *lds_l, double *lds_u) {
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, nw = blockDim.x >> 6;
     const int i = lane & 15, kq = lane >> 4;
+    if (wave == 0) chol_inv16_p<TLD, true>(T, 0, U, lds_l, lds_u, lane);
+    __syncthreads();
 #pragma unroll 1
     for (int J = 0; J < nb; ++J) {
-        if (wave == 0) chol_inv16_p<TLD, true>(T + tix(J, J) * TSZ, 0, U + tix(J, J) * TSZ, lds_l, lds_u, lane);
-        __syncthreads();
         const double *Uj = U + tix(J, J) * TSZ;
         for (int I = J + 1 + wave; I < nb; I += nw) {
             double *A = T + tix(I, J) * TSZ;
@@ -78,7 +71,22 @@ __device__ __forceinline__ void potrf_inv(double *T, double *U, int nb, double *
             for (int g = 0; g < 4; ++g) A[i * TLD + kq + 4 * g] = acc[g];
         }
         __syncthreads();
-        trailing(T, J, nb, wave, lane);
+        if (J + 1 == nb) break;
+        if (wave == 0) {
+            double *D = T + tix(J + 1, J + 1) * TSZ;
+            const double *L = T + tix(J + 1, J) * TSZ;
+            tile_nt_acc(D, L, L, -1.0, lane);
+            __builtin_amdgcn_wave_barrier();
+            chol_inv16_p<TLD, true>(D, 0, U + tix(J + 1, J + 1) * TSZ, lds_l, lds_u, lane);
+        } else {   // trailing tiles of column J but the next diagonal one (tri_pair(0))
+            const int m = nb - 1 - J, ntr = m * (m + 1) / 2;
+            for (int tt = wave; tt < ntr; tt += nw - 1) {
+                int a, b;
+                tri_pair(tt, a, b);
+                const int I = J + 1 + a, K = J + 1 + b;
+                tile_nt_acc(T + tix(I, K) * TSZ, T + tix(I, J) * TSZ, T + tix(K, J) * TSZ, -1.0, lane);
+            }
+        }
         __syncthreads();
     }
 }
