@@ -1091,7 +1091,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     auto after_delta = [&]() {            // iteration it - 1 is complete
         h->cur ^= 1;
         if (h->trace_n < h->trace_cap) {                                  // dcfm_set_trace
-            launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4, s);
+            launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4 * TRACE_SLICES, s);
             h->trace_n += 1;
         }
     };
@@ -1251,7 +1251,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         if (!fused) {
             h->cur ^= 1;
             if (h->trace_n < h->trace_cap) {                              // dcfm_set_trace
-                launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4, s);
+                launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4 * TRACE_SLICES, s);
                 h->trace_n += 1;
             }
         }
@@ -1299,7 +1299,7 @@ int dcfm_set_trace(dcfm_handle *h, int64_t capacity) {
     h->trace = nullptr;
     h->trace_cap = h->trace_n = 0;
     if (capacity == 0) return DCFM_OK;
-    if (hipMalloc(&h->trace, (size_t)capacity * h->d.G * 4 * sizeof(double)) != hipSuccess)
+    if (hipMalloc(&h->trace, (size_t)capacity * h->d.G * TRACE_SLICES * 4 * sizeof(double)) != hipSuccess)
         return fail(h, DCFM_ERR_ALLOC, "set_trace: %lld rows", (long long)capacity);
     h->trace_cap = capacity;
     return DCFM_OK;
@@ -1311,13 +1311,17 @@ int dcfm_get_trace(dcfm_handle *h, double *out, int64_t *count) {
     HIPC(h, hipStreamSynchronize(h->stream));
     *count = h->trace_n;
     if (out && h->trace_n) {
-        const int G = h->d.G;
-        std::vector<double> part((size_t)h->trace_n * G * 4);
+        const int G = h->d.G, S = TRACE_SLICES;
+        std::vector<double> part((size_t)h->trace_n * G * S * 4);
         HIPC(h, hipMemcpy(part.data(), h->trace, part.size() * sizeof(double), hipMemcpyDeviceToHost));
         for (int64_t t = 0; t < h->trace_n; ++t)
             for (int q = 0; q < 4; ++q) {
                 double acc = 0.0;
-                for (int m = 0; m < G; ++m) acc += part[((size_t)t * G + m) * 4 + q];   // shard order
+                for (int m = 0; m < G; ++m) {                       // shard order, slices in row order
+                    double sm = 0.0;
+                    for (int sl = 0; sl < S; ++sl) sm += part[(((size_t)t * G + m) * S + sl) * 4 + q];
+                    acc += sm;
+                }
                 out[t * 4 + q] = acc;
             }
     }

@@ -125,6 +125,7 @@ struct Bufs {
 
 // k_wcol shard sum of A
 constexpr int XSUM_BLOCKS = 8;
+constexpr int TRACE_SLICES = 16;       // k_trace_part blocks per local shard (slices of its loading rows)
 // Bufs::sync: [0] the X operators (k_xdraw, several ranks), [1] spare, [2, 2 + 256) chunk counters of the A sum, [SYNC_ZM, SYNC_ZM + G) the
 // per-shard Z-operator counters (the fused W pass draws Z once its shard's operators are out)
 constexpr int SYNC_ZM = 2 + 256;

@@ -8,10 +8,11 @@
 //   q1 = sum_m sum_j omega_j                  tr(Omega)  -> q0 + q1 = tr(Sigma draw, dc:185)
 //   q2 = sum_m sum_j log ps_j                 residual precisions (dc:170)
 //   q3 = sum_m sum_h log tau_h^m              the shrinkage process (dc:163)
-// one block per local shard (fixed in-order sums: deterministic) writing the shard's
-// partials [G][4] of the iteration's trace row; dcfm_get_trace adds them in shard order
-// on the host (a second, one-block summing launch cost 7.6 us per iteration on the
-// chain).  Ranks that split one chain's shards add their rows (the host all-reduces).  Cost when enabled: one read of Lambda
+// TRACE_SLICES blocks per local shard, each a fixed slice of the shard's loading rows (fixed
+// in-order sums: deterministic), writing partials [G][TRACE_SLICES][4] of the iteration's trace
+// row; dcfm_get_trace adds them in (shard, slice) order on the host (a second, one-block summing
+// launch cost 7.6 us per iteration on the chain; one block per shard, 159 us at c4: a latency-
+// bound walk over the shard's 1.3 MB of Lambda).  Ranks that split one chain's shards add their rows (the host all-reduces).  Cost when enabled: one read of Lambda
 // (G x PP x KW doubles; 5 MB at c3), off by default.
 #include "dcfm_internal.h"
 
@@ -22,16 +23,18 @@ __global__ __launch_bounds__(256) void k_trace_part(const double *__restrict__ L
                                                     int P, int PP, int KW, int K, int shard0,
                                                     double *__restrict__ part) {
     __shared__ double red[4][256];
-    const int m = blockIdx.x, t = threadIdx.x;
+    const int sl = blockIdx.x, m = blockIdx.y, t = threadIdx.x;
+    const int j0 = (int)((long long)P * sl / TRACE_SLICES), j1 = (int)((long long)P * (sl + 1) / TRACE_SLICES);
     const double *L = Lam + (size_t)m * PP * KW;
     double q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
-    const int nl = P * KW;                       // rows j < P (padding columns k >= K hold zeros)
-    for (int e = t; e < nl; e += 256) { const double v = L[e]; q0 += v * v; }
-    for (int j = t; j < P; j += 256) {
+    // rows [j0, j1) (padding columns k >= K hold zeros)
+    for (int e = j0 * KW + t; e < j1 * KW; e += 256) { const double v = L[e]; q0 += v * v; }
+    for (int j = j0 + t; j < j1; j += 256) {
         q1 += omega[(size_t)m * PP + j];
         q2 += log(ps[(size_t)m * PP + j]);
     }
-    for (int hh = t; hh < K; hh += 256) q3 += log(tau[(size_t)(shard0 + m) * KW + hh]);
+    if (sl == 0)
+        for (int hh = t; hh < K; hh += 256) q3 += log(tau[(size_t)(shard0 + m) * KW + hh]);
     red[0][t] = q0; red[1][t] = q1; red[2][t] = q2; red[3][t] = q3;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
@@ -41,11 +44,11 @@ __global__ __launch_bounds__(256) void k_trace_part(const double *__restrict__ L
         }
         __syncthreads();
     }
-    if (t < 4) part[(size_t)m * 4 + t] = red[t][0];
+    if (t < 4) part[((size_t)m * TRACE_SLICES + sl) * 4 + t] = red[t][0];
 }
 
 void launch_trace(const Dims &d, const Bufs &b, const double *tau_cur, double *part, hipStream_t s) {
-    hipLaunchKernelGGL(k_trace_part, dim3(d.G), dim3(256), 0, s, b.Lam, b.omega, b.ps, tau_cur, d.P, d.PP, d.kp,
+    hipLaunchKernelGGL(k_trace_part, dim3(TRACE_SLICES, d.G), dim3(256), 0, s, b.Lam, b.omega, b.ps, tau_cur, d.P, d.PP, d.kp,
                        d.K, d.shard0, part);
 }
 
