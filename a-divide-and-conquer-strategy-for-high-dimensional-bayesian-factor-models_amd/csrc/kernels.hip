@@ -1820,11 +1820,12 @@ void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
     static_assert(LAM_GEN_THREADS == 256, "k_wcol blocks are 256 threads");
     LamGen lg = {};
     if (lamgen && b.ldraw) lg = lam_gen_plan(d, b.ldraw);
-    // W pass tiles: 64-row blocks while 128-row blocks would leave CUs idle
+    // W pass tiles: 64-row blocks up to one 128-row block per CU (the g = 32 share of c3: 256
+    // blocks; 64-row ones measured 2.8 % faster there, 128-row ones faster at c3's 512)
 #ifdef DCFM_WCOL_WMODE
     const int wmode = DCFM_WCOL_WMODE;   // dev A/B: forced block height
 #else
-    const int wmode = (d.NP / 128) * d.G < 256 ? 2 : 1;
+    const int wmode = (d.NP / 128) * d.G <= 256 ? 2 : 1;
 #endif
     const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / (64 * (3 - wmode))) * d.G : 0);
     if (nb + lg.b_total == 0) return;
@@ -1868,7 +1869,9 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &d
     const int ndel = (delta_in && d.kp == KP) ? cdiv(d.g, cp_waves<32>()) : 0;
     switch (d.kp) {
     case 32:
-        if (grid.x < 512)   // a few shards per rank: split the k columns by parity (k_cpass PS)
+        // a few shards per rank: split the k columns by parity (k_cpass PS) below 128 blocks
+        // (c3's g = 8 share, 88 blocks: +7 %; the g = 16 / 32 shares, 176 / 352: -4 / -2 %)
+        if (grid.x < 128)
             hipLaunchKernelGGL((k_cpass<32, true>), dim3(2 * grid.x + ndel), dim3(64 * cp_waves<32>()), 0, s, d, b.Y,
                                b.X, b.Z, b.C, b.E, dr, b.sall, da, ndel);
         else

@@ -168,9 +168,12 @@ __device__ inline double delta_G(const Dims &d, const DrawsDev &dr, int64_t iter
     return Rng(d.seed).gamma(shape, SITE_DELTA, (uint32_t)mg, 0, (uint32_t)h, (uint32_t)iter);
 }
 
-// eta = sqrt(rho) X + sqrt(1-rho) Z    (dc:81,133) — one definition for every use
+// eta = sqrt(rho) X + sqrt(1-rho) Z    (dc:81,133) — one definition for every use, with the
+// contraction spelled out: left to fp-contract, hipcc fused either product depending on the
+// surrounding code, so two instantiations of one kernel (k_cpass with and without the parity
+// split) gave different last bits
 __device__ __forceinline__ double eta_of(double sr, double s1r, double x, double z) {
-    return sr * x + s1r * z;
+    return fma(sr, x, s1r * z);
 }
 
 // ----------------------------------------------------------------------------

@@ -117,6 +117,9 @@ def test_loopback_ranks_match_oracle(dcfm, n, g, K, nobs, p):
     (4, 8, 1, 40, 9, 0),            # K = 1, g = 8 over 4 ranks (Q5 across ranks)
     (8, 8, 1, 30, 5, 0),            # K = 1, one shard per rank
     (8, 64, 4, 40, 40, 3),          # p = 2,560 over 8 ranks, 3-sample flushes
+    # n = 520: one rank takes 128-row W tiles and the unsplit C pass, each of 8 ranks 64-row tiles
+    # and the parity-split C pass (launch geometry follows the shards per rank; the bits may not)
+    (8, 64, 30, 520, 6, 0),
 ])
 def test_loopback_eight_ranks(dcfm, n, g, K, nobs, P, asm_batch):
     burnin, mcmc, thin = 1, 5, 2
