@@ -213,9 +213,6 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 #define DCFM_WP_RING 3
 #endif
 constexpr int WP_RING = DCFM_WP_RING;   // W pass register ring depth (chunks)
-#ifndef DCFM_WP_SPLIT
-#define DCFM_WP_SPLIT 1
-#endif
 // ============================================================================
 // k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA, Y pass 1
 // one wave = (shard m, 16 MT rows i = MT M-tiles) x 32 k (even / odd k tiles) of
@@ -258,7 +255,6 @@ __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restric
         l0[k] = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q) * KW);
         l1[k] = *reinterpret_cast<const d2 *>(L + (size_t)(j + 2 * q + 1) * KW);
     };
-#if DCFM_WP_SPLIT
     // the two k-steps of a chunk accumulate into separate sets (8 independent MFMA chains per wave
     // instead of 4), added at the end: W = (sum over even j) + (sum over odd j)
     d4 acc2[MT][2];
@@ -266,7 +262,6 @@ __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restric
     for (int a = 0; a < MT; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc2[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-#endif
     auto mma = [&](int k) {
         const double b00 = ww[k].x * l0[k].x, b01 = ww[k].x * l0[k].y;
         const double b10 = ww[k].y * l1[k].x, b11 = ww[k].y * l1[k].y;
@@ -276,21 +271,12 @@ __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restric
             acc[MT - 1][0] = mfma16x16x4(b00, y1[k].x, acc[MT - 1][0]);
             acc[MT - 1][1] = mfma16x16x4(b01, y1[k].x, acc[MT - 1][1]);
         }
-#if DCFM_WP_SPLIT
         acc2[0][0] = mfma16x16x4(b10, y0[k].y, acc2[0][0]);
         acc2[0][1] = mfma16x16x4(b11, y0[k].y, acc2[0][1]);
         if (MT == 2) {
             acc2[MT - 1][0] = mfma16x16x4(b10, y1[k].y, acc2[MT - 1][0]);
             acc2[MT - 1][1] = mfma16x16x4(b11, y1[k].y, acc2[MT - 1][1]);
         }
-#else
-        acc[0][0] = mfma16x16x4(b10, y0[k].y, acc[0][0]);
-        acc[0][1] = mfma16x16x4(b11, y0[k].y, acc[0][1]);
-        if (MT == 2) {
-            acc[MT - 1][0] = mfma16x16x4(b10, y1[k].y, acc[MT - 1][0]);
-            acc[MT - 1][1] = mfma16x16x4(b11, y1[k].y, acc[MT - 1][1]);
-        }
-#endif
     };
 #pragma unroll
     for (int k = 0; k < R - 1; ++k)
@@ -303,12 +289,10 @@ __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restric
             if (t + k < nch) mma(k);
         }
     }
-#if DCFM_WP_SPLIT
 #pragma unroll
     for (int a = 0; a < MT; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] += acc2[a][b];
-#endif
 }
 
 template <int KW, int MT = 2>
@@ -368,75 +352,9 @@ constexpr int ZROWS = 128, ZTHREADS = 512;     // rows and threads per k_zdraw b
 // +1] as one 16-byte pair); every element keeps its products and their order, so the values
 // are those of the unpermuted product.  Shared by k_zdraw (W from HBM) and k_wcol's
 // fused W pass (W' still in the W-pass accumulators), which therefore give the same bits.
-#ifndef DCFM_ZD_SPLIT
-#define DCFM_ZD_SPLIT 0
-#endif
 __device__ __forceinline__ void zdraw_rows(const Dims &d, const double (*Ms)[KP][KP + 1], const d2 (&wv)[4],
                                            const d2 (&xv)[4], const d2 (&ev)[4], double *__restrict__ Zr,
                                            double *__restrict__ Sr, bool live, int c, int q) {
-#if DCFM_ZD_SPLIT
-    // each product's k-steps split over two accumulators (even / odd t): 12 + 4 independent MFMA
-    // chains of half the length (the epilogue runs with no other wave's MFMAs to hide behind)
-    d4 zw[2][2], zx[2][2], ze[2][2], as[2][2];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) zw[mt][h] = zx[mt][h] = ze[mt][h] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        double mo[2][3][2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-#pragma unroll
-            for (int mat = 0; mat < 3; ++mat)
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) mo[e][mat][mt] = Ms[mat][16 * mt + c][8 * t + 2 * q + e];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const double we = e ? wv[t].y : wv[t].x, xe = e ? xv[t].y : xv[t].x;
-            const double ee = e ? ev[t].y : ev[t].x;
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                zw[mt][t & 1] = mfma16x16x4(mo[e][0][mt], we, zw[mt][t & 1]);
-                zx[mt][t & 1] = mfma16x16x4(mo[e][1][mt], xe, zx[mt][t & 1]);
-                ze[mt][t & 1] = mfma16x16x4(mo[e][2][mt], ee, ze[mt][t & 1]);
-            }
-        }
-    }
-    d4 az[2];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-        az[mt] = ((zw[mt][0] + zw[mt][1]) + (zx[mt][0] + zx[mt][1])) + (ze[mt][0] + ze[mt][1]);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) as[mt][0][g] = mt ? wv[g].y : wv[g].x;     // W[i][8g + 2q + mt]
-        as[mt][1] = d4{0.0, 0.0, 0.0, 0.0};
-    }
-    const int prow = 8 * (c >> 2) + 2 * (c & 3);
-#pragma unroll
-    for (int mt2 = 0; mt2 < 2; ++mt2)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int kk = 16 * mt2 + 4 * g + q;
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) as[mt][g & 1] = mfma16x16x4(Ms[3][prow + mt][kk], az[mt2][g], as[mt][g & 1]);
-        }
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) as[mt][0] = as[mt][0] + as[mt][1];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int k = 16 * mt + q + 4 * g;
-            if (live) Zr[k] = (k < d.K) ? az[mt][g] : 0.0;
-        }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        d2 v;
-        v.x = live ? as[0][0][g] : 0.0;
-        v.y = live ? as[1][0][g] : 0.0;
-        *reinterpret_cast<d2 *>(Sr + 8 * g + 2 * q) = v;
-    }
-#else
     d4 zw[2], zx[2], ze[2], as[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) zw[mt] = zx[mt] = ze[mt] = d4{0.0, 0.0, 0.0, 0.0};
@@ -492,7 +410,6 @@ __device__ __forceinline__ void zdraw_rows(const Dims &d, const double (*Ms)[KP]
         v.y = live ? as[1][g] : 0.0;
         *reinterpret_cast<d2 *>(Sr + 8 * g + 2 * q) = v;
     }
-#endif
 }
 // eps[i][kk], kk = 8t + 2q + e of the Z draw (dc:104 normrnd): the injected draw buffer, or
 // generated here — Philox pair 4t + q of (SITE_Z, shard, row i) = normals kk, kk + 1
