@@ -301,7 +301,7 @@ def main():
     def sync():
         smp.synchronize()
         if have_torch_gpu:
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(device)   # this rank's GPU (without it every rank opens a context on GPU 0)
 
     def barrier():
         if world > 1:
