@@ -39,11 +39,11 @@ K_COUNT = 15
 EXPORTS = (
     "dcfm_create", "dcfm_destroy", "dcfm_last_error", "dcfm_abi_version",
     "dcfm_comm_unique_id", "dcfm_comm_init", "dcfm_comm_init_loopback", "dcfm_set_data", "dcfm_set_state",
-    "dcfm_set_draws", "dcfm_run", "dcfm_synchronize", "dcfm_get_state", "dcfm_get_sigma",
+    "dcfm_set_draws", "dcfm_run", "dcfm_synchronize", "dcfm_get_state", "dcfm_get_state_raw", "dcfm_get_sigma",
     "dcfm_get_sigma_cols", "dcfm_sigma_block",
     "dcfm_saved_samples", "dcfm_sigma_error", "dcfm_set_profiling", "dcfm_set_profiling_mask", "dcfm_set_profiling_stride", "dcfm_get_kernel_stats",
     "dcfm_kernel_name",
-    "dcfm_rng_fill", "dcfm_set_data_raw", "dcfm_get_data", "dcfm_count_nonzero_columns",
+    "dcfm_rng_fill", "dcfm_rng_fill_rows", "dcfm_set_data_raw", "dcfm_get_data", "dcfm_count_nonzero_columns",
     "dcfm_set_trace", "dcfm_get_trace", "dcfm_init_state",
 )
 
@@ -107,6 +107,7 @@ def load_library(path: Path | None = None):
         "dcfm_run": (C.c_int, [vp, C.c_int64, C.c_int64]),
         "dcfm_synchronize": (C.c_int, [vp]),
         "dcfm_get_state": (C.c_int, [vp, C.POINTER(DcfmStateView)]),
+        "dcfm_get_state_raw": (C.c_int, [vp, C.POINTER(DcfmStateView)]),
         "dcfm_get_sigma": (C.c_int, [vp, _DP]),
         "dcfm_get_sigma_cols": (C.c_int, [vp, C.c_int64, C.c_int64, _DP]),
         "dcfm_sigma_block": (C.c_int, [vp, C.POINTER(C.c_int64)]),
@@ -119,6 +120,8 @@ def load_library(path: Path | None = None):
         "dcfm_kernel_name": (C.c_char_p, [C.c_int]),
         "dcfm_rng_fill": (C.c_int, [C.c_int, C.c_uint64, C.c_int, C.c_double, C.c_int32, C.c_int32,
                                     C.c_int64, C.c_int64, _DP]),
+        "dcfm_rng_fill_rows": (C.c_int, [C.c_int, C.c_uint64, C.c_int, C.c_double, C.c_int32, C.c_int32,
+                                         C.c_int64, C.c_int64, C.c_int32, C.c_int64, _DP]),
         "dcfm_set_data_raw": (C.c_int, [vp, _DP, C.c_int64, C.POINTER(C.c_int64), _DP, _DP]),
         "dcfm_get_data": (C.c_int, [vp, _DP]),
         "dcfm_set_trace": (C.c_int, [vp, C.c_int64]),

@@ -933,12 +933,13 @@ int dcfm_set_state(dcfm_handle *h, const dcfm_state_view *s) {
     return reset_numeric(h);
 }
 
-int dcfm_get_state(dcfm_handle *h, dcfm_state_view *o) {
+static int get_state(dcfm_handle *h, dcfm_state_view *o, bool checked) {
     if (!h || !o) return fail(h, DCFM_ERR_INVALID, "null argument");
     const Dims &d = h->d;
     HIPC(h, hipSetDevice(h->cfg.device));
     sync_all(h);
-    if (int rc = numeric_status(h)) return rc;
+    if (checked)
+        if (int rc = numeric_status(h)) return rc;
     std::vector<double> v;
     int rc;
     const size_t KP = d.kp;
@@ -977,6 +978,11 @@ int dcfm_get_state(dcfm_handle *h, dcfm_state_view *o) {
     if (o->tauh) { if ((rc = down(h, v, h->b.tau + h->cur * nkg, nkg))) return rc; k_from_dev(d, v, o->tauh); }
     return DCFM_OK;
 }
+
+int dcfm_get_state(dcfm_handle *h, dcfm_state_view *o) { return get_state(h, o, true); }
+
+// forensic read after DCFM_ERR_NUMERIC: the state as the device holds it, non-finite values included
+int dcfm_get_state_raw(dcfm_handle *h, dcfm_state_view *o) { return get_state(h, o, false); }
 
 int dcfm_set_draws(dcfm_handle *h, const dcfm_draws_view *dv, int64_t first_iter, int64_t n_iter) {
     if (!h || !dv || n_iter < 1) return fail(h, DCFM_ERR_INVALID, "bad argument");
@@ -1652,14 +1658,21 @@ int dcfm_get_kernel_stats(dcfm_handle *h, double ms[DCFM_K_COUNT], int64_t launc
 
 int dcfm_rng_fill(int device, uint64_t seed, int kind, double shape, int32_t site, int32_t shard,
                   int64_t iter, int64_t count, double *out) {
-    if (!out || count < 0 || (kind != 0 && kind != 1) || (kind == 1 && !(shape > 0.0)))
+    if (count < 0) return fail(nullptr, DCFM_ERR_INVALID, "rng_fill: bad argument");
+    return dcfm_rng_fill_rows(device, seed, kind, shape, site, shard, iter, (count + 31) / 32, 32, count, out);
+}
+
+int dcfm_rng_fill_rows(int device, uint64_t seed, int kind, double shape, int32_t site, int32_t shard,
+                       int64_t iter, int64_t rows, int32_t width, int64_t count, double *out) {
+    if (!out || count < 0 || rows < 0 || width < 1 || width > (1 << 23) || count > rows * (int64_t)width ||
+        (kind != 0 && kind != 1) || (kind == 1 && !(shape > 0.0)))
         return fail(nullptr, DCFM_ERR_INVALID, "rng_fill: bad argument");
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return fail(nullptr, DCFM_ERR_HIP, "hipSetDevice: %s", hipGetErrorString(e));
     void *q = nullptr;
     e = hipMalloc(&q, std::max<int64_t>(count, 1) * sizeof(double));
     if (e != hipSuccess) return fail(nullptr, DCFM_ERR_ALLOC, "hipMalloc: %s", hipGetErrorString(e));
-    launch_rng_fill(seed, kind, shape, site, shard, iter, count, static_cast<double *>(q), nullptr);
+    launch_rng_fill(seed, kind, shape, site, shard, iter, count, width, static_cast<double *>(q), nullptr);
     e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpy(out, q, count * sizeof(double), hipMemcpyDeviceToHost);
     (void)hipFree(q);

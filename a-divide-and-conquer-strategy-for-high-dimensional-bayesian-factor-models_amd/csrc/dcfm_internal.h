@@ -245,7 +245,7 @@ void launch_finite(const Dims &d, const Bufs &b, const double *tau_cur, int *fla
 // dst[i] = sum_k src[k * count + i] in slice order (loopback all-reduce)
 void launch_sum_slices(const double *src, int ns, size_t count, double *dst, hipStream_t s);
 void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,
-                     int64_t count, double *out, hipStream_t s);
+                     int64_t count, int width, double *out, hipStream_t s);
 
 // wide-factor kernels (kp = 64 / 128; kernels_wide.hip), dispatched from the launchers above
 namespace wide {

@@ -1692,13 +1692,14 @@ __global__ __launch_bounds__(256) void k_draws(Dims d, DrawsDev dr, int64_t iter
     draws_block<GAMMAS>(d, dr, iter, pl, blockIdx.x + (GAMMAS ? 0 : pl.b_gpsi));
 }
 
+// variate e at counter (site, shard, row = e / width, index = e % width, iter)
 __global__ __launch_bounds__(256) void k_rng_fill(uint64_t seed, int kind, double shape, int site,
-                                                  int shard, int64_t iter, int64_t count,
+                                                  int shard, int64_t iter, int64_t count, int width,
                                                   double *__restrict__ out) {
     const Rng rng(seed);
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < count;
          e += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t row = (uint32_t)(e / 32), k = (uint32_t)(e % 32);
+        const uint32_t row = (uint32_t)(e / width), k = (uint32_t)(e % width);
         out[e] = kind == 0 ? rng.normal(site, shard, row, k, (uint32_t)iter)
                            : rng.gamma(shape, site, shard, row, k, (uint32_t)iter);
     }
@@ -1914,10 +1915,10 @@ void launch_sum_slices(const double *src, int ns, size_t count, double *dst, hip
     hipLaunchKernelGGL(k_sum_slices, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, src, ns, count, dst);
 }
 void launch_rng_fill(uint64_t seed, int kind, double shape, int site, int shard, int64_t iter,
-                     int64_t count, double *out, hipStream_t s) {
+                     int64_t count, int width, double *out, hipStream_t s) {
     const int grid = (int)std::min<int64_t>((count + 255) / 256, 8192);
     hipLaunchKernelGGL(k_rng_fill, dim3(grid > 0 ? grid : 1), dim3(256), 0, s, seed, kind, shape, site,
-                       shard, iter, count, out);
+                       shard, iter, count, width, out);
 }
 
 }  // namespace dcfm

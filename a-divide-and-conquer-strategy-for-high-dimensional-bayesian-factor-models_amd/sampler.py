@@ -172,13 +172,16 @@ class Sampler:
         self._check(self.lib.dcfm_synchronize(self.h))
 
     # -- outputs -------------------------------------------------------------------
-    def get_state(self, fields=STATE_FIELDS) -> dict:
+    def get_state(self, fields=STATE_FIELDS, raw=False) -> dict:
+        """The state in MATLAB shapes.  ``raw``: skip the non-finite check (dcfm_get_state_raw), to
+        read the state after a run that ended in DCFM_ERR_NUMERIC."""
         shapes = self._shapes()
         out = {f: np.zeros(shapes[f], dtype=np.float64, order="F") for f in fields}
         view = _abi.DcfmStateView()
         for f, a in out.items():
             setattr(view, f, _ptr(a))
-        self._check(self.lib.dcfm_get_state(self.h, C.byref(view)))
+        fn = self.lib.dcfm_get_state_raw if raw else self.lib.dcfm_get_state
+        self._check(fn(self.h, C.byref(view)))
         return out
 
     def get_sigma(self):
@@ -276,12 +279,18 @@ def count_nonzero_columns(Y, device=0, return_ms=False):
     return (out, ms.value) if return_ms else out
 
 
-def rng_fill(kind: str, count: int, *, seed=0, shape=1.0, site=15, shard=0, iteration=0, device=0):
-    """On-device Philox variates exactly as the sweep draws them (diagnostic)."""
+def rng_fill(kind: str, count: int, *, seed=0, shape=1.0, site=15, shard=0, iteration=0, device=0, width=32):
+    """On-device Philox variates exactly as the sweep draws them (diagnostic): variate e at the
+    counter (site, shard, row = e // width, index = e % width, iteration)."""
     lib = _abi.load_library()
     out = np.zeros(int(count), dtype=np.float64)
     k = {"normal": 0, "gamma": 1}[kind]
-    rc = lib.dcfm_rng_fill(int(device), int(seed), k, float(shape), int(site), int(shard),
-                           int(iteration), int(count), _ptr(out))
+    if width == 32:
+        rc = lib.dcfm_rng_fill(int(device), int(seed), k, float(shape), int(site), int(shard),
+                               int(iteration), int(count), _ptr(out))
+    else:
+        rows = (int(count) + int(width) - 1) // int(width)
+        rc = lib.dcfm_rng_fill_rows(int(device), int(seed), k, float(shape), int(site), int(shard),
+                                    int(iteration), rows, int(width), int(count), _ptr(out))
     _abi.check(lib, None, rc)
     return out

@@ -172,6 +172,11 @@ int  dcfm_synchronize(dcfm_handle *h);
 
 /* ---- outputs ------------------------------------------------------------ */
 int  dcfm_get_state(dcfm_handle *h, dcfm_state_view *out);
+/* dcfm_get_state without the non-finite check: after a dcfm_run that ended in
+ * DCFM_ERR_NUMERIC, the state as the device holds it (NaN / Inf included), so a
+ * caller can see which stage of the failing iteration went non-finite.  The
+ * handle stays in its error state until set_state / init_state. */
+int  dcfm_get_state_raw(dcfm_handle *h, dcfm_state_view *out);
 /* Sigmaout, p x p (p = P*g), symmetric, in the reference's permuted and
  * standardised coordinates (dc:186-195, quirk Q7).  Collective when
  * nranks > 1: every rank must call it; rank 0 receives the matrix (out may be
@@ -247,6 +252,12 @@ const char *dcfm_kernel_name(int id);
  * Variate i uses counter (site, shard, row = i / 32, k = i % 32, iter). */
 int  dcfm_rng_fill(int device, uint64_t seed, int kind, double shape, int32_t site,
                    int32_t shard, int64_t iter, int64_t count, double *out);
+/* As dcfm_rng_fill with rows of `width` variates: out[e], e < count <= rows * width, uses
+ * counter (site, shard, row = e / width, k = e % width, iter) — e.g. width = K for the
+ * per-row variates of the K > 32 kernels (row j's normals / gammas at indices 0..K-1). */
+int  dcfm_rng_fill_rows(int device, uint64_t seed, int kind, double shape, int32_t site,
+                        int32_t shard, int64_t iter, int64_t rows, int32_t width, int64_t count,
+                        double *out);
 
 #ifdef __cplusplus
 }

@@ -21,7 +21,7 @@ It operates on the same :class:`oracle.dc_oracle.SamplerState` (MATLAB shapes);
 from __future__ import annotations
 
 import numpy as np
-from scipy.linalg.blas import dsyrk
+from scipy.linalg.blas import dsyrk, dtrsv
 
 from .dc_oracle import Hyper, SamplerState, matlab_cumprod_delta
 from .draws import IterDraws
@@ -101,11 +101,31 @@ def loading_systems(st: SamplerState, D: Data, d: IterDraws):
     return E, C, Q, b, L, z
 
 
+def _loading_solve(L, b, z):
+    """Lambda_j = L_j' \\ (L_j \\ b_j + z_j) (dc:143-144) for a stack of lower factors (g x P x K x K).
+    Small K: batched LAPACK solves; K >= 64 (c4): two triangular solves per row (BLAS dtrsv), which
+    skips the batched solver's O(K^3) factorisation of an already triangular matrix."""
+    g, P, K = b.shape
+    if K < 64:
+        v = np.linalg.solve(L, b[..., None])[..., 0]
+        return np.linalg.solve(np.swapaxes(L, -1, -2), (v + z)[..., None])[..., 0]
+    lam = np.empty_like(b)
+    for m in range(g):
+        for j in range(P):
+            Lj = L[m, j]
+            v = dtrsv(Lj, b[m, j], lower=1)
+            lam[m, j] = dtrsv(Lj, v + z[m, j], lower=1, trans=1)
+    return lam
+
+
 def residual_ss(D: Data, st: SamplerState, lam):
     """dc:169 as the reference writes it: sum_i (Yd - eta Lambda')_ij^2 per shard (g x P)."""
-    eta = np.moveaxis(st.eta, 2, 0)                                  # g x n x K
-    R = D.Ys - eta @ np.swapaxes(lam, 1, 2)                          # g x n x P
-    return np.einsum("mij,mij->mj", R, R)
+    g, n, P = D.Ys.shape
+    SS = np.empty((g, P))
+    for m in range(g):                                               # one BLAS GEMM per shard
+        R = D.Ys[m] - np.ascontiguousarray(st.eta[:, :, m]) @ lam[m].T   # n x P
+        SS[m] = np.einsum("ij,ij->j", R, R)
+    return SS
 
 
 def update_Lambda_psi_delta_ps(st: SamplerState, D: Data, hyper: Hyper, d: IterDraws, lam_given=None,
@@ -117,8 +137,7 @@ def update_Lambda_psi_delta_ps(st: SamplerState, D: Data, hyper: Hyper, d: IterD
     g, n, P = D.Ys.shape
     E, C, Q, b, L, z = loading_systems(st, D, d)
     if lam_given is None:
-        v = np.linalg.solve(L, b[..., None])[..., 0]
-        lam = np.linalg.solve(np.swapaxes(L, -1, -2), (v + z)[..., None])[..., 0]   # g x P x K
+        lam = _loading_solve(L, b, z)                                # g x P x K
     else:
         lam = np.ascontiguousarray(np.moveaxis(np.asarray(lam_given, dtype=np.float64), 2, 0))
     st.Lambda[...] = np.moveaxis(lam, 0, 2)

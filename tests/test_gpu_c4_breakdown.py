@@ -1,0 +1,124 @@
+"""BASELINE config c4 (p 10,000, n 2,000, K 100, g 8; "8 parallel chains"): the GPU chains' breakdown
+rate and posterior error against the oracle's (north_star check 2; divideconquer.m:142,180-196).
+
+At c4 some chains of the reference sampler make an X excursion that escalates until a loading system
+of dc:141 is no longer positive definite and chol (dc:142) raises -- MATLAB stops there; the library
+returns DCFM_ERR_NUMERIC (that it fails at the same iteration and stage as the oracle, from the same
+state and variates, is tests/test_gpu_excursion.py::test_breakdown_is_the_references[c4]).  Whether
+that happens to a chain is a property of the sampler, so the GPU chains must break down at the
+oracle's rate:
+
+* fixture tests/golden/c4_breakdown.json (make_c4_breakdown.py): R = 24 oracle chains (vectorised
+  oracle, dc:169's direct residual, NumPy draws) from one data set and initial state, BURNIN 250 +
+  MCMC 250 iterations, thin 5; each chain's breakdown iteration (or none) and, for the chains that
+  complete, the Frobenius / operator-norm error of the posterior-mean Sigmaout against the truth;
+* here M = 96 GPU chains from the same data and initial state with independent Philox draws.
+
+Checks (each at 1 %, two-sided):
+  breakdown fraction   Fisher's exact test of the 2 x 2 table (GPU / oracle x broke / completed);
+  posterior error      over the completed chains, for both norms: Welch's z of the mean error and the
+                       two-sample Kolmogorov-Smirnov test of the error distributions.
+Everything goes to gpurun_out/c4_breakdown_gpu.json (kept under profiles/ per round)."""
+import json
+import os
+import time
+from pathlib import Path
+
+import numpy as np
+import pytest
+from scipy import stats
+
+import oracle
+from helpers import make_case, state_dict
+
+pytestmark = pytest.mark.gpu
+
+FIXTURE = Path(__file__).resolve().parent / "golden" / "c4_breakdown.json"
+Z99 = 2.5758293035489004
+DCFM_ERR_NUMERIC = 5
+M_GPU = 96
+SEED0 = 7000
+CHUNK = 25
+
+
+def _welch(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    se = float(np.sqrt(np.var(a, ddof=1) / len(a) + np.var(b, ddof=1) / len(b)))
+    return float((np.mean(a) - np.mean(b)) / se), se
+
+
+@pytest.mark.timeout(900)
+def test_c4_breakdown_rate_and_error_match_oracle(dcfm, record_property):
+    if not FIXTURE.exists():
+        pytest.skip("tests/golden/c4_breakdown.json not generated (tests/golden/make_c4_breakdown.py)")
+    doc = json.loads(FIXTURE.read_text())
+    prm, reps = doc["params"], doc["replicates"]
+    n, p, g, K, rho = prm["n"], prm["p"], prm["g"], prm["K"], prm["rho"]
+    burnin, mcmc, thin = prm["burnin"], prm["mcmc"], prm["thin"]
+    N = burnin + mcmc
+    c = make_case(n, p, g, K, seed=doc["case_seed"], k0=prm["k0"], rho=rho, dense_truth=False)
+    Y, _, L0, sig2 = oracle.synth.make_data(n, p, k0=prm["k0"], factors=True, dense_truth=False)
+    assert np.array_equal(c["Y"], Y)
+    U, s = dcfm.truth_factors(L0, sig2, Y, c["keep"], c["init"].varind)
+    done = [r for r in reps if r["breakdown_iter"] is None]
+    truth_fro, truth_op = done[0]["truth_fro"], done[0]["truth_op"]
+    start = {f: v for f, v in state_dict(c["st"]).items() if f != "eta"}
+
+    out = Path(os.environ.get("DCFM_PARITY_OUT", "gpurun_out"))
+    out.mkdir(parents=True, exist_ok=True)
+    progress = out / "c4_breakdown_progress.txt"
+    gpu = []
+    t0 = time.time()
+    for k in range(M_GPU):
+        smp = dcfm.Sampler(n, c["P"], g, K, rho, burnin, mcmc, thin, seed=SEED0 + k)
+        rec = {"seed": SEED0 + k, "breakdown_by": None}
+        try:
+            smp.set_data(c["Yd"])
+            smp.set_state(start)
+            try:
+                for it in range(1, N + 1, CHUNK):
+                    smp.run(it, min(CHUNK, N + 1 - it))
+                    smp.synchronize()
+                e = smp.sigma_error(U, s, iters=120)
+            except dcfm.DcfmError as err:   # chol of dc:142 fails (test_breakdown_is_the_references[c4])
+                assert err.code == DCFM_ERR_NUMERIC, err
+                rec["breakdown_by"] = min(it + CHUNK - 1, N)
+            else:
+                assert abs(e["truth_fro"] / truth_fro - 1) < 1e-9          # same truth, same coordinates
+                rec.update(fro_rel=e["fro"] / truth_fro, op_rel=e["op"] / truth_op)
+        finally:
+            smp.close()
+        gpu.append(rec)
+        with progress.open("a") as f:
+            f.write(json.dumps({**rec, "t": round(time.time() - t0, 1)}) + "\n")
+
+    gb = sum(r["breakdown_by"] is not None for r in gpu)
+    ob = sum(r["breakdown_iter"] is not None for r in reps)
+    R = len(reps)
+    _, p_fisher = stats.fisher_exact([[gb, M_GPU - gb], [ob, R - ob]], alternative="two-sided")
+    summary = {"params": prm, "oracle_chains": R, "oracle_broke_down": ob,
+               "oracle_breakdown_iters": sorted(r["breakdown_iter"] for r in reps if r["breakdown_iter"]),
+               "oracle_stages": sorted({r["stage"] for r in reps if r["stage"]}),
+               "gpu_chains": M_GPU, "gpu_broke_down": gb,
+               "gpu_breakdown_by": sorted(r["breakdown_by"] for r in gpu if r["breakdown_by"]),
+               "fisher_p": float(p_fisher), "gpu_seeds": [SEED0, M_GPU], "chunk": CHUNK}
+    ok = {"breakdown_rate": p_fisher > 0.01}
+    gdone = [r for r in gpu if r["breakdown_by"] is None]
+    for key in ("fro_rel", "op_rel"):
+        a = [r[key] for r in done]
+        b = [r[key] for r in gdone]
+        z, se = _welch(a, b)
+        ks = float(stats.ks_2samp(a, b).pvalue)
+        summary[key] = {"oracle_mean": float(np.mean(a)), "gpu_mean": float(np.mean(b)), "z": z,
+                        "bar": Z99 * se, "bar_rel": Z99 * se / float(np.mean(a)), "ks_p": ks,
+                        "oracle": a, "gpu": b}
+        ok[key] = abs(z) < Z99 and ks > 0.01
+    summary["ok"] = ok
+    (out / "c4_breakdown_gpu.json").write_text(json.dumps(summary, indent=1) + "\n")
+    record_property("c4_breakdown", {k: summary[k] for k in ("oracle_broke_down", "gpu_broke_down", "fisher_p")})
+    print("C4_BREAKDOWN", json.dumps({"oracle": f"{ob}/{R}", "gpu": f"{gb}/{M_GPU}", "fisher_p": p_fisher,
+                                      **{k: {kk: summary[k][kk] for kk in ("z", "bar_rel", "ks_p")}
+                                         for k in ("fro_rel", "op_rel")}}))
+    for key, good in ok.items():
+        assert good, (key, {k: v for k, v in summary.items() if k not in ("fro_rel", "op_rel")}
+                      if key == "breakdown_rate" else summary[key])

@@ -31,8 +31,8 @@ reference's own algebra ends -- chol of a loading system that is no longer posit
 import numpy as np
 import pytest
 
-from helpers import (STATE_CMP, make_case, residual_rounding_bound, scaled_rel_err, stacked_draws, stagewise_errors,
-                     state_dict)
+from helpers import (STATE_CMP, make_case, rel_err, residual_rounding_bound, scaled_rel_err, stacked_draws,
+                     stagewise_errors, state_dict)
 
 pytestmark = pytest.mark.gpu
 
@@ -210,31 +210,56 @@ def _first_breakdown(dcfm, c, g, K, seed, iters=800, chunk=20):
     return good, it
 
 
-def test_breakdown_is_the_references(dcfm, record_property):
-    """Where an excursion escalates (c2 shape: Philox seeds 4, 11, 22 of 40; max|X| 1e7-1e8, cond(E_m)
-    ~1e18), the chain ends in DCFM_ERR_NUMERIC.  That is the reference's own end: from the GPU chain's
-    last finite state, with the failing iteration's variates (dcfm_rng_fill at the sweep's counters), the
-    faithful per-row oracle (MATLAB semantics: chol(Qlam,'lower') of dc:142 raises on a matrix that is not
-    positive definite) fails at the same iteration, and the library fed the same state and variates
-    (injected) fails there too.  The guard of the SS identity is not involved: the exact-residual mode
-    breaks down at the same point (tools/dev/nan_hunt.py)."""
+def _first_nonfinite_stage(st):
+    """The first stage of dc:97-177 whose output holds a NaN / Inf: "ZX" (Z, X, eta; dc:97-134),
+    "Lambda" (dc:137-145), "rest" (psi, delta / tau, ps / omega, Plam; dc:149-177), or None."""
+    for stage, fields in (("ZX", ("Z", "X", "eta")), ("Lambda", ("Lambda",)),
+                          ("rest", ("psi", "delta", "tauh", "ps", "omega", "Plam"))):
+        if not all(np.all(np.isfinite(st[f])) for f in fields):
+            return stage
+    return None
+
+
+# c2: Philox seeds 4, 11, 22 of 40 escalate (max|X| 1e7-1e8, cond(E_m) ~1e18) on the narrow path;
+# c4 (K = 100, wide path: k_lambda_w + k_resid_flagged): about a third of the seeds break down between
+# iterations 150 and 450 (tools/dev/excursion_probe.py: 10, 17, 18, 19, 21, 24, 26, 32, 34, 35 of 1-40)
+BREAKDOWN_CASES = {
+    "c2": dict(shape=(500, 5000, 8, 20), seeds=(11, 4, 22), iters=800),
+    "c4": dict(shape=(2000, 10000, 8, 100), seeds=(18, 24, 26, 10, 19, 21, 32, 34, 35, 17), iters=600),
+}
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("case", sorted(BREAKDOWN_CASES))
+def test_breakdown_is_the_references(dcfm, record_property, case):
+    """Where an excursion escalates, the chain ends in DCFM_ERR_NUMERIC.  That is the reference's own
+    end, at the same iteration and stage: from the GPU chain's last finite state, with the failing
+    iteration's variates (dcfm_rng_fill_rows at the sweep's counters),
+      * the faithful per-row oracle (MATLAB semantics: chol(Qlam,'lower') of dc:142 raises on a matrix
+        that is not positive definite) completes Z, X, eta (dc:97-134) and fails at the loading draw;
+      * the library fed the same state and variates (injected) fails there too: its state after the
+        failing iteration (dcfm_get_state_raw) has finite Z, X, eta equal to the oracle's at 1e-10 and the
+        first non-finite values in Lambda (dc:137-145), in rows whose loading system the oracle's chol
+        rejects.
+    The guard of the SS identity is not involved (it acts on ps / omega, after the loading draw)."""
     from numpy.linalg import LinAlgError
 
     from oracle import IterDraws
     from oracle import dc_oracle as F
     from test_gpu_generated_draws import _draws
 
-    c = make_case(500, 5000, 8, 20, seed=29, k0=10, dense_truth=False)
-    g, K = 8, 20
+    spec = BREAKDOWN_CASES[case]
+    n, p, g, K = spec["shape"]
+    c = make_case(n, p, g, K, seed=29, k0=10, dense_truth=False)
     found = None
-    for seed in (11, 4, 22):
-        found = _first_breakdown(dcfm, c, g, K, seed)
+    for seed in spec["seeds"]:
+        found = _first_breakdown(dcfm, c, g, K, seed, iters=spec["iters"])
         if found is not None:
             break
     assert found is not None, "no probed seed breaks down any more: re-probe (tools/dev/excursion_probe.py)"
     good, it = found
     dr = _draws(dcfm, seed, c["n"], c["P"], g, K, it, 1, dcfm.Hyper())
-    # the library, injected: the same failure
+    # the library, injected: the same failure; its state after the failing iteration
     smp = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], 10 ** 6, 0, 1, seed=seed, inject_draws=True)
     try:
         smp.set_data(c["Yd"])
@@ -244,13 +269,15 @@ def test_breakdown_is_the_references(dcfm, record_property):
             smp.run(it, 1)
             smp.get_state(("X",))
         assert ei.value.code == DCFM_ERR_NUMERIC
+        got = smp.get_state(raw=True)
     finally:
         smp.close()
+    gpu_stage = _first_nonfinite_stage(got)
     # the reference's algebra from the same state and variates
     st = _as_oracle({**good, "eta": np.zeros((c["n"], K, g))})
     F.update_eta(st, c["rho"])
     d = IterDraws(**{k: np.asarray(v)[..., 0] for k, v in dr.items()})
-    failed = None
+    failed, zx = None, None
     with np.errstate(all="ignore"):
         for name, fn in (("Z", lambda: F.update_Z(st, c["Yd"], c["rho"], d)),
                          ("X", lambda: F.update_X(st, c["Yd"], c["rho"], d)),
@@ -259,6 +286,8 @@ def test_breakdown_is_the_references(dcfm, record_property):
                          ("psi", lambda: F.update_psi(st, c["hyper"], d)),
                          ("delta", lambda: F.update_delta_tau(st, c["hyper"], d)),
                          ("ps", lambda: F.update_ps(st, c["Yd"], c["hyper"], d))):
+            if name == "Lambda":     # the oracle's state before the loading draw
+                zx = {f: getattr(st, f).copy() for f in ("Z", "X", "eta")}
             try:
                 fn()
             except LinAlgError:
@@ -267,8 +296,30 @@ def test_breakdown_is_the_references(dcfm, record_property):
             if not all(np.all(np.isfinite(v)) for v in st.as_dict().values()):
                 failed = name
                 break
-    record_property("breakdown", {"seed": seed, "iteration": it, "oracle_stage": failed,
-                                  "xmax_before": float(np.abs(good["X"]).max())})
-    print("BREAKDOWN", {"seed": seed, "iteration": it, "oracle_stage": failed,
-                        "xmax_before": float(np.abs(good["X"]).max())})
-    assert failed is not None, f"the oracle completes iteration {it} where the library fails"
+    info = {"case": case, "seed": seed, "iteration": it, "oracle_stage": failed, "gpu_stage": gpu_stage,
+            "xmax_before": float(np.abs(good["X"]).max())}
+    if zx is not None:
+        info.update({f"{f}_rel_err": rel_err(got[f], zx[f]) for f in ("Z", "X", "eta")})
+        # rows whose loading system Q_j = diag(Plam_j) + ps_j E_m (dc:141, from the oracle's eta) chol rejects,
+        # against the rows the library left non-finite
+        eta = np.moveaxis(zx["eta"], 2, 0)
+        bad_o, bad_g = set(), set()
+        lam_bad = ~np.all(np.isfinite(got["Lambda"]), axis=1)                  # P x g
+        for m in range(g):
+            E = eta[m].T @ eta[m]
+            for j in range(c["P"]):
+                Q = np.diag(good["Plam"][j, :, m]) + good["ps"][j, 0, m] * E
+                try:
+                    np.linalg.cholesky(Q)
+                except LinAlgError:
+                    bad_o.add((m, j))
+                if lam_bad[j, m]:
+                    bad_g.add((m, j))
+        info.update(oracle_rows_rejected=len(bad_o), gpu_rows_nonfinite=len(bad_g), rows_both=len(bad_o & bad_g))
+    record_property("breakdown", info)
+    print("BREAKDOWN", info)
+    assert failed == "Lambda", f"the oracle fails at {failed}, not at the loading draw (dc:142), iteration {it}"
+    assert gpu_stage == "Lambda", f"the library's first non-finite stage is {gpu_stage}, not the loading draw"
+    for f in ("Z", "X", "eta"):
+        assert info[f"{f}_rel_err"] < TOL, (f, info)
+    assert info["gpu_rows_nonfinite"] > 0 and info["rows_both"] > 0, info

@@ -4,8 +4,9 @@ delta gammas in the delta chain) and the wide kernels read k_draws buffers.  Eve
 addressed by its counter (site, shard, row, index, iteration; csrc/philox.h), so a chain in
 generated mode must be BITWISE the chain run in injected mode on the variates dcfm_rng_fill
 produces at those counters (row = i / 32, index = i % 32: a fill of rows x 32 is the row's
-first 32 indices, so K <= 32 here).  This pins the in-place draws to the counter scheme the
-RNG tests check statistically (tests/test_gpu_rng.py).
+first 32 indices; dcfm_rng_fill_rows with width K reaches the wide kernels' indices up to 127).
+This pins the in-place draws of both paths to the counter scheme the RNG tests check statistically
+(tests/test_gpu_rng.py).
 """
 import numpy as np
 import pytest
@@ -19,8 +20,11 @@ SITE_Z, SITE_X, SITE_LAMBDA, SITE_PSI, SITE_DELTA, SITE_PS = 1, 2, 3, 4, 5, 6
 
 def _rows(dcfm, kind, rows, seed, site, shard, it, K, shape=1.0):
     """rows x K block of variates at (site, shard, row, index < K, it)."""
-    x = dcfm.rng_fill(kind, rows * 32, seed=seed, shape=shape, site=site, shard=shard, iteration=it)
-    return x.reshape(rows, 32)[:, :K]
+    if K <= 32:
+        x = dcfm.rng_fill(kind, rows * 32, seed=seed, shape=shape, site=site, shard=shard, iteration=it)
+        return x.reshape(rows, 32)[:, :K]
+    x = dcfm.rng_fill(kind, rows * K, seed=seed, shape=shape, site=site, shard=shard, iteration=it, width=K)
+    return x.reshape(rows, K)
 
 
 def _draws(dcfm, seed, n, P, g, K, first, T, hyper):
@@ -34,13 +38,15 @@ def _draws(dcfm, seed, n, P, g, K, first, T, hyper):
             NL[:, :, m, t] = _rows(dcfm, "normal", P, seed, SITE_LAMBDA, m, it, K).T
             Gpsi[:, :, m, t] = _rows(dcfm, "gamma", P, seed, SITE_PSI, m, it, K, shape=hyper.df / 2 + 0.5)
             Gps[:, m, t] = _rows(dcfm, "gamma", P, seed, SITE_PS, m, it, 1, shape=hyper.as_ + n / 2)[:, 0]
-            for h in range(K):   # delta shapes depend on h (dc:158,163): row 0, index h
+        for m in range(g):       # delta: every shard (replicated chain); shapes depend on h (dc:158,163): row 0, index h
+            for h in range(K):
                 shp = hyper.ad1 + P * K / 2 if h == 0 else hyper.ad2 + P * (K - h) / 2
                 Gdelta[h, m, t] = _rows(dcfm, "gamma", 1, seed, SITE_DELTA, m, it, K, shape=shp)[0, h]
     return dict(NZ=NZ, NX=NX, NL=NL, Gpsi=Gpsi, Gdelta=Gdelta, Gps=Gps)
 
 
-@pytest.mark.parametrize("n,p,g,K", [(40, 60, 4, 5), (50, 96, 8, 30), (36, 64, 2, 32), (44, 80, 4, 20), (30, 52, 4, 13)])
+@pytest.mark.parametrize("n,p,g,K", [(40, 60, 4, 5), (50, 96, 8, 30), (36, 64, 2, 32), (44, 80, 4, 20), (30, 52, 4, 13),
+                                     (80, 96, 4, 40), (150, 128, 2, 100)])
 def test_generated_equals_injected_at_the_counters(dcfm, n, p, g, K):
     seed, burnin, mcmc, thin = 77, 1, 3, 1
     N = burnin + mcmc

@@ -1,22 +1,68 @@
 """CPU checks of the statistical-parity machinery (tests/stat_parity.py) on synthetic chain errors:
 the mode clustering finds well-separated modes and ignores a few outlying chains, and the
 mode-conditional z statistic accepts oracle values drawn from the GPU chains' own distribution and
-rejects a shift of a fraction of a percent."""
+rejects a shift of a fraction of a percent.
+
+The mode-conditional arm compares each oracle value with its mode's MEAN and SD.  Its first form
+(round 5, before the GPU run in gpurun_out/t_r5k.log) used the mode's median and 1.4826 MAD: on the
+c2 GPU chains that arm gave z = 4.44 and failed.  The GPU modes are skewed (skewness 1.6-2.2, mean -
+median ~0.23 sd, MAD-sd / sd ~0.5-0.7 in one mode each at c2 and c3; profiles/r05_f_c{2,3}_parity_gpu.json),
+and under parity o - median does not have expectation 0 there while o - mean does; the MAD also
+understates the spread.  test_skewed_modes_* below reproduces that on synthetic modes of the same
+shape: the median / MAD arm raises false alarms far above its nominal 1 %, the mean / SD arm holds
+~1 % and still catches a 0.6 % shift.  Round 6 found that the round-5 mean / SD arm still drew its
+modes from the gap split, which cuts a skewed mode's tail into minor clusters (mean biased toward the
+median, sd too small: 4.8 % false alarms on these modes); membership is now the oracle values' own rule
+applied to every GPU chain (stat_parity._mode_conditional), and an oracle value outside every mode
+counts against the check instead of being dropped."""
 import numpy as np
 
 import stat_parity as sp
 
+MODES = (0.486, 0.517)
+SD = 0.001
 
-def _rows(rng, R=6, M=16, shift=0.0, modes=(0.486, 0.517), sd=0.001, outliers=1):
+
+def _dev(rng, size, skew):
+    """Within-mode deviations of sd SD: Gaussian, or (skew) a centred log-normal (sigma 0.6: skewness
+    ~2.3, as the skewed GPU modes)."""
+    if not skew:
+        return SD * rng.standard_normal(size)
+    s = 0.6
+    x = rng.lognormal(0.0, s, size)
+    m, v = np.exp(s * s / 2), (np.exp(s * s) - 1) * np.exp(s * s)
+    return SD * (x - m) / np.sqrt(v)
+
+
+def _rows(rng, R=6, M=16, shift=0.0, modes=MODES, outliers=1, skew=False, oracle_outside=0):
     rows = []
     for r in range(R):
         pick = rng.random(M) < 0.5
-        g = np.where(pick, modes[1], modes[0]) + sd * rng.standard_normal(M)
+        g = np.where(pick, modes[1], modes[0]) + _dev(rng, M, skew)
         if r < outliers:
             g[0] = 0.57                                    # a chain that spent time in an excursion
-        o = (modes[1] if rng.random() < 0.5 else modes[0]) + sd * rng.standard_normal() + shift
+        o = (modes[1] if rng.random() < 0.5 else modes[0]) + _dev(rng, 1, skew)[0] + shift
+        if r < oracle_outside:
+            o = 0.60                                       # an oracle value outside every major mode
         rows.append({"gpu_fro_rel": g.tolist(), "oracle_fro_rel": float(o)})
     return rows
+
+
+def _median_mad_z(rows, key="fro_rel"):
+    """The round-5 first form of the mode-conditional arm: o - median over 1.4826 MAD (superseded)."""
+    g = np.concatenate([np.asarray(r[f"gpu_{key}"]) for r in rows])
+    parts, _ = sp._clusters(g)
+    major = [v for lo, hi, v in parts if len(v) >= 0.1 * len(g) and len(v) >= 5]
+    med = np.array([np.median(v) for v in major])
+    mad = np.array([1.4826 * np.median(np.abs(v - np.median(v))) for v in major])
+    ns = np.array([len(v) for v in major])
+    d, var = [], []
+    for r in rows:
+        ov = r[f"oracle_{key}"]
+        k = int(np.argmin(np.abs(ov - med)))
+        d.append(ov - med[k])
+        var.append(mad[k] ** 2 * (1 + 1 / ns[k]))
+    return float(np.sum(d) / np.sqrt(np.sum(var)))
 
 
 def test_clusters_find_the_modes():
@@ -35,6 +81,37 @@ def test_mode_conditional_accepts_parity_and_rejects_a_shift():
     assert np.mean(np.abs(zs) < sp.Z99) > 0.95                 # ~1 % false alarms under parity
     shifted = [sp._mode_conditional(_rows(rng, shift=0.003), "fro_rel")["z"] for _ in range(50)]
     assert np.mean(np.abs(shifted) > sp.Z99) > 0.9             # a 0.6 % shift is caught
+
+
+def test_skewed_modes_mean_arm_holds_its_false_alarm_rate():
+    """Skewed modes, parity (R = 8 oracle values, 16 GPU chains each, as c2): the mean / SD arm's
+    false-alarm rate stays near 1 %; the median / MAD arm's does not."""
+    rng = np.random.default_rng(5)
+    trials = [_rows(rng, R=8, skew=True) for _ in range(400)]
+    new = np.array([not sp._mode_conditional(t, "fro_rel")["ok"] for t in trials])
+    old = np.array([abs(_median_mad_z(t)) > sp.Z99 for t in trials])
+    assert new.mean() < 0.03, new.mean()
+    assert old.mean() > 0.08, old.mean()                    # ~15 %: many times the nominal 1 %
+
+
+def test_skewed_modes_mean_arm_catches_a_shift():
+    rng = np.random.default_rng(6)
+    hit = [not sp._mode_conditional(_rows(rng, R=8, skew=True, shift=0.003), "fro_rel")["ok"] for _ in range(100)]
+    assert np.mean(hit) > 0.9                                  # a 0.6 % shift is caught
+
+
+def test_oracle_values_outside_the_modes_count():
+    """An oracle value outside every major mode is counted, not dropped: one of 8 is consistent with the
+    GPU chains' own outside rate (a few of 128), three of 8 are not, and fewer than 3 values inside the
+    modes fail the check."""
+    rng = np.random.default_rng(7)
+    one = sp._mode_conditional(_rows(rng, R=8, outliers=4, oracle_outside=1), "fro_rel")
+    assert one["oracle_outside"] == 1 and one["oracle_outside_values"] == [0.60] and one["n_used"] == 7
+    assert one["p_outside"] > 0.01
+    three = sp._mode_conditional(_rows(rng, R=8, outliers=4, oracle_outside=3), "fro_rel")
+    assert three["oracle_outside"] == 3 and three["p_outside"] < 0.01 and not three["ok"]
+    few = sp._mode_conditional(_rows(rng, R=4, outliers=4, oracle_outside=2), "fro_rel")
+    assert few["n_used"] == 2 and not few["ok"]
 
 
 def test_unimodal_errors_have_no_modes():
