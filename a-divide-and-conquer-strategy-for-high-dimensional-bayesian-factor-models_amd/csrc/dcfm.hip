@@ -97,7 +97,7 @@ struct dcfm_handle {
     bool used_pending[2] = {false, false};   // e_used[slot] recorded after the slot's last consumer
     int DB = 1;                              // iterations per draws batch
     size_t draw_iter_sz[6] = {};             // per-iteration doubles of NZ, NX, NL, Gpsi, Gdelta, Gps
-    // per-iteration chain trace (dcfm_set_trace): per-shard partials [trace_cap][G][4]
+    // per-iteration chain trace (dcfm_set_trace): [scratch | rows [trace_cap][G][4]] (trace.hip)
     double *trace = nullptr;
     int64_t trace_cap = 0, trace_n = 0;
     bool prof = false;
@@ -310,6 +310,11 @@ static void sync_all(dcfm_handle *h) {
     if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->sdraw) (void)hipStreamSynchronize(h->sdraw);
     if (h->sasm) (void)hipStreamSynchronize(h->sasm);
+}
+
+// row t of the chain trace ([G][4] shard sums after the scratch, trace.hip)
+static double *trace_row(dcfm_handle *h, int64_t t) {
+    return h->trace + trace_scratch_doubles(h->d.G) + (size_t)t * h->d.G * 4;
 }
 
 // DCFM_ERR_NUMERIC once the sentinel of a finished dcfm_run has seen a non-finite state
@@ -543,9 +548,10 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         b.rflag = reinterpret_cast<int *>(rf);
     }
     ALLOC(b.xpart, (size_t)G * KP * KP);  // k_wcol: xsum_blocks(G) <= G chunk sums
+    ALLOC(b.xmp, (size_t)xsum_blocks((int)G) * NP * KP);
     {
         double *tk = nullptr;
-        ALLOC(tk, 1);
+        ALLOC(tk, (wcol_tickets((int)NP, (int)G) + 1) / 2);   // zeroed
         b.ticket = reinterpret_cast<unsigned *>(tk);
         double *sy = nullptr;
         ALLOC(sy, SYNC_ZM + G);           // zeroed: the hand-off counters start at 0 (<= 255 chunks, G shards)
@@ -1093,11 +1099,12 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     // draw.  k_wcol also draws the loading-row variates of t (generated chain).  The last
     // iteration's chain runs after the loop (k_delta).
     const bool wc = fused && !d.coll;
+    const bool xtail = fused && wcol_xtail(d);   // k_wcol sums the X message (and one rank draws X)
     bool delta_pending = false;           // k_lambda of it - 1 ran, its delta chain not yet queued
     auto after_delta = [&]() {            // iteration it - 1 is complete
         h->cur ^= 1;
         if (h->trace_n < h->trace_cap) {                                  // dcfm_set_trace
-            launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4 * TRACE_SLICES, s);
+            launch_trace(d, b, b.tau + h->cur * nkg, h->trace, trace_row(h, h->trace_n), s);
             h->trace_n += 1;
         }
     };
@@ -1169,7 +1176,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
                 h->wc_ops += 1;
                 launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s, lamgen);
             }
-            { KTimer t(h, DCFM_K_XRED, s); launch_xred(d, b, s); }
+            if (!xtail) { KTimer t(h, DCFM_K_XRED, s); launch_xred(d, b, s); }   // split tiles: in k_wcol
             KTimer t(h, DCFM_K_COMM, s);
             if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)) return rc;
         } else {
@@ -1199,7 +1206,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             KTimer t(h, DCFM_K_XDRAW, s);
             h->xm_ops += 1;
             launch_xdraw_mr(d, b, dr, it, h->xm_ops, s);
-        } else {
+        } else if (!(wc && xtail)) {   // (split W tiles, one rank: X is drawn in k_wcol)
             KTimer t(h, DCFM_K_XDRAW, s);
             launch_xdraw(d, b, dr, it, s, wc);
         }
@@ -1257,7 +1264,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
         if (!fused) {
             h->cur ^= 1;
             if (h->trace_n < h->trace_cap) {                              // dcfm_set_trace
-                launch_trace(d, b, b.tau + h->cur * nkg, h->trace + h->trace_n * d.G * 4 * TRACE_SLICES, s);
+                launch_trace(d, b, b.tau + h->cur * nkg, h->trace, trace_row(h, h->trace_n), s);
                 h->trace_n += 1;
             }
         }
@@ -1305,8 +1312,10 @@ int dcfm_set_trace(dcfm_handle *h, int64_t capacity) {
     h->trace = nullptr;
     h->trace_cap = h->trace_n = 0;
     if (capacity == 0) return DCFM_OK;
-    if (hipMalloc(&h->trace, (size_t)capacity * h->d.G * TRACE_SLICES * 4 * sizeof(double)) != hipSuccess)
+    const size_t nd = trace_scratch_doubles(h->d.G) + (size_t)capacity * h->d.G * 4;
+    if (hipMalloc(&h->trace, nd * sizeof(double)) != hipSuccess)
         return fail(h, DCFM_ERR_ALLOC, "set_trace: %lld rows", (long long)capacity);
+    HIPC(h, hipMemset(h->trace, 0, trace_scratch_doubles(h->d.G) * sizeof(double)));   // tickets start at 0
     h->trace_cap = capacity;
     return DCFM_OK;
 }
@@ -1317,17 +1326,13 @@ int dcfm_get_trace(dcfm_handle *h, double *out, int64_t *count) {
     HIPC(h, hipStreamSynchronize(h->stream));
     *count = h->trace_n;
     if (out && h->trace_n) {
-        const int G = h->d.G, S = TRACE_SLICES;
-        std::vector<double> part((size_t)h->trace_n * G * S * 4);
-        HIPC(h, hipMemcpy(part.data(), h->trace, part.size() * sizeof(double), hipMemcpyDeviceToHost));
+        const int G = h->d.G;
+        std::vector<double> rows((size_t)h->trace_n * G * 4);
+        HIPC(h, hipMemcpy(rows.data(), trace_row(h, 0), rows.size() * sizeof(double), hipMemcpyDeviceToHost));
         for (int64_t t = 0; t < h->trace_n; ++t)
             for (int q = 0; q < 4; ++q) {
                 double acc = 0.0;
-                for (int m = 0; m < G; ++m) {                       // shard order, slices in row order
-                    double sm = 0.0;
-                    for (int sl = 0; sl < S; ++sl) sm += part[(((size_t)t * G + m) * S + sl) * 4 + q];
-                    acc += sm;
-                }
+                for (int m = 0; m < G; ++m) acc += rows[((size_t)t * G + m) * 4 + q];   // shard order
                 out[t * 4 + q] = acc;
             }
     }

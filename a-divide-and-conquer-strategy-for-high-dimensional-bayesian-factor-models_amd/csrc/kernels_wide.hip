@@ -112,6 +112,7 @@ __global__ __launch_bounds__(64 * GRAM_WAVES) void k_gram(Dims d, const double *
 #endif
 constexpr int TILE_THREADS = DCFM_TILE_THREADS;   // k_prep / k_xchol: 16 waves share the tile steps (c4: 4 waves
                                                   // 99 / 77 us, 16 with the look-ahead 40 / 48 us)
+static_assert(TILE_THREADS >= 128 && TILE_THREADS % 64 == 0, "potrf_inv's look-ahead needs at least two whole waves");
 template <int KW>
 __global__ __launch_bounds__(TILE_THREADS) void k_prep(Dims d, const double *__restrict__ A, double *__restrict__ ZM) {
     constexpr int NB = KW / tile::TS, NT = tile::ntiles(NB);

@@ -56,6 +56,8 @@ __device__ __forceinline__ void tile_nt_acc(double *C, const double *A, const do
 __device__ __forceinline__ void potrf_inv(double *T, double *U, int nb, double *lds_l, double *lds_u) {
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, nw = blockDim.x >> 6;
     const int i = lane & 15, kq = lane >> 4;
+    // the look-ahead gives the trailing update to waves 1 .. nw - 1: every caller launches at least
+    // two waves (kernels_wide.hip static_asserts TILE_THREADS >= 128)
     if (wave == 0) chol_inv16_p<TLD, true>(T, 0, U, lds_l, lds_u, lane);
     __syncthreads();
 #pragma unroll 1
@@ -76,7 +78,8 @@ __device__ __forceinline__ void potrf_inv(double *T, double *U, int nb, double *
             double *D = T + tix(J + 1, J + 1) * TSZ;
             const double *L = T + tix(J + 1, J) * TSZ;
             tile_nt_acc(D, L, L, -1.0, lane);
-            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_wave_barrier();              // D's LDS stores before chol_inv16_p's reads
+            asm volatile("" ::: "memory");
             chol_inv16_p<TLD, true>(D, 0, U + tix(J + 1, J + 1) * TSZ, lds_l, lds_u, lane);
         } else {   // trailing tiles of column J but the next diagonal one (tri_pair(0))
             const int m = nb - 1 - J, ntr = m * (m + 1) / 2;

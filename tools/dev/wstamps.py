@@ -37,8 +37,10 @@ if G > 8:
         chunk *= 2
     nxs = G // chunk
 NP = (n + 127) // 128 * 128
-wmode = 2 if (NP // 128) * G < 256 else 1
-nw = NP // (64 * (3 - wmode)) * G
+import os
+wmode = int(os.environ.get("WMODE", "0")) or (3 if (NP // 32) * G >= 1024 else 4)   # kernels.hip wcol_mode
+rows = {1: 128, 2: 64, 3: 32, 4: 16}[wmode]
+nw = NP // rows * G
 w0 = 2 * G + nxs
 
 
@@ -49,11 +51,14 @@ def line(name, lo, hi, *cols):
     print(out)
 
 
-print(f"blocks with stamps: {nb}  (G {G}, A-sum blocks {nxs}, W tiles {nw} of {64 * (3 - wmode)} rows)")
+print(f"blocks with stamps: {nb}  (G {G}, A-sum blocks {nxs}, W tiles {nw} of {rows} rows, mode {wmode})")
 line("OPS", 0, G, ("start", st), ("A out", s2), ("U out", s3), ("end", en))
 line("colsum", G, 2 * G, ("start", st), ("end", en))
 line("A-sum", 2 * G, w0, ("start", st), ("end", en))
 line("W tiles", w0, w0 + nw, ("start", st), ("pass", s2), ("ops in", s3), ("staged", s4), ("draw 1", s5), ("end", en))
+tail = en[w0:w0 + nw] - s5[w0:w0 + nw]
+print(f"W tiles end - draw: med {np.median(tail):.2f} max {tail.max():.2f} us; end percentiles 50/90/99/100: "
+      + " ".join(f"{np.percentile(en[w0:w0 + nw], q):.2f}" for q in (50, 90, 99, 100)))
 if nb > w0 + nw:
     line("lam gen", w0 + nw, nb, ("start", st), ("end", en))
 clk = (b[:, 7] - b[:, 6]) / np.maximum(b[:, 1] - b[:, 0], 1) * 100e6 / 1e9   # GHz
