@@ -548,10 +548,9 @@ int dcfm_create(const dcfm_config *cfg, dcfm_handle **out) {
         b.rflag = reinterpret_cast<int *>(rf);
     }
     ALLOC(b.xpart, (size_t)G * KP * KP);  // k_wcol: xsum_blocks(G) <= G chunk sums
-    ALLOC(b.xmp, (size_t)xsum_blocks((int)G) * NP * KP);
     {
         double *tk = nullptr;
-        ALLOC(tk, (wcol_tickets((int)NP, (int)G) + 1) / 2);   // zeroed
+        ALLOC(tk, 1);
         b.ticket = reinterpret_cast<unsigned *>(tk);
         double *sy = nullptr;
         ALLOC(sy, SYNC_ZM + G);           // zeroed: the hand-off counters start at 0 (<= 255 chunks, G shards)
@@ -1099,7 +1098,6 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
     // draw.  k_wcol also draws the loading-row variates of t (generated chain).  The last
     // iteration's chain runs after the loop (k_delta).
     const bool wc = fused && !d.coll;
-    const bool xtail = fused && wcol_xtail(d);   // k_wcol sums the X message (and one rank draws X)
     bool delta_pending = false;           // k_lambda of it - 1 ran, its delta chain not yet queued
     auto after_delta = [&]() {            // iteration it - 1 is complete
         h->cur ^= 1;
@@ -1176,7 +1174,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
                 h->wc_ops += 1;
                 launch_wcol(d, b, dr, it, true, delta_pending, true, h->wc_ops, s, lamgen);
             }
-            if (!xtail) { KTimer t(h, DCFM_K_XRED, s); launch_xred(d, b, s); }   // split tiles: in k_wcol
+            { KTimer t(h, DCFM_K_XRED, s); launch_xred(d, b, s); }
             KTimer t(h, DCFM_K_COMM, s);
             if (int rc = coll_allgather(h, CH_MAIN, b.sloc, b.msg_all, (size_t)d.xstride, s)) return rc;
         } else {
@@ -1206,7 +1204,7 @@ int dcfm_run(dcfm_handle *h, int64_t first_iter, int64_t n_iter) {
             KTimer t(h, DCFM_K_XDRAW, s);
             h->xm_ops += 1;
             launch_xdraw_mr(d, b, dr, it, h->xm_ops, s);
-        } else if (!(wc && xtail)) {   // (split W tiles, one rank: X is drawn in k_wcol)
+        } else {
             KTimer t(h, DCFM_K_XDRAW, s);
             launch_xdraw(d, b, dr, it, s, wc);
         }

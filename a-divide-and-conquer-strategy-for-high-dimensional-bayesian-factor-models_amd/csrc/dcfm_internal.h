@@ -110,9 +110,7 @@ struct Bufs {
     double *Lb[2], *wsum[2], *Sigma;
     double *xa, *xa_all, *XM;          // per-rank sum of A, gathered sums, X-draw operators
     double *xpart;                     // k_wcol chunk sums of A (xsum_blocks(G) x KP x KP)
-    double *xmp;                       // k_wcol X-message chunk sums (xsum_blocks(G) x NP x KP; split W tiles)
-    unsigned *ticket;                  // k_wcol last-arrival tickets (0 between launches): [0] the A sum,
-                                       // [2, ..) the split W tiles' message tails (wcol_tickets)
+    unsigned *ticket;                  // k_wcol last-arrival ticket (0 between launches)
     unsigned long long *sync;          // hand-off counters (monotonic): [0] = k_xdraw XM out (several ranks),
                                        // [2 + chunk] = k_wcol A_m of the chunk out,
                                        // [SYNC_ZM + m] = k_wcol Z operators of shard m out
@@ -141,14 +139,6 @@ __host__ __device__ inline int xsum_blocks(int G) {
     while (G / chunk > XSUM_BLOCKS && (G / chunk) % 2 == 0) chunk *= 2;
     return G / chunk;
 }
-
-// k_wcol W-tile layouts (wpass mode): 1 / 2 = 128- / 64-row tiles, 3 / 4 = split 32- / 16-row tiles
-// whose message tail sums the X message in the launch (kernels.hip wsplit_tile)
-__host__ __device__ constexpr int wcol_rows(int mode) { return mode == 1 ? 128 : mode == 2 ? 64 : mode == 3 ? 32 : 16; }
-int wcol_mode(const Dims &d);                 // the layout launch_wcol uses for this share
-bool wcol_xtail(const Dims &d);               // its tiles sum the X message (k_xdraw / k_xred not launched)
-// tickets of the split tiles' message tails: [NP/16][xsum_blocks(G)] chunk tickets + [NP/16] row blocks
-inline size_t wcol_tickets(int NP, int G) { return 2 + (size_t)(NP / 16) * (size_t)(G + 1); }
 
 // Sigma block-sharding helpers (host + device)
 __host__ __device__ inline long long tri(long long t) { return t * (t + 1) / 2; }

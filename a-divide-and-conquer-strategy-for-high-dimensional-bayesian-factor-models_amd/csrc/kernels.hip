@@ -231,21 +231,21 @@ constexpr int WP_RING = DCFM_WP_RING;   // W pass register ring depth (chunks)
 // Register ring of R chunks: chunk t + R - 1 is requested while chunk t multiplies, so R - 1
 // chunks are in flight behind the MFMAs.  pre() runs once the first R - 1 chunks' loads are
 // issued (VALU work hidden behind their latency).
-// Chunks [c0, c0 + nch) of the reduction (c0 = 0, nch = PP / 8: all of it).
 template <int KW, int MT, int R = WP_RING, class Pre>
 __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restrict__ Y, const double *__restrict__ Lam,
-                                          const double *__restrict__ omega, int m, int i0, int kt, int c0, int nch,
-                                          d4 (&acc)[MT][2], Pre &&pre) {
+                                          const double *__restrict__ omega, int m, int i0, int kt, d4 (&acc)[MT][2],
+                                          Pre &&pre) {
     const int lane = threadIdx.x & 63;
     const int r = lane & 15, q = lane >> 4;
-    const double *Y0 = Y + ((size_t)m * d.NP + i0 + r) * d.PP + 8 * c0 + 2 * q;
+    const double *Y0 = Y + ((size_t)m * d.NP + i0 + r) * d.PP + 2 * q;
     const double *Y1 = Y0 + (size_t)16 * (MT - 1) * d.PP;
-    const double *L = Lam + ((size_t)m * d.PP + 8 * c0) * KW + 32 * kt + 2 * r;
-    const double *wp = omega + (size_t)m * d.PP + 8 * c0 + 2 * q;
+    const double *L = Lam + (size_t)m * d.PP * KW + 32 * kt + 2 * r;
+    const double *wp = omega + (size_t)m * d.PP + 2 * q;
 #pragma unroll
     for (int a = 0; a < MT; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    const int nch = d.PP >> 3;
     d2 y0[R], y1[R], ww[R], l0[R], l1[R];
     auto load = [&](int t, int k) {
         const int j = 8 * t;
@@ -305,7 +305,7 @@ __device__ __forceinline__ void wpass_tile(const Dims &d, const double *__restri
     const int i0 = rb * 64 * MT + wave * 16 * MT;
     const int r = lane & 15, q = lane >> 4;
     d4 acc[MT][2];
-    wpass_acc<KW, MT>(d, Y, Lam, omega, m, i0, kt, 0, d.PP >> 3, acc, [] {});
+    wpass_acc<KW, MT>(d, Y, Lam, omega, m, i0, kt, acc, [] {});
     // acc[a][tb][g] = W[i0 + 16a + r][32 kt + 8g + 2q + tb]: one 16-byte pair per (a, g)
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
@@ -352,8 +352,6 @@ constexpr int ZROWS = 128, ZTHREADS = 512;     // rows and threads per k_zdraw b
 // +1] as one 16-byte pair); every element keeps its products and their order, so the values
 // are those of the unpermuted product.  Shared by k_zdraw (W from HBM) and k_wcol's
 // fused W pass (W' still in the W-pass accumulators), which therefore give the same bits.
-// PUB: the X message rows go out as agent-scope stores (summed by other blocks of the launch)
-template <bool PUB = false>
 __device__ __forceinline__ void zdraw_rows(const Dims &d, const double (*Ms)[KP][KP + 1], const d2 (&wv)[4],
                                            const d2 (&xv)[4], const d2 (&ev)[4], double *__restrict__ Zr,
                                            double *__restrict__ Sr, bool live, int c, int q) {
@@ -410,12 +408,7 @@ __device__ __forceinline__ void zdraw_rows(const Dims &d, const double (*Ms)[KP]
         d2 v;
         v.x = live ? as[0][g] : 0.0;
         v.y = live ? as[1][g] : 0.0;
-        if (PUB) {
-            st_agent(Sr + 8 * g + 2 * q, v.x);
-            st_agent(Sr + 8 * g + 2 * q + 1, v.y);
-        } else {
-            *reinterpret_cast<d2 *>(Sr + 8 * g + 2 * q) = v;
-        }
+        *reinterpret_cast<d2 *>(Sr + 8 * g + 2 * q) = v;
     }
 }
 // eps[i][kk], kk = 8t + 2q + e of the Z draw (dc:104 normrnd): the injected draw buffer, or
@@ -746,59 +739,6 @@ struct DeltaArgs {
 // blocks of XD_ROWS rows (the MFMA's other columns padding), every lane summing one part of a
 // source chunk: the shard-message sums are bound by the memory parallelism of the CUs that
 // issue them (phase stamps: 9 of 14 us with 63 blocks of 16 rows at c3).
-// eps of dc:126 for X row i, in the X draw's lane map (lane (c, q): columns 8t + 2q, +1): the
-// injected draw buffer, or generated (SITE_X, row i): Philox pair 4t + q
-__device__ __forceinline__ void x_eps(const Dims &d, const DrawsDev &dr, int64_t iter, int i, bool live, int q,
-                                      d2 (&ev)[4]) {
-    if (d.inject) {
-        const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int kk = 8 * t + 2 * q;
-            ev[t].x = (live && kk < d.K) ? nx[kk] : 0.0;
-            ev[t].y = (live && kk + 1 < d.K) ? nx[kk + 1] : 0.0;
-        }
-    } else {
-        const Rng rng(d.seed);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int kk = 8 * t + 2 * q;
-            double n0 = 0.0, n1 = 0.0;
-            if (live && kk < d.K) rng.normal2(SITE_X, 0u, (uint32_t)i, (uint32_t)(4 * t + q), (uint32_t)iter, n0, n1);
-            ev[t].x = n0;
-            ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
-        }
-    }
-}
-// X rows from the summed message (dc:125-128): X' = Tx S' + Ux eps' as one accumulator chain per
-// 16-column half (Ms = {Tx, Ux}, k_xchol); lane (c, q) holds S and eps of row c, columns 8t + 2q,
-// +1 and stores X row c if live.  Shared by k_xdraw and k_wcol's message tail (same bits).
-__device__ __forceinline__ void xdraw_mfma(const Dims &d, const double (*Ms)[KP][KP + 1], const d2 (&sv)[4],
-                                           const d2 (&ev)[4], double *__restrict__ Xr, bool live, int c, int q) {
-    d4 ax[2];
-    ax[0] = ax[1] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int kk = 8 * t + 2 * q + e;
-            const double se = e ? sv[t].y : sv[t].x, ee = e ? ev[t].y : ev[t].x;
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                ax[mt] = mfma16x16x4(Ms[0][16 * mt + c][kk], se, ax[mt]);
-                ax[mt] = mfma16x16x4(Ms[1][16 * mt + c][kk], ee, ax[mt]);
-            }
-        }
-    if (!live) return;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int k = 16 * mt + q + 4 * g;
-            Xr[k] = (k < d.K) ? ax[mt][g] : 0.0;
-        }
-}
-
 constexpr int XD_ROWS = 4;
 constexpr int XD_SMEM = (2 * KP * (KP + 1) + 4 * 4 * 64 * 2) > XCHOL_SMEM ? (2 * KP * (KP + 1) + 4 * 4 * 64 * 2)
                                                                           : XCHOL_SMEM;
@@ -830,7 +770,25 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
     int nch, chunk;
     xdraw_chunks(nsrc, nch, chunk);     // chunk < 1024 (TreeSum levels below); dcfm_create caps g
     d2 sv[4], ev[4];
-    if (w == 0) x_eps(d, dr, iter, i, live, q, ev);   // in flight during the sum
+    if (w == 0 && d.inject) {   // eps of dc:126 (injected draw buffer), in flight during the sum
+        const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int kk = 8 * t + 2 * q;
+            ev[t].x = (live && kk < d.K) ? nx[kk] : 0.0;
+            ev[t].y = (live && kk + 1 < d.K) ? nx[kk + 1] : 0.0;
+        }
+    } else if (w == 0) {        // generated here (SITE_X, row i): Philox pair 4t + q
+        const Rng rng(d.seed);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int kk = 8 * t + 2 * q;
+            double n0 = 0.0, n1 = 0.0;
+            if (live && kk < d.K) rng.normal2(SITE_X, 0u, (uint32_t)i, (uint32_t)(4 * t + q), (uint32_t)iter, n0, n1);
+            ev[t].x = n0;
+            ev[t].y = (kk + 1 < d.K) ? n1 : 0.0;
+        }
+    }
     // one rank: the operators are already out (k_wcol's last arrival): their loads go out before
     // the sums' (two per thread), the LDS stores after
     double xmv[2] = {0.0, 0.0};
@@ -883,7 +841,29 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
         for (int k = 0; k < nch; ++k) ts.push(part[k][t][lane]);
         sv[t] = ts.total();
     }
-    xdraw_mfma(d, Ms, sv, ev, X + (size_t)i * KP, live, c, q);
+    d4 ax[2];
+    ax[0] = ax[1] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int kk = 8 * t + 2 * q + e;
+            const double se = e ? sv[t].y : sv[t].x, ee = e ? ev[t].y : ev[t].x;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                ax[mt] = mfma16x16x4(Ms[0][16 * mt + c][kk], se, ax[mt]);
+                ax[mt] = mfma16x16x4(Ms[1][16 * mt + c][kk], ee, ax[mt]);
+            }
+        }
+    if (!live) return;
+    double *Xr = X + (size_t)i * KP;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int k = 16 * mt + q + 4 * g;
+            Xr[k] = (k < d.K) ? ax[mt][g] : 0.0;
+        }
 }
 
 // ============================================================================
@@ -1277,7 +1257,7 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
     const int mg = d.shard0 + m;
     const int i0 = rb * 64 * MT + wave * 16 * MT;
     d4 acc[MT][2];
-    wpass_acc<KP, MT>(d, b.Y, b.Lam, b.omega, m, i0, 0, 0, d.PP >> 3, acc, [] {});
+    wpass_acc<KP, MT>(d, b.Y, b.Lam, b.omega, m, i0, 0, acc, [] {});
     WSTAMP(2);
     // the operators are normally out long before the pass ends; their loads and the rows' X are
     // issued first, the first tile's normals drawn while they are in flight
@@ -1322,188 +1302,6 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
         if (a == 0) WSTAMP(5);
         __builtin_amdgcn_sched_barrier(0);   // one tile's draw at a time (registers)
     }
-}
-
-
-// ----------------------------------------------------------------------------
-// k_wcol split W tiles (wpass modes 3, 4; round 6).  Block = (shard m, R = 16 MT rows); its 4
-// waves split the reduction over j in quarters (chunks [w nq, (w + 1) nq) of 8 columns, each
-// wave's even / odd k-step sets added as in wpass_acc) and the block adds the quarter sums
-// ((Q0 + Q1) + (Q2 + Q3)) through LDS; waves a < MT then draw Z for rows 16a .. 16a + 15 from
-// the sums (zdraw_rows).  Each element's order depends only on j and the quarters, so MT is free
-// per share size and N ranks reproduce one rank.  Against the unsplit 128-row tiles (all of a
-// launch's tiles streaming Y, then all drawing Z with HBM idle): 4x the
-// blocks at a quarter of the chain each, so blocks that draw overlap blocks that stream, and a
-// share of a few shards streams its Y in a quarter of the time.            dc:101-107,121-123
-//
-// Then the X message of the row block (dc:120-124) is summed over the shards inside the launch:
-// the last arrival among a chunk's tiles of the row block (a chunk = a canonical subtree of
-// shards, xsum_blocks(G) as for the A sum) sums the chunk, the last chunk sums the chunk sums —
-// the canonical tree T(0, G) (linalg.h TreeSum) — and one rank draws X for the rows right there
-// (k_xdraw's arithmetic, xdraw_mfma; operators from the A-sum block, published at sync[1]);
-// several ranks write the rank's message rows into xin (all-gathered after the launch).  This
-// replaces k_xdraw (one rank) and k_xred (several ranks).                   dc:119-128
-// ----------------------------------------------------------------------------
-template <int MT>
-__device__ __forceinline__ void xmsg_tail(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, int m,
-                                          int rb, int xdraw, unsigned long long xm_epoch, double *smem) {
-    constexpr int R = 16 * MT, NE = R * KP / 256;                 // message elements per thread
-    const int G = d.G, nxs = xsum_blocks(G), chunk = G / nxs, j = m / chunk, m0 = j * chunk;
-    const int nrb = d.NP / R, i0 = rb * R, t = threadIdx.x;
-    unsigned *tk = b.ticket + 2;                                  // [nrb][nxs] chunk tickets, [nrb] row blocks
-    if (!last_arrival(tk + (size_t)rb * nxs + j, (unsigned)chunk, smem)) return;
-    const size_t sst = (size_t)d.NP * KP;                         // Sp shard stride
-    const double *sp = b.Sp + (size_t)i0 * KP + t;
-    double vs[NE];
-    if (chunk <= 8) {                                             // tree8 with zeros past chunk = T(m0, chunk)
-        double v[NE][8];
-#pragma unroll
-        for (int u = 0; u < NE; ++u)
-#pragma unroll
-            for (int U = 0; U < 8; ++U) v[u][U] = (U < chunk) ? ld_agent(sp + (m0 + U) * sst + 256 * u) : 0.0;
-#pragma unroll
-        for (int u = 0; u < NE; ++u) vs[u] = tree8(v[u]);
-    } else {                                                      // chunk a power of two > 8: groups of 8
-#pragma unroll
-        for (int u = 0; u < NE; ++u) {
-            TreeSum<double, 6> ts;
-            for (int k = 0; k < chunk; k += 8) {
-                double v[8];
-#pragma unroll
-                for (int U = 0; U < 8; ++U) v[U] = ld_agent(sp + (m0 + k + U) * sst + 256 * u);
-                ts.push(tree8(v));
-            }
-            vs[u] = ts.total();
-        }
-    }
-    if (nxs > 1) {   // publish the chunk sum; the row block's last chunk adds them (canonical tree)
-        double *xp = b.xmp + (size_t)i0 * KP + t;
-#pragma unroll
-        for (int u = 0; u < NE; ++u) st_agent(xp + j * sst + 256 * u, vs[u]);
-        if (!last_arrival(tk + (size_t)nrb * nxs + rb, (unsigned)nxs, smem)) return;
-        if (nxs <= 8) {
-            double v[NE][8];
-#pragma unroll
-            for (int u = 0; u < NE; ++u)
-#pragma unroll
-                for (int U = 0; U < 8; ++U)
-                    v[u][U] = (U < nxs) ? (U == j ? vs[u] : ld_agent(xp + U * sst + 256 * u)) : 0.0;
-#pragma unroll
-            for (int u = 0; u < NE; ++u) vs[u] = tree8(v[u]);
-        } else {   // a non-power-of-two G: single-shard chunks, nxs = G > 8
-#pragma unroll
-            for (int u = 0; u < NE; ++u) {
-                TreeSum<double, 8> ts;
-                for (int k = 0; k < nxs; k += 8) {
-                    double v[8];
-#pragma unroll
-                    for (int U = 0; U < 8; ++U)
-                        v[U] = (k + U < nxs) ? (k + U == j ? vs[u] : ld_agent(xp + (k + U) * sst + 256 * u)) : 0.0;
-                    static_for<8>([&](auto U) { if (k + U < nxs) ts.push(v[U]); });
-                }
-                vs[u] = ts.total();
-            }
-        }
-    }
-    if (!xdraw) {   // several ranks: this rank's message rows (gathered after the launch)
-#pragma unroll
-        for (int u = 0; u < NE; ++u) b.xin[(size_t)i0 * KP + t + 256 * u] = vs[u];
-        return;
-    }
-    // one rank: X rows i0 .. i0 + R - 1 (the X operators of this launch's A-sum block)
-    double (*Mx)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);   // Tx, Ux
-    double *Sx = smem + 2 * KP * (KP + 1);                                          // [R][KP]
-    wait_count(b.sync + 1, xm_epoch);
-    double xmv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) xmv[u] = ld_agent(b.XM + t + 256 * u);
-#pragma unroll
-    for (int u = 0; u < NE; ++u) Sx[t + 256 * u] = vs[u];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        const int e = t + 256 * u, mat = e / (KP * KP), rem = e % (KP * KP);
-        Mx[mat][rem / KP][rem % KP] = xmv[u];
-    }
-    __syncthreads();
-    const int wave = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
-    if (wave >= MT) return;
-    const int i = i0 + 16 * wave + c;
-    const bool live = i < d.n;
-    d2 sv[4], ev[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) sv[u] = *reinterpret_cast<const d2 *>(Sx + (16 * wave + c) * KP + 8 * u + 2 * q);
-    x_eps(d, dr, iter, i, live, q, ev);
-    xdraw_mfma(d, Mx, sv, ev, b.X + (size_t)i * KP, live, c, q);
-}
-
-template <int MT>
-__device__ __forceinline__ void wsplit_tile(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, int w,
-                                            unsigned long long ops_epoch, int xdraw, double *smem) {
-    const int nrb = d.NP / (16 * MT);
-    const int m = w / nrb, rb = w % nrb;
-    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, c = lane & 15, q = lane >> 4;
-    const int mg = d.shard0 + m, i0 = rb * 16 * MT;
-    const int nq = (d.PP >> 3) >> 2;                               // PP is a multiple of 32
-    d4 acc[MT][2];
-    wpass_acc<KP, MT>(d, b.Y, b.Lam, b.omega, m, i0, 0, wave * nq, nq, acc, [] {});
-    WSTAMP(2);
-    // the shard's Z operators (normally out long before): their loads in flight during the sum
-    wait_count(b.sync + SYNC_ZM + m, ops_epoch);
-    WSTAMP(3);
-    constexpr int NU = 4 * KP * KP / 256;
-    double zv[NU];
-    {
-        const double *Zm = b.ZM + (size_t)m * 4 * KP * KP;
-#pragma unroll
-        for (int u = 0; u < NU; ++u) zv[u] = ld_agent(Zm + t + 256 * u);
-    }
-    // quarter sums: red[wave][a][tb][g][lane]
-#pragma unroll
-    for (int a = 0; a < MT; ++a)
-#pragma unroll
-        for (int tb = 0; tb < 2; ++tb)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) smem[(((wave * MT + a) * 2 + tb) * 4 + g) * 64 + lane] = acc[a][tb][g];
-    __syncthreads();
-    d2 wv[4];
-    if (wave < MT) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            double h[2];
-#pragma unroll
-            for (int tb = 0; tb < 2; ++tb) {
-                const double *r = smem + ((wave * 2 + tb) * 4 + g) * 64 + lane;   // quarter 0, tile a = wave
-                constexpr int QS = MT * 2 * 4 * 64;                                // quarter stride
-                h[tb] = (r[0] + r[QS]) + (r[2 * QS] + r[3 * QS]);
-            }
-            wv[g].x = h[0];
-            wv[g].y = h[1];
-        }
-    }
-    __syncthreads();
-    double (*Ms)[KP][KP + 1] = reinterpret_cast<double (*)[KP][KP + 1]>(smem);    // M1, M2, U, NA
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        const int e = t + 256 * u, mat = e / (KP * KP), rem = e % (KP * KP);
-        Ms[mat][rem / KP][rem % KP] = zv[u];
-    }
-    __syncthreads();
-    WSTAMP(4);
-    if (wave < MT) {
-        const int i = i0 + 16 * wave + c;
-        const bool live = i < d.n;
-        d2 xv[4], ev[4];
-        const double *Xi = b.X + (size_t)i * KP + 2 * q;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) xv[u] = *reinterpret_cast<const d2 *>(Xi + 8 * u);
-        z_eps(d, dr, iter, mg, i, live, q, ev);
-        zdraw_rows<true>(d, Ms, wv, xv, ev, b.Z + ((size_t)m * d.NP + i) * KP, b.Sp + ((size_t)m * d.NP + i) * KP,
-                         live, c, q);
-    }
-    WSTAMP(5);
-#ifndef DCFM_DEV_NO_XTAIL   // dev A/B: the split tiles without the message tail (k_xdraw / k_xred sum Sp)
-    xmsg_tail<MT>(d, b, dr, iter, m, rb, xdraw, ops_epoch, smem);
-#endif
 }
 
 __device__ __forceinline__ void wcol_body(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, int ops, int colsum,
@@ -1623,28 +1421,16 @@ __device__ __forceinline__ void wcol_body(const Dims &d, const Bufs &b, const Dr
 #pragma unroll
             for (int u = 0; u < NU; ++u) xprec_store(d, smem, t + 256 * u, xs[u]);
             __syncthreads();
-            if (wpass >= 3) {                         // the W tiles' message tails draw X in this launch
-                xchol_factor<true>(d, b.XM, smem);    // Xprec = g I + rho sum A (dc:117), Rx (dc:118)
-                signal_count(b.sync + 1);
-            } else {
-                xchol_factor(d, b.XM, smem);
-            }
+            xchol_factor(d, b.XM, smem);              // Xprec = g I + rho sum A (dc:117), Rx (dc:118)
             return;
         }
         blk -= nxs;
     }
-    if (wpass) {   // 1: 128-row blocks, 2: 64-row blocks; 3, 4: split 32- / 16-row blocks + the X
-                   // message tail (wcol_rows); W' -> the Z draw
-        const int nw = (d.NP / wcol_rows(wpass)) * d.G;
+    if (wpass) {   // 1: 128-row blocks, 2: 64-row blocks (wcol_wpass_mode); W' -> the Z draw
+        const int nw = (d.NP / (64 * (3 - wpass))) * d.G;
         if (blk < nw) {
-            const int w = xcd_remap(blk, nw);
-#if defined(DCFM_WCOL_WMODE) && DCFM_WCOL_WMODE < 3   // dev A/B: the unsplit tiles (+ k_xdraw / k_xred)
-            if (wpass == 2) wpass_z_tile<1>(d, b, dr, iter, w, ops_epoch, smem);
-            else wpass_z_tile<2>(d, b, dr, iter, w, ops_epoch, smem);
-#else
-            if (wpass == 3) wsplit_tile<2>(d, b, dr, iter, w, ops_epoch, xchol, smem);
-            else wsplit_tile<1>(d, b, dr, iter, w, ops_epoch, xchol, smem);
-#endif
+            if (wpass == 2) wpass_z_tile<1>(d, b, dr, iter, xcd_remap(blk, nw), ops_epoch, smem);
+            else wpass_z_tile<2>(d, b, dr, iter, xcd_remap(blk, nw), ops_epoch, smem);
             return;
         }
         blk -= nw;
@@ -1946,22 +1732,6 @@ void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
         hipLaunchKernelGGL(k_zdraw<ZTHREADS>, dim3((d.NP / ZROWS) * d.G), dim3(ZTHREADS), 0, s, d, b.W, b.ZM, b.X, b.Z,
                            b.Sp, dr, iter);
 }
-// k_wcol's W-tile layout: split 32-row tiles (2,048 blocks at c3), or split 16-row ones where those
-// would not give every CU several blocks (a few shards per rank: the g = 8 share of c3, 256 -> 512)
-bool wcol_xtail(const Dims &d) {
-#ifdef DCFM_DEV_NO_XTAIL
-    return false;
-#else
-    return wcol_mode(d) >= 3;
-#endif
-}
-int wcol_mode(const Dims &d) {
-#ifdef DCFM_WCOL_WMODE
-    return DCFM_WCOL_WMODE;   // dev A/B: forced layout (1, 2: the unsplit tiles + k_xdraw / k_xred)
-#else
-    return (d.NP / 32) * d.G >= 1024 ? 3 : 4;
-#endif
-}
 // k_wcol launch (K <= 32)
 void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, bool ops, bool colsum, bool wpass,
                  unsigned long long ops_epoch, hipStream_t s, bool lamgen) {
@@ -1970,8 +1740,12 @@ void launch_wcol(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter,
     if (lamgen && b.ldraw) lg = lam_gen_plan(d, b.ldraw);
     // W pass tiles: 64-row blocks up to one 128-row block per CU (the g = 32 share of c3: 256
     // blocks; 64-row ones measured 2.8 % faster there, 128-row ones faster at c3's 512)
-    const int wmode = wcol_mode(d);
-    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / wcol_rows(wmode)) * d.G : 0);
+#ifdef DCFM_WCOL_WMODE
+    const int wmode = DCFM_WCOL_WMODE;   // dev A/B: forced block height
+#else
+    const int wmode = (d.NP / 128) * d.G <= 256 ? 2 : 1;
+#endif
+    const int nb = (ops ? d.G + xsum_blocks(d.G) : 0) + (colsum ? d.G : 0) + (wpass ? (d.NP / (64 * (3 - wmode))) * d.G : 0);
     if (nb + lg.b_total == 0) return;
     hipLaunchKernelGGL(k_wcol, dim3(nb + lg.b_total), dim3(256), 0, s, d, b, dr, iter, ops ? 1 : 0, colsum ? 1 : 0,
                        wpass ? wmode : 0, ops_epoch, d.coll ? 0 : 1, lg);

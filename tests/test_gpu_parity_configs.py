@@ -139,3 +139,44 @@ def test_baseline_shape_parity(dcfm, name, mode):
         assert e < TOL, f"{name}: Sigmaout rel err {e:.3e} (bar {TOL:.0e})"
     finally:
         smp.close()
+
+
+@pytest.mark.timeout(900)
+def test_c5_sweep_parity(dcfm, record_property):
+    """configs[4] (c5: p = 100,096 = 391 x 256, n = 2,000, g = 256, K = 30) at its own
+    shape: one injected-draw iteration of the sweep (dc:97-177) with thin > N, so Sigmaout (80 GB
+    dense at this p; its assembly is pinned at this shape by test_gpu_scale.py) is skipped.  Every
+    state array against the vectorised oracle at 1e-10 normwise, the stages of helpers.stagewise_errors
+    (Z, X, eta; the loading draw's backward error; psi, delta / tau, Plam from the GPU's own Lambda;
+    ps / omega per row against dc:169's direct residual), default (SS-identity) path."""
+    n, p, g, K = 2000, 100096, 256, 30
+    c = make_case(n, p, g, K, seed=29, k0=10, dense_truth=False)
+    st, Yd = c["st"], c["Yd"]
+    D = V.Data(Yd)
+    smp = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], 0, 1, 10, inject_draws=True, asm_batch=1)
+    try:
+        smp.set_data(Yd)
+        smp.set_state({f: v for f, v in state_dict(st).items() if f != "eta"})
+        smp.set_draws(stacked_draws(c["src"], 1, 1), 1, 1)
+        smp.run(1, 1)
+        got = smp.get_state()
+        assert smp.saved_samples() == 0
+    finally:
+        smp.close()
+    start = st.copy()
+    ref = st.copy()
+    V.run_chain(D, ref, c["rho"], c["hyper"], c["src"].iteration, 1, 1, 0, 1, 10, SigLower=np.zeros((1, 1)),
+                direct=True)
+    errs = {f: rel_err(got[f], getattr(ref, f)) for f in STATE_CMP}
+    stage, bw, _ = stagewise_errors(start, got, D, c["rho"], c["hyper"], c["src"].iteration(1))
+    ps_row = _ps_direct_err(got, start, D, c, 1)
+    record_property("c5_state_rel_err", errs)
+    record_property("c5_stage_rel_err", {**stage, "lambda_bw": bw, "ps_direct_per_row": ps_row})
+    print("C5_PARITY", {k: f"{v:.2e}" for k, v in {**errs, **{"stage_" + s: e for s, e in stage.items()},
+                                                    "lambda_bw": bw, "ps_direct_per_row": ps_row}.items()})
+    for f, e in errs.items():
+        assert e < TOL, f"c5: {f} rel err {e:.3e} (bar {TOL:.0e})"
+    for f, e in stage.items():
+        assert e < TOL, f"c5: stage {f} rel err {e:.3e} (bar {TOL:.0e})"
+    assert bw < BW_TOL, f"c5: loading backward error {bw:.3e}"
+    assert ps_row < TOL, f"c5: ps / omega vs dc:169 residual, per row {ps_row:.3e}"
