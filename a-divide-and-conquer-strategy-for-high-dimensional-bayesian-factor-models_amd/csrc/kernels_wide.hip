@@ -384,6 +384,37 @@ __device__ __forceinline__ void trail_tile(d4 *T) {
     for (int s4 = 0; s4 < 4; ++s4) T[t] = mfma16x16x4(-T[a][s4], T[b][s4], T[t]);
 }
 
+// The trailing tiles of block column J but the next diagonal one, (Kc, I) with J < Kc <= I < NB in
+// row-major order, numbered from 0: pivot step S of the next diagonal block issues tiles
+// [S n / 16, (S + 1) n / 16) of the n = NT_J of them.
+template <int NB, int J>
+__host__ __device__ constexpr int la_count() { return (NB - J - 1) * (NB - J) / 2 - 1; }
+template <int NB, int J>
+__host__ __device__ constexpr int la_index(int Kc, int I) {
+    int e = 0;
+    for (int a = J + 1; a < NB; ++a)
+        for (int b = a; b < NB; ++b) {
+            if (a == J + 1 && b == J + 1) continue;
+            if (a == Kc && b == I) return e;
+            ++e;
+        }
+    return -1;
+}
+template <int NB, int J, int S>
+__device__ __forceinline__ void la_step(d4 *T) {
+    constexpr int n = la_count<NB, J>(), lo = S * n / 16, hi = (S + 1) * n / 16;
+    static_for<NB>([&](auto KC) {
+        constexpr int Kc = decltype(KC)::value;
+        static_for<NB>([&](auto IC) {
+            constexpr int I = decltype(IC)::value;
+            if constexpr (Kc > J && I >= Kc && !(Kc == J + 1 && I == J + 1)) {
+                constexpr int e = la_index<NB, J>(Kc, I);
+                if constexpr (e >= lo && e < hi) trail_tile<NB, J, Kc, I>(T);
+            }
+        });
+    });
+}
+
 template <int KW, int NB>
 __global__ __launch_bounds__(64) void k_lambda_w(
     Dims d, const double *__restrict__ C, const double *__restrict__ E, const double *__restrict__ yy,
@@ -474,14 +505,18 @@ __global__ __launch_bounds__(64) void k_lambda_w(
             }
         });
     });
-    // ---- blocked factorisation with the forward solve
+    // ---- blocked factorisation with the forward solve.  Look-ahead (round 6): block column J's
+    //      trailing update of the next diagonal tile goes first, then the next diagonal block's
+    //      factorisation (a chain of 16 dependent pivots through LDS) runs with the rest of J's
+    //      trailing MFMAs issued into its latency (chol_inv16_hook, la_step); every tile sees the same
+    //      operations in the same order as without it
+#pragma unroll
+    for (int g = 0; g < 4; ++g) Sd[(q + 4 * g) * LD + c16] = T[utix<NB>(0, 0)][g];
+    __syncthreads();
+    chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
+    __syncthreads();
     static_for<NB>([&](auto JC) {
         constexpr int J = decltype(JC)::value, tJ = utix<NB>(J, J);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) Sd[(q + 4 * g) * LD + c16] = T[tJ][g];
-        __syncthreads();
-        chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
-        __syncthreads();
         if (q == 0) udg[16 * J + c16] = Ud[c16 * LD + c16];                    // 1 / L_kk (the guard)
         double u[4], bq[4];
 #pragma unroll
@@ -522,13 +557,17 @@ __global__ __launch_bounds__(64) void k_lambda_w(
                 if (q == 0) vb[16 * I + c16] -= pv;
             }
         });
-        static_for<NB>([&](auto KC) {                     // trailing T_{Kc,I} -= R_{J,Kc}' R_{J,I}
-            constexpr int Kc = decltype(KC)::value;
-            static_for<NB>([&](auto IC) {
-                constexpr int I = decltype(IC)::value;
-                if constexpr (Kc > J && I >= Kc) trail_tile<NB, J, Kc, I>(T);
+        if constexpr (J + 1 < NB) {   // trailing T_{Kc,I} -= R_{J,Kc}' R_{J,I}: the next diagonal tile first
+            trail_tile<NB, J, J + 1, J + 1>(T);
+            __syncthreads();                                                   // U_JJ's reads are done
+#pragma unroll
+            for (int g = 0; g < 4; ++g) Sd[(q + 4 * g) * LD + c16] = T[utix<NB>(J + 1, J + 1)][g];
+            __syncthreads();
+            chol_inv16_hook<LD>(Sd, 0, Ud, lds_l, lds_u, lane, [&](auto S) {
+                la_step<NB, J, decltype(S)::value>(T);                         // the rest, 1/16 per pivot
             });
-        });
+            __syncthreads();
+        }
     });
     // ---- w = v + z (dc:142 normrnd), back solve R x = w (dc:144):
     //      x_J = U_JJ' (w_J - sum_{I>J} R_{J,I} x_I); lane (c16, .) holds x_I[c16] in xr[I]

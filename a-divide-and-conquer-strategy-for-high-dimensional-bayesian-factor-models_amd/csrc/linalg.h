@@ -397,6 +397,59 @@ __device__ __forceinline__ void chol_inv16_p(const double *Sm, int o, double *Ub
         urow[0] = R0 * ik; urow[4] = R1 * ik; urow[8] = R2 * ik; urow[12] = R3 * ik;
     }
 }
+// chol_inv16_p with its 16 pivot steps unrolled, calling hook(std::integral_constant<int, k>) once step
+// k's LDS hand-off is in flight: independent work (k_lambda_w's look-ahead: the rest of the previous
+// block column's trailing MFMAs) issued into the pivot chain's latency.  Same operations on the block as
+// chol_inv16_p, so the same bits.
+template <int J, class Hook>
+__device__ __forceinline__ void chol16_step_h(double &a0, double &a1, double &a2, double &a3, double &R0, double &R1,
+                                              double &R2, double &R3, double &dr, int kk, int r, int cg,
+                                              double *lds_l, double *lds_u, Hook &&hook) {
+    const int k = 4 * kk + J;
+    const double v = quad_bcast<J>(a0);                         // a[r][k]
+    lds_l[r] = (r > k) ? v : 0.0;
+    if (r == k) {
+        lds_u[cg] = R0; lds_u[4 + cg] = R1; lds_u[8 + cg] = R2; lds_u[12 + cg] = R3;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const double *pl = lds_l + 4 * kk + cg;
+    const double l0 = pl[0], l1 = pl[4], l2 = pl[8], l3 = pl[12];
+    const double u0 = lds_u[cg], u1 = lds_u[4 + cg], u2 = lds_u[8 + cg], u3 = lds_u[12 + cg];
+    __builtin_amdgcn_sched_barrier(0);                          // the reads are in flight during the chain
+    hook();
+    const double piv = readlane_d(a0, 4 * k + J);
+    const double f = (r > k) ? v * rcp_f64(piv) : 0.0;
+    a0 = fma(-f, l0, a0); a1 = fma(-f, l1, a1); a2 = fma(-f, l2, a2); a3 = fma(-f, l3, a3);
+    R0 = fma(-f, u0, R0); R1 = fma(-f, u1, R1); R2 = fma(-f, u2, R2); R3 = fma(-f, u3, R3);
+    dr = (r == k) ? piv : dr;
+    __builtin_amdgcn_wave_barrier();
+}
+template <int LDP, class Hook>
+__device__ __forceinline__ void chol_inv16_hook(const double *Sm, int o, double *Ub, double *lds_l, double *lds_u,
+                                                int lane, Hook &&hook) {
+    const int r = lane >> 2, cg = lane & 3;
+    const double *srow = Sm + (o + r) * LDP + o + cg;
+    double a0 = srow[0], a1 = srow[4], a2 = srow[8], a3 = srow[12];
+    double R0 = (cg == r) ? 1.0 : 0.0, R1 = (4 + cg == r) ? 1.0 : 0.0;
+    double R2 = (8 + cg == r) ? 1.0 : 0.0, R3 = (12 + cg == r) ? 1.0 : 0.0;
+    double dr = 1.0;
+    if (lane < 16) lds_l[16 + lane] = 0.0;
+    static_for<4>([&](auto KK) {
+        constexpr int kk = decltype(KK)::value;
+        chol16_step_h<0>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u,
+                         [&] { hook(std::integral_constant<int, 4 * kk>{}); });
+        chol16_step_h<1>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u,
+                         [&] { hook(std::integral_constant<int, 4 * kk + 1>{}); });
+        chol16_step_h<2>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u,
+                         [&] { hook(std::integral_constant<int, 4 * kk + 2>{}); });
+        chol16_step_h<3>(a0, a1, a2, a3, R0, R1, R2, R3, dr, kk, r, cg, lds_l, lds_u,
+                         [&] { hook(std::integral_constant<int, 4 * kk + 3>{}); });
+        a0 = a1; a1 = a2; a2 = a3; a3 = 0.0;
+    });
+    const double ik = rsqrt_f64(dr);                     // 1 / L_rr
+    double *urow = Ub + (o + r) * LDP + o + cg;
+    urow[0] = R0 * ik; urow[4] = R1 * ik; urow[8] = R2 * ik; urow[12] = R3 * ik;
+}
 __device__ __forceinline__ void chol_inv16(const double (*Sm)[KP + 1], int o, double (*Ub)[KP + 1],
                                            double *lds_l, double *lds_u, int lane) {
     chol_inv16_p<KP + 1>(&Sm[0][0], o, &Ub[0][0], lds_l, lds_u, lane);
