@@ -102,7 +102,13 @@ def test_c4_breakdown_rate_and_error_match_oracle(dcfm, record_property):
                "gpu_chains": M_GPU, "gpu_broke_down": gb,
                "gpu_breakdown_by": sorted(r["breakdown_by"] for r in gpu if r["breakdown_by"]),
                "fisher_p": float(p_fisher), "gpu_seeds": [SEED0, M_GPU], "chunk": CHUNK}
-    ok = {"breakdown_rate": p_fisher > 0.01}
+    ok = {"breakdown_rate": bool(p_fisher > 0.01)}
+    # reported, not asserted: when the breakdowns happen (the GPU's at chunk resolution: the end of the
+    # CHUNK-iteration run in which the chain went non-finite, so up to CHUNK - 1 later than the event)
+    bo = [r["breakdown_iter"] for r in reps if r["breakdown_iter"]]
+    bg = [r["breakdown_by"] for r in gpu if r["breakdown_by"]]
+    if len(bo) >= 3 and len(bg) >= 3:
+        summary["breakdown_time_mannwhitney_p"] = float(stats.mannwhitneyu(bo, [v - (CHUNK - 1) / 2 for v in bg]).pvalue)
     gdone = [r for r in gpu if r["breakdown_by"] is None]
     for key in ("fro_rel", "op_rel"):
         a = [r[key] for r in done]
@@ -112,7 +118,7 @@ def test_c4_breakdown_rate_and_error_match_oracle(dcfm, record_property):
         summary[key] = {"oracle_mean": float(np.mean(a)), "gpu_mean": float(np.mean(b)), "z": z,
                         "bar": Z99 * se, "bar_rel": Z99 * se / float(np.mean(a)), "ks_p": ks,
                         "oracle": a, "gpu": b}
-        ok[key] = abs(z) < Z99 and ks > 0.01
+        ok[key] = bool(abs(z) < Z99 and ks > 0.01)
     summary["ok"] = ok
     (out / "c4_breakdown_gpu.json").write_text(json.dumps(summary, indent=1) + "\n")
     record_property("c4_breakdown", {k: summary[k] for k in ("oracle_broke_down", "gpu_broke_down", "fisher_p")})

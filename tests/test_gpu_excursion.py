@@ -239,8 +239,8 @@ def test_breakdown_is_the_references(dcfm, record_property, case):
         that is not positive definite) completes Z, X, eta (dc:97-134) and fails at the loading draw;
       * the library fed the same state and variates (injected) fails there too: its state after the
         failing iteration (dcfm_get_state_raw) has finite Z, X, eta equal to the oracle's at 1e-10 and the
-        first non-finite values in Lambda (dc:137-145), in rows whose loading system the oracle's chol
-        rejects.
+        first non-finite values in Lambda (dc:137-145), every such row one whose loading system the
+        oracle's chol rejects (round 6: c2 499 of the oracle's 624 rejected rows, c4 768 of 1,250).
     The guard of the SS identity is not involved (it acts on ps / omega, after the loading draw)."""
     from numpy.linalg import LinAlgError
 
@@ -322,4 +322,6 @@ def test_breakdown_is_the_references(dcfm, record_property, case):
     assert gpu_stage == "Lambda", f"the library's first non-finite stage is {gpu_stage}, not the loading draw"
     for f in ("Z", "X", "eta"):
         assert info[f"{f}_rel_err"] < TOL, (f, info)
-    assert info["gpu_rows_nonfinite"] > 0 and info["rows_both"] > 0, info
+    # every row the library left non-finite is one whose system the oracle's chol rejects (the library may
+    # still finish a row the oracle rejects: a pivot within rounding of zero)
+    assert info["gpu_rows_nonfinite"] > 0 and info["rows_both"] == info["gpu_rows_nonfinite"], info
