@@ -180,13 +180,21 @@ def test_c4_generated_chain_through_excursions(dcfm, record_property):
     pytest.fail(f"no seed ran 1,200 iterations through an excursion: {tried}")
 
 
-def _first_breakdown(dcfm, c, g, K, seed, iters=800, chunk=20):
-    """(last finite state, first non-finite iteration) of the generated chain, or None."""
+_BREAKDOWNS = {}
+
+
+def _first_breakdown(dcfm, c, g, K, seed, iters=800, chunk=20, with_prev=False):
+    """(last finite state, first non-finite iteration) of the generated chain, or None; with_prev: also
+    the state one iteration earlier, (prev, last finite, iteration).  Cached per (shape, seed)."""
+    key = (c["n"], c["P"], g, K, seed, iters, chunk)
+    if key in _BREAKDOWNS:
+        r = _BREAKDOWNS[key]
+        return None if r is None else (r if with_prev else r[1:])
     st = {f: v for f, v in state_dict(c["st"]).items() if f != "eta"}
 
     def chain(state, first, count, step):
         smp = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], 10 ** 6, 0, 1, seed=seed)
-        good, it = state, first
+        prev, good, it = None, state, first
         try:
             smp.set_data(c["Yd"])
             smp.set_state(state)
@@ -196,18 +204,20 @@ def _first_breakdown(dcfm, c, g, K, seed, iters=800, chunk=20):
                     s = smp.get_state()
                 except dcfm.DcfmError as e:
                     assert e.code == DCFM_ERR_NUMERIC, e
-                    return good, it
-                good = {f: v for f, v in s.items() if f != "eta"}
+                    return prev, good, it
+                prev, good = good, {f: v for f, v in s.items() if f != "eta"}
                 it += step
         finally:
             smp.close()
-        return good, None
+        return prev, good, None
 
-    good, it = chain(st, 1, iters, chunk)
+    _, good, it = chain(st, 1, iters, chunk)
     if it is None:
+        _BREAKDOWNS[key] = None
         return None
-    good, it = chain(good, it, chunk, 1)
-    return good, it
+    r = chain(good, it, chunk, 1)
+    _BREAKDOWNS[key] = r
+    return r if with_prev else r[1:]
 
 
 def _first_nonfinite_stage(st):
@@ -325,3 +335,68 @@ def test_breakdown_is_the_references(dcfm, record_property, case):
     # every row the library left non-finite is one whose system the oracle's chol rejects (the library may
     # still finish a row the oracle rejects: a pivot within rounding of zero)
     assert info["gpu_rows_nonfinite"] > 0 and info["rows_both"] == info["gpu_rows_nonfinite"], info
+
+
+@pytest.mark.timeout(600)
+def test_wide_guard_fires_before_breakdown(dcfm, record_property):
+    """The wide path's SS-identity guard (k_lambda_w flags, k_resid_flagged) decides right where
+    it matters.  In the iteration before a c4 chain's breakdown (state one iteration before the last finite
+    one, that iteration's variates injected) the excursion makes SS_j = yy_j - 2 lam_j.C_j + lam_j E lam_j'
+    cancel for many rows: evaluated on the host from the library's own eta and Lambda, the identity misses
+    dc:169's direct residual by more than the bar (max(1e-10, the residual's own rounding bound) per row) on
+    those rows.  The library's ps / omega must meet the bar on EVERY row, so every such row must have been
+    flagged and redone by dc:169 on the device."""
+    from helpers import elem_rel_err
+    from oracle import IterDraws
+    from oracle import dc_oracle as F
+    from test_gpu_generated_draws import _draws
+
+    spec = BREAKDOWN_CASES["c4"]
+    n, p, g, K = spec["shape"]
+    c = make_case(n, p, g, K, seed=29, k0=10, dense_truth=False)
+    found = None
+    for seed in spec["seeds"]:
+        found = _first_breakdown(dcfm, c, g, K, seed, iters=spec["iters"], with_prev=True)
+        if found is not None and found[0] is not None:
+            break
+    assert found is not None and found[0] is not None, "no c4 breakdown with a previous state found"
+    prev, _, it = found
+    it0 = it - 1
+    dr = _draws(dcfm, seed, c["n"], c["P"], g, K, it0, 1, dcfm.Hyper())
+    smp = dcfm.Sampler(c["n"], c["P"], g, K, c["rho"], 10 ** 6, 0, 1, seed=seed, inject_draws=True)
+    try:
+        smp.set_data(c["Yd"])
+        smp.set_state(prev)
+        smp.set_draws(dr, it0, 1)
+        smp.run(it0, 1)
+        got = smp.get_state()
+    finally:
+        smp.close()
+    d = IterDraws(**{k: np.asarray(v)[..., 0] for k, v in dr.items()})
+    # dc:169-171 as written on the library's own eta and Lambda
+    st = _as_oracle({**prev, "eta": got["eta"]})
+    st.Lambda[...] = got["Lambda"]
+    F.update_ps(st, c["Yd"], c["hyper"], d)
+    bound = residual_rounding_bound(got, c["Yd"]).T                           # P x g
+    bar = np.maximum(TOL, bound)
+    err_lib = np.abs(got["ps"][:, 0, :] - st.ps[:, 0, :]) / st.ps[:, 0, :] / bar * TOL
+    # the identity on the host, from the same eta and Lambda
+    Ys = np.moveaxis(c["Yd"], 2, 0)                                            # g x n x P
+    eta = np.moveaxis(got["eta"], 2, 0)
+    lam = np.moveaxis(got["Lambda"], 2, 0)                                     # g x P x K
+    yy = np.einsum("mij,mij->mj", Ys, Ys)
+    C = np.swapaxes(Ys, 1, 2) @ eta                                            # g x P x K
+    E = np.swapaxes(eta, 1, 2) @ eta
+    SS_id = yy - 2.0 * np.einsum("mjk,mjk->mj", lam, C) + np.einsum("mjk,mkl,mjl->mj", lam, E, lam)
+    ps_id = ((1.0 / (c["hyper"].bs + 0.5 * SS_id)) * d.Gps.T).T                # P x g
+    err_id = np.abs(ps_id - st.ps[:, 0, :]) / st.ps[:, 0, :] / bar * TOL
+    n_id_bad = int(np.sum(~(err_id < TOL)))
+    info = {"seed": seed, "iteration": it0, "xmax": float(np.abs(got["X"]).max()),
+            "rows_identity_off": n_id_bad, "rows": int(err_id.size),
+            "worst_identity": float(np.nanmax(np.where(np.isfinite(err_id), err_id, np.inf))),
+            "worst_library": float(err_lib.max()), "bound_max": float(bound.max()),
+            "omega_vs_dc169": elem_rel_err(got["omega"], st.omega)}
+    record_property("wide_guard", info)
+    print("WIDE_GUARD", info)
+    assert n_id_bad > 0, f"the identity holds on every row at this state: the guard is not exercised ({info})"
+    assert err_lib.max() < TOL, f"library ps vs dc:169 per row {err_lib.max():.3e} x bar ({info})"
