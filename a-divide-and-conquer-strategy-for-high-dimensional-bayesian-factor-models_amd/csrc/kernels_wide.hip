@@ -363,7 +363,7 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
 // Q_j = R'R (R = Llam', dc:142) on the NB x NB upper tiles T_{Kc,I} (Kc <= I) of Q_j, all held
 // in this wave's registers in the fp64 MFMA C/D layout (lane (c16, q) holds T[q + 4g][c16],
 // g = 0..3).  That layout is the B operand of a product with k = q + 4g and the A operand of
-// its transpose, so per block column J, with U_JJ = L_JJ^{-1} from chol_inv16 (LDS):
+// its transpose, so per block column J, with U_JJ = L_JJ^{-1} from chol_inv16_blk (staged in LDS):
 //   panel     R_{J,I}  = U_JJ T_{J,I}                (A = U_JJ from LDS, B = registers)
 //   trailing  T_{Kc,I} -= R_{J,Kc}' R_{J,I}           (both operands in registers)
 //   forward   b_I -= R_{J,I}' v_J,  v_J = U_JJ b_J    (dc:143, sums over q by lane shuffles)
@@ -400,9 +400,9 @@ __host__ __device__ constexpr int la_index(int Kc, int I) {
         }
     return -1;
 }
-template <int NB, int J, int S>
+template <int NB, int J, int S, int NS = 16>
 __device__ __forceinline__ void la_step(d4 *T) {
-    constexpr int n = la_count<NB, J>(), lo = S * n / 16, hi = (S + 1) * n / 16;
+    constexpr int n = la_count<NB, J>(), lo = S * n / NS, hi = (S + 1) * n / NS;
     static_for<NB>([&](auto KC) {
         constexpr int Kc = decltype(KC)::value;
         static_for<NB>([&](auto IC) {
@@ -422,10 +422,9 @@ __global__ __launch_bounds__(64) void k_lambda_w(
     double *__restrict__ psi, double *__restrict__ ps, double *__restrict__ omega, double *__restrict__ cpart,
     DrawsDev dr, int64_t iter, double kappa_max, int *__restrict__ rflag) {
     constexpr int NT = NB * (NB + 1) / 2, LD = 17, TZ = 16 * LD, NH = KW / 64;
-    __shared__ double Sd[TZ], Ud[TZ];
+    __shared__ double Ud[TZ];
     __shared__ double vb[KW], vx[KW], ein[5][KW];   // per row index r: NL, Gpsi, tau, C, Plam
     __shared__ double edg[KW], udg[KW];             // the guard: E_m[r][r], 1 / L_rr (L = chol(Q_j))
-    __shared__ double lds_l[32], lds_u[16];
     const int j = blockIdx.x, m = blockIdx.y, mg = d.shard0 + m;
     const int lane = threadIdx.x, c16 = lane & 15, q = lane >> 4;
     const int K = d.K;
@@ -490,6 +489,15 @@ __global__ __launch_bounds__(64) void k_lambda_w(
         static_for<NB>([&](auto IC) {
             constexpr int I = decltype(IC)::value;
             if constexpr (I >= Kc) {
+                if (16 * I + 16 <= K) {                  // no padding in the tile: no selects
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        double val = psj * T[utix<NB>(Kc, I)][g];
+                        if constexpr (I == Kc) val = (q + 4 * g == c16) ? val + pl[Kc][g] : val;
+                        T[utix<NB>(Kc, I)][g] = val;
+                    }
+                    return;
+                }
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const int r = 16 * Kc + q + 4 * g, c = 16 * I + c16;
@@ -505,15 +513,16 @@ __global__ __launch_bounds__(64) void k_lambda_w(
             }
         });
     });
-    // ---- blocked factorisation with the forward solve.  Look-ahead (round 6): block column J's
-    //      trailing update of the next diagonal tile goes first, then the next diagonal block's
-    //      factorisation (a chain of 16 dependent pivots through LDS) runs with the rest of J's
-    //      trailing MFMAs issued into its latency (chol_inv16_hook, la_step); every tile sees the same
-    //      operations in the same order as without it
+    // ---- blocked factorisation with the forward solve.  Look-ahead: block column J's trailing update
+    //      of the next diagonal tile goes first, then that block's factor U = L^{-1} from its registers
+    //      (chol_inv16_blk: 4 x 4 block steps, no LDS) with the rest of J's trailing MFMAs issued into
+    //      its four steps (la_step).  Round 6 replaced the pivot-by-pivot LDS factor (chol_inv16_hook,
+    //      16 round trips per block): k_lambda_w 369 -> 337 us at c4
+    {
+        const d4 U0 = chol_inv16_blk(T[utix<NB>(0, 0)], lane, [](auto) {});
 #pragma unroll
-    for (int g = 0; g < 4; ++g) Sd[(q + 4 * g) * LD + c16] = T[utix<NB>(0, 0)][g];
-    __syncthreads();
-    chol_inv16_p<LD>(Sd, 0, Ud, lds_l, lds_u, lane);
+        for (int g = 0; g < 4; ++g) Ud[(q + 4 * g) * LD + c16] = U0[g];
+    }
     __syncthreads();
     static_for<NB>([&](auto JC) {
         constexpr int J = decltype(JC)::value, tJ = utix<NB>(J, J);
@@ -559,13 +568,14 @@ __global__ __launch_bounds__(64) void k_lambda_w(
         });
         if constexpr (J + 1 < NB) {   // trailing T_{Kc,I} -= R_{J,Kc}' R_{J,I}: the next diagonal tile first
             trail_tile<NB, J, J + 1, J + 1>(T);
+            // the next diagonal block's factor from its registers (chol_inv16_blk), the rest of J's
+            // trailing MFMAs issued into its four block steps
+            const d4 Un = chol_inv16_blk(T[utix<NB>(J + 1, J + 1)], lane, [&](auto S) {
+                la_step<NB, J, decltype(S)::value, 4>(T);
+            });
             __syncthreads();                                                   // U_JJ's reads are done
 #pragma unroll
-            for (int g = 0; g < 4; ++g) Sd[(q + 4 * g) * LD + c16] = T[utix<NB>(J + 1, J + 1)][g];
-            __syncthreads();
-            chol_inv16_hook<LD>(Sd, 0, Ud, lds_l, lds_u, lane, [&](auto S) {
-                la_step<NB, J, decltype(S)::value>(T);                         // the rest, 1/16 per pivot
-            });
+            for (int g = 0; g < 4; ++g) Ud[(q + 4 * g) * LD + c16] = Un[g];
             __syncthreads();
         }
     });

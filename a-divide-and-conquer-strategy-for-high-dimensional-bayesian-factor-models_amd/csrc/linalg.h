@@ -450,6 +450,76 @@ __device__ __forceinline__ void chol_inv16_hook(const double *Sm, int o, double 
     double *urow = Ub + (o + r) * LDP + o + cg;
     urow[0] = R0 * ik; urow[4] = R1 * ik; urow[8] = R2 * ik; urow[12] = R3 * ik;
 }
+// U = L^{-1} (L L' = S) of a 16x16 SPD tile held in registers in the fp64 MFMA C/D layout (lane
+// (c16, q) holds S[q + 4g][c16] in element g; its upper triangle is read), returned in the same
+// layout, by 4 x 4 blocks with no LDS: block step b reads S_bb (10 readlanes), factors it and
+// forms M_b = L_bb^{-1} uniformly in every lane, then four fp64 MFMAs:
+//   P   = S_{.b} M_b'      panel L_{.b}       (A = M_b, B = block row b of S: element b, as held)
+//   V   = M_b W_{b.}       block row b of U   (W: the running I - sum L_{.j} U_{j.}, W_0 = I)
+//   S  -= P_m P_m'          Schur complement   (P_m: P on the rows below block b, else 0)
+//   W  -= P_m V
+// P's and V's element 0 is the A / B operand of the next product as it lands (lane (r, k) holds
+// P[r][k], lane (c, k) V[k][c]), so the per-block chain is readlanes -> 4 x 4 factor -> two
+// dependent MFMAs, four times, instead of 16 pivot round trips through LDS.  hook(b) runs once
+// block b's readlanes are issued (independent MFMAs into the chain's latency).  A non-positive
+// pivot gives NaN (rsqrt of a negative or zero number), which the caller's finite check reports
+// as the reference's chol failure (dc:142).
+template <class Hook>
+__device__ __forceinline__ d4 chol_inv16_blk(d4 S, int lane, Hook &&hook) {
+    const int c16 = lane & 15, q = lane >> 4;
+    d4 W, U;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        W[g] = (q + 4 * g == c16) ? 1.0 : 0.0;
+        U[g] = 0.0;
+    }
+    const d4 zero = {0.0, 0.0, 0.0, 0.0};
+    static_for<4>([&](auto BC) {
+        constexpr int b = decltype(BC)::value, o = 4 * b;
+        // S_bb[m][n] (m <= n) = S[o + m][o + n]: lane 16 m + o + n, element b
+        const double s00 = readlane_d(S[b], o), s01 = readlane_d(S[b], o + 1);
+        const double s02 = readlane_d(S[b], o + 2), s03 = readlane_d(S[b], o + 3);
+        const double s11 = readlane_d(S[b], 16 + o + 1), s12 = readlane_d(S[b], 16 + o + 2);
+        const double s13 = readlane_d(S[b], 16 + o + 3), s22 = readlane_d(S[b], 32 + o + 2);
+        const double s23 = readlane_d(S[b], 32 + o + 3), s33 = readlane_d(S[b], 48 + o + 3);
+        hook(std::integral_constant<int, b>{});
+        const double i0 = rsqrt_f64(s00);
+        const double l10 = s01 * i0, l20 = s02 * i0, l30 = s03 * i0;
+        const double i1 = rsqrt_f64(fma(-l10, l10, s11));
+        const double l21 = fma(-l20, l10, s12) * i1, l31 = fma(-l30, l10, s13) * i1;
+        const double i2 = rsqrt_f64(fma(-l21, l21, fma(-l20, l20, s22)));
+        const double l32 = fma(-l31, l21, fma(-l30, l20, s23)) * i2;
+        const double i3 = rsqrt_f64(fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, s33))));
+        const double m10 = -(l10 * i0) * i1;
+        const double m21 = -(l21 * i1) * i2;
+        const double m20 = -fma(l21, m10, l20 * i0) * i2;
+        const double m32 = -(l32 * i2) * i3;
+        const double m31 = -fma(l32, m21, l31 * i1) * i3;
+        const double m30 = -fma(l32, m20, fma(l31, m10, l30 * i0)) * i3;
+        // A operand: lane (k = c16, m = q) = lane 16 m + k holds M_b[k][m] (rows k >= 4 zero); one
+        // select per entry on a constant lane (a nested choice by c16 and q compiled to branches)
+        double a = lane == 0 ? i0 : 0.0;
+        a = lane == 1 ? m10 : a;
+        a = lane == 17 ? i1 : a;
+        a = lane == 2 ? m20 : a;
+        a = lane == 18 ? m21 : a;
+        a = lane == 34 ? i2 : a;
+        a = lane == 3 ? m30 : a;
+        a = lane == 19 ? m31 : a;
+        a = lane == 35 ? m32 : a;
+        a = lane == 51 ? i3 : a;
+        const d4 P = mfma16x16x4(a, S[b], zero);
+        const d4 V = mfma16x16x4(a, W[b], zero);
+        U[b] = V[0];
+        if constexpr (b < 3) {
+            const double pm = (c16 >= o + 4) ? P[0] : 0.0;
+            S = mfma16x16x4(-pm, pm, S);
+            W = mfma16x16x4(-pm, V[0], W);
+        }
+    });
+    return U;
+}
+
 __device__ __forceinline__ void chol_inv16(const double (*Sm)[KP + 1], int o, double (*Ub)[KP + 1],
                                            double *lds_l, double *lds_u, int lane) {
     chol_inv16_p<KP + 1>(&Sm[0][0], o, &Ub[0][0], lds_l, lds_u, lane);
