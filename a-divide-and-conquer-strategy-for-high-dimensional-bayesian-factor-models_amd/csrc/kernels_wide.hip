@@ -471,13 +471,15 @@ __global__ __launch_bounds__(64) void k_lambda_w(
         ein[1][r] = tl ? Gr[h] : 0.0;
         ein[2][r] = tl ? trr[h] : 0.0;
         ein[3][r] = tl ? cr[h] : 0.0;
-        ein[4][r] = tl ? (plam_src ? pr[h] : pr[h] * trr[h]) : 0.0;    // Plam_j (dc:176)
+        // Plam_j (dc:176); 1 in the padding: E_m is exactly zero there (X, Z padding zero), so
+        // ps_j E_m + diag(Plam_j) is the identity padding with no selects on K
+        ein[4][r] = tl ? (plam_src ? pr[h] : pr[h] * trr[h]) : 1.0;
         vb[r] = tl ? psj * cr[h] : 0.0;                                  // blam (dc:141)
     }
     __syncthreads();
-    // ---- Q_j tiles: ps_j eta2 + diag(Plam_j) (dc:141), identity padding.  Plam_j only meets
-    //      the diagonal tiles (a compile-time fact: an LDS read per element of every tile made
-    //      this a chain of 112 dependent LDS round trips)
+    // ---- Q_j tiles: ps_j eta2 + diag(Plam_j) (dc:141); the padding is the identity by construction
+    //      (ein[4] above).  Plam_j only meets the diagonal tiles (a compile-time fact: an LDS read per
+    //      element of every tile made this a chain of 112 dependent LDS round trips)
     double pl[NB][4];
     static_for<NB>([&](auto JC) {
         constexpr int J = decltype(JC)::value;
@@ -489,25 +491,10 @@ __global__ __launch_bounds__(64) void k_lambda_w(
         static_for<NB>([&](auto IC) {
             constexpr int I = decltype(IC)::value;
             if constexpr (I >= Kc) {
-                if (16 * I + 16 <= K) {                  // no padding in the tile: no selects
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        double val = psj * T[utix<NB>(Kc, I)][g];
-                        if constexpr (I == Kc) val = (q + 4 * g == c16) ? val + pl[Kc][g] : val;
-                        T[utix<NB>(Kc, I)][g] = val;
-                    }
-                    return;
-                }
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const int r = 16 * Kc + q + 4 * g, c = 16 * I + c16;
                     double val = psj * T[utix<NB>(Kc, I)][g];
-                    if constexpr (I == Kc) {
-                        if (r == c) val += pl[Kc][g];
-                        val = (r < K && c < K) ? val : (r == c ? 1.0 : 0.0);
-                    } else {
-                        val = (r < K && c < K) ? val : 0.0;
-                    }
+                    if constexpr (I == Kc) val = (q + 4 * g == c16) ? val + pl[Kc][g] : val;
                     T[utix<NB>(Kc, I)][g] = val;
                 }
             }
