@@ -381,7 +381,7 @@ template <int NB, int J, int Kc, int I>
 __device__ __forceinline__ void trail_tile(d4 *T) {
     constexpr int a = utix<NB>(J, Kc), b = utix<NB>(J, I), t = utix<NB>(Kc, I);
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) T[t] = mfma16x16x4(-T[a][s4], T[b][s4], T[t]);
+    for (int s4 = 0; s4 < 4; ++s4) T[t] = mfma16x16x4_na(T[a][s4], T[b][s4], T[t]);
 }
 
 // The trailing tiles of block column J but the next diagonal one, (Kc, I) with J < Kc <= I < NB in

@@ -154,8 +154,8 @@ __device__ __forceinline__ void resid_rows8(const Dims &d, const double *__restr
         for (int t = 0; t < NT; ++t) {
             const d2 xa = *reinterpret_cast<const d2 *>(xr + 8 * t);
             const d2 za = *reinterpret_cast<const d2 *>(zr + 8 * t);
-            acc = mfma16x16x4(-eta_of(d.sr, d.s1r, xa.x, za.x), lb[t].x, acc);
-            acc = mfma16x16x4(-eta_of(d.sr, d.s1r, xa.y, za.y), lb[t].y, acc);
+            acc = mfma16x16x4_na(eta_of(d.sr, d.s1r, xa.x, za.x), lb[t].x, acc);
+            acc = mfma16x16x4_na(eta_of(d.sr, d.s1r, xa.y, za.y), lb[t].y, acc);
         }
 #pragma unroll
         for (int v = 0; v < 4; ++v) ss = (i0 + q + 4 * v < d.n) ? fma(acc[v], acc[v], ss) : ss;   // data rows only

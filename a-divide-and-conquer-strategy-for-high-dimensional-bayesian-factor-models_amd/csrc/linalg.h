@@ -19,6 +19,11 @@ __device__ __forceinline__ d4 mfma16x16x4(double a, double b, d4 c) {
     // C/D: col = lane&15, row = (lane>>4) + 4*reg
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
+// the same product with A negated by the instruction's neg modifier (blgp bit 0 of an f64 MFMA on
+// gfx950: neg:[1,0,0]) -- bit for bit (-a) b + c, without a VALU sign flip of the operand
+__device__ __forceinline__ d4 mfma16x16x4_na(double a, double b, d4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 1);
+}
 
 __device__ __forceinline__ double readlane_d(double x, int l) {
     const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
@@ -129,6 +134,15 @@ __device__ __forceinline__ double rsqrt_f64(double x) {
         y = fma(0.5 * y, e, y);
     }
     return y;
+}
+
+// 1/sqrt(x): hardware estimate + one third-order (Halley-type) step y (1 + e/2 + 3e^2/8), e = 1 - x y^2
+// (6 operations instead of rsqrt_f64's 9).  Measured on gfx950 (tools/dev/rsq_acc.hip, 4M arguments over
+// 2^-100 .. 2^100): max relative error 0.624 x 2^-52, as rsqrt_f64 (0.622); the estimate alone 2^-24.2
+__device__ __forceinline__ double rsqrt_f64_h(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    const double e = fma(-x * y, y, 1.0);
+    return fma(y * e, fma(e, 0.375, 0.5), y);
 }
 
 // XCD-aware block remap (bijective): hardware deals consecutive block ids
@@ -483,13 +497,13 @@ __device__ __forceinline__ d4 chol_inv16_blk(d4 S, int lane, Hook &&hook) {
         const double s13 = readlane_d(S[b], 16 + o + 3), s22 = readlane_d(S[b], 32 + o + 2);
         const double s23 = readlane_d(S[b], 32 + o + 3), s33 = readlane_d(S[b], 48 + o + 3);
         hook(std::integral_constant<int, b>{});
-        const double i0 = rsqrt_f64(s00);
+        const double i0 = rsqrt_f64_h(s00);
         const double l10 = s01 * i0, l20 = s02 * i0, l30 = s03 * i0;
-        const double i1 = rsqrt_f64(fma(-l10, l10, s11));
+        const double i1 = rsqrt_f64_h(fma(-l10, l10, s11));
         const double l21 = fma(-l20, l10, s12) * i1, l31 = fma(-l30, l10, s13) * i1;
-        const double i2 = rsqrt_f64(fma(-l21, l21, fma(-l20, l20, s22)));
+        const double i2 = rsqrt_f64_h(fma(-l21, l21, fma(-l20, l20, s22)));
         const double l32 = fma(-l31, l21, fma(-l30, l20, s23)) * i2;
-        const double i3 = rsqrt_f64(fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, s33))));
+        const double i3 = rsqrt_f64_h(fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, s33))));
         const double m10 = -(l10 * i0) * i1;
         const double m21 = -(l21 * i1) * i2;
         const double m20 = -fma(l21, m10, l20 * i0) * i2;
@@ -513,8 +527,8 @@ __device__ __forceinline__ d4 chol_inv16_blk(d4 S, int lane, Hook &&hook) {
         U[b] = V[0];
         if constexpr (b < 3) {
             const double pm = (c16 >= o + 4) ? P[0] : 0.0;
-            S = mfma16x16x4(-pm, pm, S);
-            W = mfma16x16x4(-pm, V[0], W);
+            S = mfma16x16x4_na(pm, pm, S);
+            W = mfma16x16x4_na(pm, V[0], W);
         }
     });
     return U;
@@ -583,7 +597,7 @@ __device__ __forceinline__ void chol_inv32(double (*Sm)[KP + 1], double (*Us)[KP
 #pragma unroll
     for (int g = 0; g < 4; ++g) s22[g] = Sm[16 + q + 4 * g][16 + i];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) s22 = mfma16x16x4(-Wk[i][4 * s + q], Wk[i][4 * s + q], s22);
+    for (int s = 0; s < 4; ++s) s22 = mfma16x16x4_na(Wk[i][4 * s + q], Wk[i][4 * s + q], s22);
 #pragma unroll
     for (int g = 0; g < 4; ++g) Sm[16 + q + 4 * g][16 + i] = s22[g];
     __builtin_amdgcn_wave_barrier();
@@ -596,7 +610,7 @@ __device__ __forceinline__ void chol_inv32(double (*Sm)[KP + 1], double (*Us)[KP
     for (int s = 0; s < 4; ++s) x = mfma16x16x4(Wk[i][4 * s + q], Us[4 * s + q][i], x);
     d4 u21 = {0.0, 0.0, 0.0, 0.0};                       // U21 = -U22 X, X in C/D layout = B operand
 #pragma unroll
-    for (int g = 0; g < 4; ++g) u21 = mfma16x16x4(-Us[16 + i][16 + q + 4 * g], x[g], u21);
+    for (int g = 0; g < 4; ++g) u21 = mfma16x16x4_na(Us[16 + i][16 + q + 4 * g], x[g], u21);
 #pragma unroll
     for (int g = 0; g < 4; ++g) Us[16 + q + 4 * g][i] = u21[g];
     __builtin_amdgcn_wave_barrier();

@@ -111,7 +111,7 @@ __device__ __forceinline__ void trtri(const double *T, double *U, int nb) {
             const double *Uii = U + tix(I, I) * TSZ;
             d4 R = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int s = 0; s < 4; ++s) R = mfma16x16x4(-Uii[(4 * s + kq) * TLD + i], S[s], R);
+            for (int s = 0; s < 4; ++s) R = mfma16x16x4_na(Uii[(4 * s + kq) * TLD + i], S[s], R);
             double *Uij = U + tix(I, J) * TSZ;
 #pragma unroll
             for (int g = 0; g < 4; ++g) Uij[i * TLD + kq + 4 * g] = R[g];
