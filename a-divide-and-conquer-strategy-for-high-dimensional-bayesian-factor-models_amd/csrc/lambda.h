@@ -268,12 +268,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             q[c] = e.x;
             q[c + 1] = e.y;
         }
+        // the diagonal entry of this lane's row: selects on the lane, no branch per column (a
+        // conditional per column compiled to an exec-mask branch around an LDS store each)
+        double e_kk = 0.0;
 #pragma unroll
-        for (int c = 8 * b; c < nc; ++c)
-            if (c == l + 8 * b) {
-                if (grp == 0) Dg[c] = q[c];                // E_m[k][k] (the wave's, whatever the row)
-                q[c] += dg[b];
-            }
+        for (int c = 8 * b; c < nc; ++c) {
+            const bool dgl = c == l + 8 * b;
+            e_kk = dgl ? q[c] : e_kk;
+            q[c] = dgl ? q[c] + dg[b] : q[c];
+        }
+        if (grp == 0 && l + 8 * b < nc) Dg[l + 8 * b] = e_kk;   // E_m[k][k] (the wave's, whatever the row)
     });
     __builtin_amdgcn_wave_barrier();
     // image of column pair (0, 1) (overwrites E's staging: every read of it is above)
@@ -437,7 +441,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const d2 vv = *reinterpret_cast<const d2 *>(Vs + c - 1);
         const d2 iv = *reinterpret_cast<const d2 *>(Is + c - 1);
         const bool isc = l + 8 * cb == c, isc1 = l + 8 * cb == c - 1;
-        const double xa = (vv.y + z[cb] - pa) * iv.y;
+        double xa = (vv.y + z[cb] - pa) * iv.y;
+        asm volatile("" : "+v"(xa));      // formed in every lane: hipcc otherwise sinks it into an exec-mask branch
         x[cb] = isc ? xa : x[cb];
         const double t = isc ? qc[c - 1] * xa : 0.0;               // L[c][c-1] x_c
         const double tb = dpp8_d<0x101>(t);                        // row_shl:1: lane c%8 -> c%8 - 1
