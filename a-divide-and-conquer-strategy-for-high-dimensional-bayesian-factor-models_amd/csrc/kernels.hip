@@ -1270,14 +1270,16 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
 #pragma unroll
         for (int u = 0; u < NU; ++u) zv[u] = ld_agent(Zm + threadIdx.x + 256 * u);
     }
+    // each tile's X rows after its normals (tile 0's during the operators' staging, tile 1's at its
+    // own draw): held across the normals and tile 0's draw they spilled (12 VGPRs at waves_per_eu(3))
     d2 xv[MT][4], ev[MT][4];
-#pragma unroll
-    for (int a = 0; a < MT; ++a) {
+    auto load_x = [&](int a) {
         const double *Xi = b.X + (size_t)(i0 + 16 * a + c) * KP + 2 * q;
 #pragma unroll
         for (int t = 0; t < 4; ++t) xv[a][t] = *reinterpret_cast<const d2 *>(Xi + 8 * t);
-    }
+    };
     z_eps(d, dr, iter, mg, i0 + c, i0 + c < d.n, q, ev[0]);   // tile 1's after tile 0's draw (registers)
+    load_x(0);                                                  // in flight during the operators' staging
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
         const int e = threadIdx.x + 256 * u;
@@ -1290,7 +1292,10 @@ __device__ __forceinline__ void wpass_z_tile(const Dims &d, const Bufs &b, const
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
         const int i = i0 + 16 * a + c;
-        if (a > 0) z_eps(d, dr, iter, mg, i, i < d.n, q, ev[a]);
+        if (a > 0) {
+            load_x(a);
+            z_eps(d, dr, iter, mg, i, i < d.n, q, ev[a]);
+        }
         d2 wv[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
