@@ -314,22 +314,31 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
 }
 
 // ============================================================================
-// k_xdraw: X' = Tx S' + Ux eps' (S summed over ranks, canonical tree), one wave per
-// 16 rows.                                                                   dc:119-128
+// k_xdraw: X' = Tx S' + Ux eps' (S summed over ranks, canonical tree), one block of XD_WAVES waves per
+// 16 rows, the KW/16 output tiles dealt over the waves.  One wave per 16 rows issued all 8 tiles' 512
+// MFMAs on one SIMD behind 16 rounds of dependent L2 loads (c4: 125 waves on 1,024 SIMDs, 39 us);
+// every tile keeps its products and their order, so X keeps its bits.               dc:119-128
 // ============================================================================
+#ifndef DCFM_XD_WAVES
+#define DCFM_XD_WAVES 4
+#endif
+template <int KW> constexpr int xd_waves() { return KW / 16 < DCFM_XD_WAVES ? KW / 16 : DCFM_XD_WAVES; }
 template <int KW>
-__global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__ xall, const double *__restrict__ XM,
-                                              double *__restrict__ X, DrawsDev dr, int64_t iter) {
-    constexpr int MT = KW / 16;
-    const int lane = threadIdx.x, c = lane & 15, q = lane >> 4;
+__global__ __launch_bounds__(64 * xd_waves<KW>()) void k_xdraw(Dims d, const double *__restrict__ xall, const double *__restrict__ XM,
+                                                         double *__restrict__ X, DrawsDev dr, int64_t iter) {
+    constexpr int MT = KW / 16, MPW = MT / xd_waves<KW>();   // output tiles per wave
+    static_assert(MT % xd_waves<KW>() == 0, "whole tiles per wave");
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int c = lane & 15, q = lane >> 4;
     const int i = blockIdx.x * 16 + c;
     const bool live = i < d.n;
     const size_t stride = (size_t)d.NP * KW;
     const double *Tx = XM, *Ux = XM + KW * KW;
     const double *nx = dr.NX + ((size_t)(iter - dr.first_iter) * d.n + (live ? i : 0)) * d.K;
-    d4 ax[MT];
+    d4 ax[MPW];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) ax[mt] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int u = 0; u < MPW; ++u) ax[u] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
     for (int t = 0; t < KW / 8; ++t) {
         const int kk = 8 * t + 2 * q;
         TreeSum<d2> ts;                                  // the ranks' message sums, canonical tree
@@ -337,24 +346,25 @@ __global__ __launch_bounds__(64) void k_xdraw(Dims d, const double *__restrict__
         const d2 sv = ts.total();
         const d2 ev = row_normals(d, nx, live, SITE_X, 0, i, kk, iter);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
+        for (int u = 0; u < MPW; ++u) {
+            const int mt = wave * MPW + u;
             const size_t o = (size_t)(16 * mt + c) * KW + kk;
             const d2 a1 = *reinterpret_cast<const d2 *>(Tx + o);
             const d2 a2 = *reinterpret_cast<const d2 *>(Ux + o);
-            ax[mt] = mfma16x16x4(a1.x, sv.x, ax[mt]);
-            ax[mt] = mfma16x16x4(a2.x, ev.x, ax[mt]);
-            ax[mt] = mfma16x16x4(a1.y, sv.y, ax[mt]);
-            ax[mt] = mfma16x16x4(a2.y, ev.y, ax[mt]);
+            ax[u] = mfma16x16x4(a1.x, sv.x, ax[u]);
+            ax[u] = mfma16x16x4(a2.x, ev.x, ax[u]);
+            ax[u] = mfma16x16x4(a1.y, sv.y, ax[u]);
+            ax[u] = mfma16x16x4(a2.y, ev.y, ax[u]);
         }
     }
     if (!live) return;
     double *Xr = X + (size_t)i * KW;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int u = 0; u < MPW; ++u)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            const int k = 16 * mt + q + 4 * g;
-            Xr[k] = (k < d.K) ? ax[mt][g] : 0.0;
+            const int k = 16 * (wave * MPW + u) + q + 4 * g;
+            Xr[k] = (k < d.K) ? ax[u][g] : 0.0;
         }
 }
 
@@ -838,8 +848,8 @@ void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter
                                            b.ZM, b.X, b.Z, b.Sp, dr, iter));
 }
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
-    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_xdraw<KW>, dim3(cdiv(d.n, 16)), dim3(64), 0, s, d, b.xall, b.XM, b.X,
-                                           dr, iter));
+    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_xdraw<KW>, dim3(cdiv(d.n, 16)), dim3(64 * xd_waves<KW>()), 0, s, d, b.xall, b.XM,
+                                           b.X, dr, iter));
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *tau_cur,
                    const double *plam_src, hipStream_t s, double kappa_max) {
