@@ -186,7 +186,10 @@ __device__ __forceinline__ d2 row_normals(const Dims &d, const double *inj, bool
 #define DCFM_ZD_RT 4
 #endif
 constexpr int ZD_RT = DCFM_ZD_RT;   // 16-row tiles per block: the A operands (A_m, M1, U) serve 4 (c4: 138 -> 81 us vs 1)
-template <int KW>
+// TK = ceil(K / 8) (a template argument, so the k loops keep their unrolling): the k-steps past K add exact
+// zeros (A_m, M1, U zero across the live / padding boundary; X, V, eps, Z zero in the padding) and are not
+// issued -- c4: 13 of 16 eight-wide and 26 of 32 four-wide steps; the same values
+template <int KW, int TK = KW / 8>
 __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict__ W, const double *__restrict__ A,
                                                const double *__restrict__ ZM, const double *__restrict__ X,
                                                double *__restrict__ Z, double *__restrict__ Sp, DrawsDev dr,
@@ -219,7 +222,7 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
 #pragma unroll
         for (int u = 0; u < MW; ++u) av[h][u] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 2
-    for (int t = 0; t < KW / 8; ++t) {
+    for (int t = 0; t < TK; ++t) {
         const int kk = 8 * t + 2 * q;
         d2 xv[RT];
 #pragma unroll
@@ -253,7 +256,7 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
         for (int u = 0; u < MW; ++u) az[h][u] = d4{0.0, 0.0, 0.0, 0.0};
     const size_t nzb = ((size_t)(iter - dr.first_iter) * d.g + mg) * d.n;
 #pragma unroll 2
-    for (int t = 0; t < KW / 4; ++t) {
+    for (int t = 0; t < 2 * TK; ++t) {
         const int kk = 4 * t + q;
         double vb[RT], e[RT];
 #pragma unroll
@@ -286,7 +289,7 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
 #pragma unroll
         for (int u = 0; u < MW; ++u) as[h][u] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 2
-    for (int t = 0; t < KW / 4; ++t) {
+    for (int t = 0; t < 2 * TK; ++t) {
         const int kk = 4 * t + q;
         double zb[RT];
 #pragma unroll
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(256) void k_zdraw(Dims d, const double *__restrict_
 #define DCFM_XD_WAVES 4
 #endif
 template <int KW> constexpr int xd_waves() { return KW / 16 < DCFM_XD_WAVES ? KW / 16 : DCFM_XD_WAVES; }
-template <int KW>
+template <int KW, int TK = KW / 8>   // TK = ceil(K / 8): as k_zdraw
 __global__ __launch_bounds__(64 * xd_waves<KW>()) void k_xdraw(Dims d, const double *__restrict__ xall, const double *__restrict__ XM,
                                                          double *__restrict__ X, DrawsDev dr, int64_t iter) {
     constexpr int MT = KW / 16, MPW = MT / xd_waves<KW>();   // output tiles per wave
@@ -339,7 +342,7 @@ __global__ __launch_bounds__(64 * xd_waves<KW>()) void k_xdraw(Dims d, const dou
 #pragma unroll
     for (int u = 0; u < MPW; ++u) ax[u] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
-    for (int t = 0; t < KW / 8; ++t) {
+    for (int t = 0; t < TK; ++t) {
         const int kk = 8 * t + 2 * q;
         TreeSum<d2> ts;                                  // the ranks' message sums, canonical tree
         for (int rk = 0; rk < d.nranks; ++rk) ts.push(*reinterpret_cast<const d2 *>(xall + rk * stride + (size_t)i * KW + kk));
@@ -843,13 +846,26 @@ void launch_xchol(const Dims &d, const Bufs &b, hipStream_t s) {
     WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_xchol<KW>, dim3(1), dim3(TILE_THREADS), 0, s, d,
                                            d.coll ? b.xa_all : b.xa, b.XM));
 }
+// f(std::integral_constant<int, ceil(K / 8)>) for the wide widths (KW = 64: 5..8, KW = 128: 9..16)
+template <int KW, class F, int... I>
+static void dispatch_tk_impl(int tk, F &&f, std::integer_sequence<int, I...>) {
+    ((tk == KW / 16 + 1 + I ? (f(std::integral_constant<int, KW / 16 + 1 + I>{}), 0) : 0), ...);
+}
+template <int KW, class F>
+static void dispatch_tk(int K, F &&f) {   // tk in KW / 16 + 1 .. KW / 8
+    dispatch_tk_impl<KW>((K + 7) / 8, f, std::make_integer_sequence<int, KW / 16>{});
+}
 void launch_zdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
-    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_zdraw<KW>, dim3((d.NP / (16 * ZD_RT)) * d.G), dim3(256), 0, s, d, b.W, b.A,
-                                           b.ZM, b.X, b.Z, b.Sp, dr, iter));
+    WIDE_DISPATCH(d.kp, dispatch_tk<KW>(d.K, [&](auto T) {
+        hipLaunchKernelGGL((k_zdraw<KW, decltype(T)::value>), dim3((d.NP / (16 * ZD_RT)) * d.G), dim3(256), 0, s, d, b.W,
+                           b.A, b.ZM, b.X, b.Z, b.Sp, dr, iter);
+    }));
 }
 void launch_xdraw(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, hipStream_t s) {
-    WIDE_DISPATCH(d.kp, hipLaunchKernelGGL(k_xdraw<KW>, dim3(cdiv(d.n, 16)), dim3(64 * xd_waves<KW>()), 0, s, d, b.xall, b.XM,
-                                           b.X, dr, iter));
+    WIDE_DISPATCH(d.kp, dispatch_tk<KW>(d.K, [&](auto T) {
+        hipLaunchKernelGGL((k_xdraw<KW, decltype(T)::value>), dim3(cdiv(d.n, 16)), dim3(64 * xd_waves<KW>()), 0, s, d,
+                           b.xall, b.XM, b.X, dr, iter);
+    }));
 }
 void launch_lambda(const Dims &d, const Bufs &b, const DrawsDev &dr, int64_t iter, const double *tau_cur,
                    const double *plam_src, hipStream_t s, double kappa_max) {
