@@ -213,6 +213,12 @@ __global__ __launch_bounds__(256) void k_prep(Dims d, const double *__restrict__
 #define DCFM_WP_RING 3
 #endif
 constexpr int WP_RING = DCFM_WP_RING;   // W pass register ring depth (chunks)
+#ifndef DCFM_WP_RING_WIDE
+#define DCFM_WP_RING_WIDE 4
+#endif
+// the wide layouts' pass (k_wpass<64 / 128>: 2 waves per SIMD at c4) takes one chunk more in flight
+// (c4: 152 -> 127 us; ab_rg in profiles/r06_ab_summary.txt); the same products in the same order
+constexpr int WP_RING_WIDE = DCFM_WP_RING_WIDE;
 // ============================================================================
 // k_wpass: W_m[i][k] = sum_j Y_m[i][j] (w_j Lambda_m[j][k])   fp64 MFMA, Y pass 1
 // one wave = (shard m, 16 MT rows i = MT M-tiles) x 32 k (even / odd k tiles) of
@@ -231,7 +237,7 @@ constexpr int WP_RING = DCFM_WP_RING;   // W pass register ring depth (chunks)
 // Register ring of R chunks: chunk t + R - 1 is requested while chunk t multiplies, so R - 1
 // chunks are in flight behind the MFMAs.  pre() runs once the first R - 1 chunks' loads are
 // issued (VALU work hidden behind their latency).
-template <int KW, int MT, int R = WP_RING, class Pre>
+template <int KW, int MT, int R = (KW > KP ? WP_RING_WIDE : WP_RING), class Pre>
 __device__ __forceinline__ void wpass_acc(const Dims &d, const double *__restrict__ Y, const double *__restrict__ Lam,
                                           const double *__restrict__ omega, int m, int i0, int kt, d4 (&acc)[MT][2],
                                           Pre &&pre) {
