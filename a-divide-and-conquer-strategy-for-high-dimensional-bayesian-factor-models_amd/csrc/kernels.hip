@@ -887,7 +887,9 @@ __global__ __launch_bounds__(1024) void k_xdraw(Dims d, const double *__restrict
 // IS_E: the A operand is eta itself, columns te*32.. (Yp = nullptr; Xa/Za point at
 // them); SAME_T: te == kt, so the A operand is the B operand (no extra loads).
 // PS: the block computes only the k columns of parity par (acc[.][0]); same per-element order
-template <int KW, bool IS_E, bool SAME_T, bool PS = false>
+// ETA (wide): Xp / Xa point at eta itself (formed once per iteration by k_eta into the free W buffer,
+// with the same eta_of), Zp / Za unused: one load per operand instead of two
+template <int KW, bool IS_E, bool SAME_T, bool PS = false, bool ETA = false>
 __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restrict__ Yp,
                                            const double *__restrict__ Xp,
                                            const double *__restrict__ Zp,
@@ -901,22 +903,26 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
         for (int u = 0; u < 4; ++u) {
             const int i = 4 * (s + u) + q;
             x[u] = *reinterpret_cast<const d2 *>(Xp + (size_t)i * KW);
-            z[u] = *reinterpret_cast<const d2 *>(Zp + (size_t)i * KW);
+            if (!ETA) z[u] = *reinterpret_cast<const d2 *>(Zp + (size_t)i * KW);
             if (!IS_E) {
                 y[u] = *reinterpret_cast<const d2 *>(Yp + (size_t)i * d.PP);
             } else if (EXTRA) {   // eta of tile te, formed into y
                 const d2 xa = *reinterpret_cast<const d2 *>(Xa + (size_t)i * KW);
-                const d2 za = *reinterpret_cast<const d2 *>(Za + (size_t)i * KW);
-                y[u].x = eta_of(d.sr, d.s1r, xa.x, za.x);
-                y[u].y = eta_of(d.sr, d.s1r, xa.y, za.y);
+                if (ETA) {
+                    y[u] = xa;
+                } else {
+                    const d2 za = *reinterpret_cast<const d2 *>(Za + (size_t)i * KW);
+                    y[u].x = eta_of(d.sr, d.s1r, xa.x, za.x);
+                    y[u].y = eta_of(d.sr, d.s1r, xa.y, za.y);
+                }
             }
         }
     };
     auto mma = [&](d2 (&y)[4], d2 (&x)[4], d2 (&z)[4]) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const double e0 = eta_of(d.sr, d.s1r, x[u].x, z[u].x);
-            const double e1 = eta_of(d.sr, d.s1r, x[u].y, z[u].y);
+            const double e0 = ETA ? x[u].x : eta_of(d.sr, d.s1r, x[u].x, z[u].x);
+            const double e1 = ETA ? x[u].y : eta_of(d.sr, d.s1r, x[u].y, z[u].y);
             const double a0 = (IS_E && SAME_T) ? e0 : y[u].x, a1 = (IS_E && SAME_T) ? e1 : y[u].y;
             if constexpr (PS) {
                 const double ep = par ? e1 : e0;
@@ -941,6 +947,9 @@ __device__ __forceinline__ void cpass_wave(const Dims &d, const double *__restri
 }
 
 template <int KW> constexpr int cp_waves() { return 4; }
+#ifndef DCFM_WIDE_ETA
+#define DCFM_WIDE_ETA 1
+#endif
 // PS (K <= 32, where the launch would leave CUs idle): each block computes one parity of its
 // 32 k columns (twice the blocks, the pair adjacent: Y from L2); per-element order unchanged
 // ndel > 0 (fused K <= 32 chain): the last ndel blocks run the previous iteration's delta / tau
@@ -979,9 +988,12 @@ __global__ __launch_bounds__(64 * cp_waves<KW>()) __attribute__((amdgpu_waves_pe
     const int te = isE ? (c0 - d.PP) >> 5 : 0;
     const int r = lane & 15, q = lane >> 4;
     const double *Yp = Y + (size_t)m * d.NP * d.PP + c0 + 2 * r;
-    const double *Xp = X + 32 * kt + 2 * r;
+    // wide: X is eta [G][NP][KW] (k_eta, launch_cpass), so the shard's rows
+    constexpr bool ETA = KW > KP && DCFM_WIDE_ETA;
+    const double *Xs = ETA ? X + (size_t)m * d.NP * KW : X;
+    const double *Xp = Xs + 32 * kt + 2 * r;
     const double *Zp = Z + (size_t)m * d.NP * KW + 32 * kt + 2 * r;
-    const double *Xa = X + 32 * te + 2 * r;
+    const double *Xa = Xs + 32 * te + 2 * r;
     const double *Za = Z + (size_t)m * d.NP * KW + 32 * te + 2 * r;
     const int nsw = d.NP / (4 * NWV);          // k-steps (4 rows each) per wave
     d4 acc[2][2];
@@ -989,9 +1001,9 @@ __global__ __launch_bounds__(64 * cp_waves<KW>()) __attribute__((amdgpu_waves_pe
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
-    if (!isE) cpass_wave<KW, false, false, PS>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc, par);
-    else if (te == kt) cpass_wave<KW, true, true, PS>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc, par);
-    else cpass_wave<KW, true, false, PS>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc, par);
+    if (!isE) cpass_wave<KW, false, false, PS, ETA>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc, par);
+    else if (te == kt) cpass_wave<KW, true, true, PS, ETA>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc, par);
+    else cpass_wave<KW, true, false, PS, ETA>(d, Yp, Xp, Zp, Xa, Za, wave * nsw, nsw, q, acc, par);
     // D row rho = q + 4g -> column c0 + 2 rho + ta;  D col r -> k = 2r + tb
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -1807,11 +1819,17 @@ void launch_cpass(const Dims &d, const Bufs &b, hipStream_t s, const DrawsDev &d
             hipLaunchKernelGGL((k_cpass<32, false>), dim3(grid.x + ndel), dim3(64 * cp_waves<32>()), 0, s, d, b.Y, b.X,
                                b.Z, b.C, b.E, dr, b.sall, da, ndel);
         break;
+    // wide: eta formed once (k_eta into W, free after k_zdraw) instead of in each of the shard's column
+    // tiles from X and Z: their two 2 MB panels shared the XCD's L2 with the Y stream (c4: 358 MB)
     case 64:
-        hipLaunchKernelGGL(k_cpass<64>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E, dr, b.sall, da, 0);
+        if (DCFM_WIDE_ETA) launch_eta(d, b, b.W, s);
+        hipLaunchKernelGGL(k_cpass<64>, grid, dim3(256), 0, s, d, b.Y, DCFM_WIDE_ETA ? b.W : b.X, b.Z, b.C, b.E, dr,
+                           b.sall, da, 0);
         break;
     default:
-        hipLaunchKernelGGL(k_cpass<128>, grid, dim3(256), 0, s, d, b.Y, b.X, b.Z, b.C, b.E, dr, b.sall, da, 0);
+        if (DCFM_WIDE_ETA) launch_eta(d, b, b.W, s);
+        hipLaunchKernelGGL(k_cpass<128>, grid, dim3(256), 0, s, d, b.Y, DCFM_WIDE_ETA ? b.W : b.X, b.Z, b.C, b.E, dr,
+                           b.sall, da, 0);
         break;
     }
 }
