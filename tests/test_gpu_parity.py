@@ -37,6 +37,11 @@ CASES = {
     "K64_full64": (70, 128, 2, 64, 0, 2, 1),
     "K100_c4_shape": (120, 200, 2, 100, 0, 2, 1),           # c4's truncation (BASELINE configs[3])
     "K128_max": (150, 256, 2, 128, 0, 2, 1),
+    # the wide draws' k loops are instantiated per ceil(K / 8) (kernels_wide.hip dispatch_tk): a few more
+    # of those instantiations, and k_lambda_w's NB = 4 / 5 / 8
+    "K50_tk7": (80, 150, 3, 50, 0, 2, 1),
+    "K70_tk9": (100, 180, 2, 70, 0, 2, 1),
+    "K118_tk15": (400, 240, 2, 118, 0, 2, 1),              # n = 150 is ill-conditioned (the two CPU oracles differ by 2e-9)
     "many_shards_wide": (50, 480, 12, 40, 0, 2, 1),
 }
 
